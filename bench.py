@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Benchmark: raft groups quorum-evaluated per second on MI355X.
+
+Workload (BASELINE.json configs[1]): 1M (2^20) raft groups x 5 voters per GPU,
+CommittedIndex + VoteResult fused in one kernel, uint64 match indexes, FIXED
+slot-major SoA layout.  One step = one pass of the hot path over one batch
+of 2^20 groups.  ``--batches`` distinct batches (default 16, ~0.96 GB with
+outputs) stay resident in HBM and are visited round-robin, so every step
+streams its batch from HBM instead of the 256 MB Infinity Cache (the
+MALL-warm single-batch rate is reported beside it as ``value_mall_warm``).
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL), groups sharded by
+global group number (weak scaling, no collective in the timed region); for
+N > 1 the node-wide all-gather of one batch's commit/vote vectors is timed
+separately (``allgather_ms``).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from etcd_amd import _lib  # noqa: E402
+from etcd_amd.quorum import batch  # noqa: E402
+
+METRIC = "raft groups quorum-evaluated/sec (1 and 8 GPUs) + % peak HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 0x5EED0002      # 0x5EED0001 + config#
+
+
+def bytes_per_group(n: int) -> int:
+    """Algorithmic bytes of the fused kernel per group:
+    read match 8n + voted + granted masks, write commit 8 + vote 1."""
+    mb = 1 if n <= 8 else 2
+    return 8 * n + 2 * mb + 8 + 1
+
+
+class HipEvents:
+    """Raw hipEvent timing on an arbitrary stream (the stream the kernels are
+    launched on); ~1 us of host time per record."""
+
+    def __init__(self, count: int):
+        self.hip = C.CDLL("libamdhip64.so")
+        self.hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+        self.hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+        self.hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [C.c_void_p]
+        self.ev = []
+        for _ in range(count):
+            e = C.c_void_p()
+            assert self.hip.hipEventCreate(C.byref(e)) == 0
+            self.ev.append(e)
+        self.record = self.hip.hipEventRecord
+
+    def elapsed_ms(self, a: int, b: int) -> float:
+        ms = C.c_float()
+        assert self.hip.hipEventElapsedTime(C.byref(ms), self.ev[a], self.ev[b]) == 0
+        return ms.value
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+
+
+def load_traffic(workload_key: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (written by
+    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this
+    same bench command, with the gfx950 FETCH_SIZE x2 correction)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(n: int, sample_groups: int, seconds: float):
+    """The oracle's faithful C restatement of the Go loop (per-group hash-map
+    MajorityConfig + AckedIndexer lookups + insertionSort, majority.go:126-210)
+    timed on the host cores over a bounded sample of the same workload."""
+    from tests import oracle_c as oc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    match, vd, gr, _ = oc.gen_fixed(SEED, n, sample_groups)
+    maps = oc.faithful_maps(n, match, vd, gr)
+
+    def rate(th):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oc.faithful_eval(maps, sample_groups, threads=th)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                return reps * sample_groups / dt, reps
+
+    r1, reps1 = rate(1)
+    rn, repsn = rate(threads)
+    return {
+        "value": rn, "unit": "groups/s", "cores": threads, "kind": "port",
+        "sample": (f"{sample_groups} groups x {n} voters (same synthetic spec), faithful C "
+                   f"restatement of majority.go CommittedIndex+VoteResult with Go-map-style "
+                   f"hash lookups; {repsn} passes on {threads} threads (GOMAXPROCS-equivalent "
+                   f"{threads}); 1 thread: {r1:.4g} groups/s over {reps1} passes"),
+        "value_1thread": r1,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
+    ap.add_argument("--voters", type=int, default=5)
+    ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, G, B, K, W = args.voters, args.groups, max(1, args.batches), args.steps, args.warmup
+    lib = _lib.load()
+    fn = lib.qb_dev_fixed_committed_vote
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    # B resident batches; global group numbers shard by rank (weak scaling)
+    groups = [batch.FixedGroups.synth(SEED, n, G, g_begin=(rank * B + b) * G, device=dev)
+              for b in range(B)]
+    outs = [(torch.empty(G, dtype=torch.int64, device=dev),
+             torch.empty(G, dtype=torch.uint8, device=dev)) for _ in range(B)]
+    call_args = [(n, G, g.match.data_ptr(), g.voted.data_ptr(), g.granted.data_ptr(),
+                  c.data_ptr(), v.data_ptr(), sp) for g, (c, v) in zip(groups, outs)]
+    torch.cuda.synchronize()
+
+    def launch(k):
+        rc = fn(*call_args[k % B])
+        if rc:
+            _lib.check(rc, "qb_dev_fixed_committed_vote")
+
+    for k in range(W):
+        launch(k)
+    ev = HipEvents(2 * K + 2)
+    rec = ev.record
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(K):
+        rec(ev.ev[2 * k], sp)
+        launch(k)
+        rec(ev.ev[2 * k + 1], sp)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    kern_ms = [ev.elapsed_ms(2 * k, 2 * k + 1) for k in range(K)]
+    ev.close()
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+
+    # MALL-warm single-batch rate (informational)
+    for _ in range(W):
+        launch(0)
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    for _ in range(K):
+        launch(0)
+    torch.cuda.synchronize()
+    warm_elapsed = time.perf_counter() - tw
+
+    allgather_ms = None
+    if world > 1:
+        t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, warm_elapsed, avg_kernel_s = (float(x) for x in t.tolist())
+        # node-wide result: all-gather one batch's commit (u64) and vote (u8) vectors
+        c, v = outs[0]
+        call = torch.empty(world * G, dtype=torch.int64, device=dev)
+        vall = torch.empty(world * G, dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(call, c)
+            dist.all_gather_into_tensor(vall, v)
+        barrier()
+        ta = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            dist.all_gather_into_tensor(call, c)
+            dist.all_gather_into_tensor(vall, v)
+        barrier()
+        allgather_ms = (time.perf_counter() - ta) / reps * 1e3
+
+    if rank == 0:
+        total_groups = world * G * K
+        value = total_groups / elapsed
+        bpg = bytes_per_group(n)
+        achieved = bpg * G / avg_kernel_s / 1e9
+        key = f"fixed_n{n}_G{G}"
+        traffic = load_traffic(key)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "groups/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (counter-based splitmix64 spec, SURVEY.md §8d; HBM-resident)",
+            "config": {
+                "workload": "BASELINE configs[1]: 1M groups x 5 voters CommittedIndex + "
+                            "VoteResult, uint64 indexes, one MI355X per shard",
+                "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA",
+                "batches_resident": B, "parallelism": f"groups sharded by id over {world} GPU(s)",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": f"k_fixed<{n},4,true,true>",
+                "bytes_per_group": bpg,
+                "avg_kernel_us": avg_kernel_s * 1e6,
+            },
+            "value_mall_warm": world * G * K / warm_elapsed,
+            "allgather_ms": allgather_ms,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+"""etcd_amd — MI355X-native batched quorum engine for etcd's raft hot path.
+
+Scope (BASELINE.json north_star): raft/quorum CommittedIndex /
+VoteResult (majority and joint), and the quorum-facing part of raft/tracker
+(MsgAppResp MaybeUpdate scatter-max, commit advance with the term gate,
+QuorumActive), evaluated for millions of independent raft groups at once on
+HIP kernels (etcd_amd/csrc) behind the C ABI in include/quorum_batch.h.
+"""
+from ._lib import QuorumBatchError, load  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,87 @@
+"""ctypes binding of libquorumbatch.so (the C ABI in include/quorum_batch.h).
+
+The library is built in-tree (``make -C etcd_amd/csrc`` or
+``__graft_entry__.build()``).  There is no fallback: if the shared object is
+missing every product entry point raises ``QuorumBatchError`` — the batch
+engine never silently computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libquorumbatch.so")
+
+QB_OK = 0
+QB_EINVAL = -1
+QB_EHIP = -2
+QB_ENOMEM = -3
+
+QB_MAX_SLOTS = 16
+QB_REC_REJECT = 0x80
+QB_STAT_NAMES = ("applied", "rejected", "stale_term", "non_member", "higher_term",
+                 "bad_group", "after_stepdown")
+QB_STAT_COUNT = 8
+
+
+class QuorumBatchError(RuntimeError):
+    pass
+
+
+_u64, _u32, _i32, _p, _u64p = C.c_uint64, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p
+
+# name -> (restype, argtypes); must list exactly the functions the header declares.
+SIGNATURES = {
+    "qb_abi_version": (_i32, []),
+    "qb_last_error": (C.c_char_p, []),
+    "qb_device_count": (_i32, []),
+    "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
+    "qb_dev_csr_committed_vote": (_i32, [_u64, _p, _p, _p, _p, _p, _p, _p]),
+    "qb_dev_csr_validate": (_i32, [_u64, _p, _p, _p]),
+    "qb_dev_csr_quorum_active": (_i32, [_u64, _p, _p, _p, _p]),
+    "qb_dev_fixed_apply_appresp": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                          _p, _p, _p]),
+    "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
+    "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
+    "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
+    "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),
+    "qb_dev_synth_csr": (_i32, [_u64, _i32, _u64, _u64, _p, _p, _p, _p, _p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> C.CDLL:
+    """Load (once) and type the library; raises QuorumBatchError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise QuorumBatchError(
+                f"{LIB_PATH} not built: run `make -C etcd_amd/csrc` (or "
+                "__graft_entry__.build()); there is no CPU fallback")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.qb_abi_version() != 1:
+            raise QuorumBatchError("libquorumbatch ABI version mismatch")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != QB_OK:
+        msg = load().qb_last_error().decode(errors="replace")
+        raise QuorumBatchError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,110 @@
+// qb_common.h — shared device/host helpers for libquorumbatch (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "qb_networks.h"
+#include "quorum_batch.h"
+
+namespace qb {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = unsigned long long;  // HIP atomics are declared on unsigned long long
+static_assert(sizeof(u64) == 8, "u64");
+
+constexpr u64 kInf = ~0ull;  // quorum.Index MaxUint64 (quorum.go:25-30)
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// ---------------------------------------------------------------- errors ---
+void set_error(const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+
+#define QB_CHECK_LAUNCH(what)                                     \
+  do {                                                            \
+    hipError_t e_ = hipGetLastError();                            \
+    if (e_ != hipSuccess) return ::qb::hip_fail(e_, what);        \
+  } while (0)
+
+#define QB_REQUIRE(cond, ...)          \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::qb::set_error(__VA_ARGS__);    \
+      return QB_EINVAL;                \
+    }                                  \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------ counter-based RNG ---
+// r(g, slot, field) = splitmix64(seed ^ (g << 12 | slot << 4 | field)).
+// The same function lives in the C oracle (oracle/quorum_oracle.c) as an
+// independent restatement of the spec in SURVEY.md §8d.
+__host__ __device__ __forceinline__ u64 splitmix64(u64 x) {
+  u64 z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ u64 rnd(u64 seed, u64 g, u32 slot, u32 field) {
+  return splitmix64(seed ^ ((g << 12) | (u64(slot) << 4) | field));
+}
+enum Field : u32 {
+  F_LAST = 0, F_HIGH = 1, F_HIGHBITS = 2, F_ABSENT = 3, F_LAG = 4, F_VOTE = 5,
+  F_TERMSTART = 6, F_N = 7, F_L = 8, F_LPOS = 9, F_OVERLAP = 10, F_ROT = 11,
+};
+
+// ------------------------------------------------- compare-exchange nets ---
+// Unsigned 64-bit compare over the full range (quorum.Index is uint64).
+__device__ __forceinline__ void cmpx(u64& a, u64& b) {
+  const bool sw = b < a;
+  const u64 lo = sw ? b : a;
+  const u64 hi = sw ? a : b;
+  a = lo;
+  b = hi;
+}
+
+template <class Net, int... K>
+__device__ __forceinline__ void run_net(u64* v, std::integer_sequence<int, K...>) {
+  ((cmpx(v[Net::A[K]], v[Net::B[K]])), ...);
+}
+
+// q-th largest of N values = ascending srt[N - (N/2+1)] (majority.go:165-171),
+// via the pruned selection network.
+template <int N>
+__device__ __forceinline__ u64 select_quorum(u64 (&v)[N]) {
+  run_net<SelNet<N>>(v, std::make_integer_sequence<int, SelNet<N>::K>{});
+  return v[SelNet<N>::POS];
+}
+
+template <int W>
+__device__ __forceinline__ void sort_net(u64 (&v)[W]) {
+  run_net<SortNet<W>>(v, std::make_integer_sequence<int, SortNet<W>::K>{});
+}
+
+// majority.go:178-210 given popcounts over the config's members.
+__host__ __device__ __forceinline__ u8 vote_from_counts(int n, int yes, int voted) {
+  if (n == 0) return QB_VOTE_WON;
+  const int q = n / 2 + 1;
+  const int missing = n - voted;
+  if (yes >= q) return QB_VOTE_WON;
+  if (yes + missing >= q) return QB_VOTE_PENDING;
+  return QB_VOTE_LOST;
+}
+
+// joint.go:61-75.
+__host__ __device__ __forceinline__ u8 joint_vote(u8 r1, u8 r2) {
+  if (r1 == r2) return r1;
+  if (r1 == QB_VOTE_LOST || r2 == QB_VOTE_LOST) return QB_VOTE_LOST;
+  return QB_VOTE_PENDING;
+}
+
+inline unsigned grid_for(u64 threads, unsigned block = kBlock) {
+  return unsigned((threads + block - 1) / block);
+}
+
+}  // namespace qb

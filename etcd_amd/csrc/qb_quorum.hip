@@ -1,0 +1,346 @@
+// qb_quorum.hip — CommittedIndex / VoteResult kernels for gfx950.
+//
+// Reference semantics (paths relative to the reference's raft/):
+//   MajorityConfig.CommittedIndex  quorum/majority.go:126-172
+//   MajorityConfig.VoteResult      quorum/majority.go:178-210
+//   JointConfig.CommittedIndex     quorum/joint.go:49-56
+//   JointConfig.VoteResult         quorum/joint.go:61-75
+//
+// Both kernels are HBM-streaming integer work (no MFMA: nothing here is a
+// contraction).  One thread owns one group (FIXED: GPT groups), the
+// order statistic is a compare-exchange network held in VGPRs, and the vote is
+// three popcounts.  Design notes and rooflines: DESIGN.md §3.
+#include <type_traits>
+
+#include "qb_common.h"
+
+namespace qb {
+
+template <int N>
+using MaskT = std::conditional_t<(N <= 8), u8, u16>;
+
+// Load CNT consecutive elements as one vector access (CNT*sizeof(E) bytes,
+// naturally aligned by the caller's choice of GPT).
+template <int BYTES>
+struct Raw;
+template <> struct Raw<1> { using T = u8; };
+template <> struct Raw<2> { using T = u16; };
+template <> struct Raw<4> { using T = u32; };
+template <> struct Raw<8> { using T = u64; };
+template <> struct Raw<16> { using T = u32 __attribute__((ext_vector_type(4))); };
+
+template <typename E, int CNT>
+__device__ __forceinline__ void vload(const E* __restrict__ p, E (&out)[CNT]) {
+  constexpr int B = int(sizeof(E)) * CNT;
+  if constexpr (B <= 16) {
+    using T = typename Raw<B>::T;
+    const T x = *reinterpret_cast<const T*>(p);
+    __builtin_memcpy(out, &x, B);
+  } else {
+    static_assert(B % 16 == 0, "chunk");
+    using T = typename Raw<16>::T;
+#pragma unroll
+    for (int i = 0; i < B / 16; ++i) {
+      const T x = reinterpret_cast<const T*>(p)[i];
+      __builtin_memcpy(reinterpret_cast<char*>(out) + 16 * i, &x, 16);
+    }
+  }
+}
+
+template <typename E, int CNT>
+__device__ __forceinline__ void vstore(E* __restrict__ p, const E (&in)[CNT]) {
+  constexpr int B = int(sizeof(E)) * CNT;
+  if constexpr (B <= 16) {
+    using T = typename Raw<B>::T;
+    T x;
+    __builtin_memcpy(&x, in, B);
+    *reinterpret_cast<T*>(p) = x;
+  } else {
+    static_assert(B % 16 == 0, "chunk");
+    using T = typename Raw<16>::T;
+#pragma unroll
+    for (int i = 0; i < B / 16; ++i) {
+      T x;
+      __builtin_memcpy(&x, reinterpret_cast<const char*>(in) + 16 * i, 16);
+      reinterpret_cast<T*>(p)[i] = x;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ FIXED ---
+
+template <int N, bool CI, bool VOTE>
+__device__ __forceinline__ void eval_fixed(u64 (&v)[N], u32 vd, u32 gr, u64& ci, u8& vr) {
+  if constexpr (CI) ci = select_quorum<N>(v);
+  if constexpr (VOTE) {
+    constexpr u32 full = (N == 32) ? ~0u : ((1u << N) - 1u);
+    // majority.go:186-200: only config members count; granted needs voted.
+    vr = vote_from_counts(N, __popc(vd & gr & full), __popc(vd & full));
+  }
+}
+
+// GPT consecutive groups per thread: every slot row is read as one
+// GPT*8-byte vector access, masks and outputs likewise.
+template <int N, int GPT, bool CI, bool VOTE>
+__global__ __launch_bounds__(kBlock) void k_fixed(const u64* __restrict__ match, u64 G,
+                                                  const MaskT<N>* __restrict__ voted,
+                                                  const MaskT<N>* __restrict__ granted,
+                                                  u64* __restrict__ commit,
+                                                  u8* __restrict__ vote) {
+  using M = MaskT<N>;
+  const u64 g0 = (u64(blockIdx.x) * kBlock + threadIdx.x) * GPT;
+  if (g0 >= G) return;
+  if (g0 + GPT <= G) {
+    u64 row[N][GPT];
+    if constexpr (CI) {
+#pragma unroll
+      for (int s = 0; s < N; ++s) vload<u64, GPT>(match + u64(s) * G + g0, row[s]);
+    }
+    M vd[GPT], gr[GPT];
+    if constexpr (VOTE) {
+      vload<M, GPT>(voted + g0, vd);
+      vload<M, GPT>(granted + g0, gr);
+    }
+    u64 ci[GPT];
+    u8 vr[GPT];
+#pragma unroll
+    for (int k = 0; k < GPT; ++k) {
+      u64 v[N];
+#pragma unroll
+      for (int s = 0; s < N; ++s) v[s] = CI ? row[s][k] : 0;
+      eval_fixed<N, CI, VOTE>(v, VOTE ? u32(vd[k]) : 0u, VOTE ? u32(gr[k]) : 0u, ci[k], vr[k]);
+    }
+    if constexpr (CI) vstore<u64, GPT>(commit + g0, ci);
+    if constexpr (VOTE) vstore<u8, GPT>(vote + g0, vr);
+  } else {
+    for (u64 g = g0; g < G; ++g) {
+      u64 v[N];
+#pragma unroll
+      for (int s = 0; s < N; ++s) v[s] = CI ? match[u64(s) * G + g] : 0;
+      u64 ci;
+      u8 vr;
+      eval_fixed<N, CI, VOTE>(v, VOTE ? u32(voted[g]) : 0u, VOTE ? u32(granted[g]) : 0u, ci, vr);
+      if constexpr (CI) commit[g] = ci;
+      if constexpr (VOTE) vote[g] = vr;
+    }
+  }
+}
+
+// Empty config (n == 0): CommittedIndex = ∞, VoteResult = VoteWon
+// (majority.go:128-133, 179-184).
+__global__ void k_fill_empty(u64 G, u64* __restrict__ commit, u8* __restrict__ vote) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= G) return;
+  if (commit) commit[g] = kInf;
+  if (vote) vote[g] = QB_VOTE_WON;
+}
+
+template <int N, int GPT, bool CI, bool VOTE>
+static void launch_fixed_t(u64 G, const u64* match, const void* voted, const void* granted,
+                           u64* commit, u8* vote, hipStream_t st) {
+  const u64 threads = (G + GPT - 1) / GPT;
+  hipLaunchKernelGGL((k_fixed<N, GPT, CI, VOTE>), dim3(grid_for(threads)), dim3(kBlock), 0, st,
+                     match, G, static_cast<const MaskT<N>*>(voted),
+                     static_cast<const MaskT<N>*>(granted), commit, vote);
+}
+
+template <int N>
+static void launch_fixed_n(u64 G, const u64* match, const void* voted, const void* granted,
+                           u64* commit, u8* vote, bool vec, hipStream_t st) {
+  const bool ci = commit != nullptr, vt = vote != nullptr;
+  // GPT = 4: 32-byte row chunks (two dwordx4 per slot), 4-8 byte mask/vote
+  // chunks.  Measured best of {1,2,4,8} for n = 5.
+  if (vec) {
+    if (ci && vt) launch_fixed_t<N, 4, true, true>(G, match, voted, granted, commit, vote, st);
+    else if (ci) launch_fixed_t<N, 4, true, false>(G, match, voted, granted, commit, vote, st);
+    else launch_fixed_t<N, 4, false, true>(G, match, voted, granted, commit, vote, st);
+  } else {
+    if (ci && vt) launch_fixed_t<N, 1, true, true>(G, match, voted, granted, commit, vote, st);
+    else if (ci) launch_fixed_t<N, 1, true, false>(G, match, voted, granted, commit, vote, st);
+    else launch_fixed_t<N, 1, false, true>(G, match, voted, granted, commit, vote, st);
+  }
+}
+
+template <int... Ns>
+static void dispatch_fixed(std::integer_sequence<int, Ns...>, int n, u64 G, const u64* match,
+                           const void* voted, const void* granted, u64* commit, u8* vote,
+                           bool vec, hipStream_t st) {
+  ((n == Ns + 1 ? launch_fixed_n<Ns + 1>(G, match, voted, granted, commit, vote, vec, st)
+                : void()),
+   ...);
+}
+
+static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_t* match,
+                                           const void* voted, const void* granted,
+                                           uint64_t* commit_out, uint8_t* vote_out,
+                                           void* stream) {
+  QB_REQUIRE(n <= QB_MAX_SLOTS, "fixed layout supports 0..%d voters, got %u", QB_MAX_SLOTS, n);
+  if (G == 0 || (!commit_out && !vote_out)) return QB_OK;
+  hipStream_t st = as_stream(stream);
+  u64* commit = reinterpret_cast<u64*>(commit_out);
+  if (n == 0) {
+    hipLaunchKernelGGL(k_fill_empty, dim3(grid_for(G)), dim3(kBlock), 0, st, G, commit, vote_out);
+    QB_CHECK_LAUNCH("k_fill_empty");
+    return QB_OK;
+  }
+  QB_REQUIRE(!commit_out || match, "match is NULL");
+  QB_REQUIRE(!vote_out || (voted && granted), "voted/granted NULL with vote_out set");
+  constexpr int GPT = 4;
+  const size_t mb = n <= 8 ? 1 : 2;
+  const bool vec = (G % GPT) == 0 && (!match || aligned(match, 8 * GPT)) &&
+                   (!commit || aligned(commit, 8 * GPT)) &&
+                   (!vote_out || (aligned(vote_out, GPT) && aligned(voted, mb * GPT) &&
+                                  aligned(granted, mb * GPT)));
+  dispatch_fixed(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), G,
+                 reinterpret_cast<const u64*>(match), voted, granted, commit, vote_out, vec, st);
+  QB_CHECK_LAUNCH("k_fixed");
+  return QB_OK;
+}
+
+// -------------------------------------------------------------------- CSR ---
+//
+// A workgroup owns kBlock consecutive groups.  Their slots are one contiguous
+// run of match[] (group-major CSR), so the run is staged into LDS with
+// coalesced 16-byte loads and each thread then reads its own <= 16 slots from
+// LDS.  Non-member slots (learners, other half) are fed as 0: zeros sort to
+// the bottom and leave the q-th largest unchanged for q <= n, exactly the
+// fill-with-zero of majority.go:149-161.  The network width W is chosen per
+// wave (uniform branch) from the wave's widest group.
+
+namespace qb {
+
+constexpr int kCsrLds = kBlock * QB_MAX_SLOTS + 2;  // +2: 16-byte head alignment
+
+template <int W>
+__device__ __forceinline__ u64 csr_select(const u64* lds, u32 lo, u32 s, u32 mask) {
+  u64 v[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) v[j] = (u32(j) < s && ((mask >> j) & 1u)) ? lds[lo + j] : 0ull;
+  sort_net<W>(v);
+  const int n = __popc(mask);
+  if (n == 0) return kInf;  // majority.go:128-133
+  const int want = W - (n / 2 + 1);  // srt[n - (n/2+1)] shifted by W - n zeros
+  u64 r = 0;
+#pragma unroll
+  for (int j = 0; j < W; ++j) r = (j == want) ? v[j] : r;
+  return r;
+}
+
+template <int W>
+__device__ __forceinline__ u64 csr_ci(const u64* lds, u32 lo, u32 s, u32 min_, u32 mout) {
+  u64 ci = csr_select<W>(lds, lo, s, min_);
+  if (mout != 0) {  // joint.go:49-56; an empty half is ∞ and drops out of the min
+    const u64 c2 = csr_select<W>(lds, lo, s, mout);
+    ci = c2 < ci ? c2 : ci;
+  }
+  return ci;
+}
+
+template <bool CI, bool VOTE>
+__global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ off,
+                                                const u64* __restrict__ match,
+                                                const u32* __restrict__ cfg,
+                                                const u32* __restrict__ votes,
+                                                u64* __restrict__ commit,
+                                                u8* __restrict__ vote) {
+  const u64 g0 = u64(blockIdx.x) * kBlock;
+  const u64 g = g0 + threadIdx.x;
+  const bool live = g < G;
+  const u32 c = live ? cfg[g] : 0u;
+  const u32 min_ = c & 0xFFFFu, mout = c >> 16;
+
+  if constexpr (CI) {
+    __shared__ __attribute__((aligned(16))) u64 lds[kCsrLds];
+    const u64 gend = (g0 + kBlock < G) ? g0 + kBlock : G;
+    const u32 base = off[g0], end = off[gend], total = off[G];
+    const u32 abase = base & ~1u;
+    const u32 npair = (end - abase + 1u) >> 1;
+    using V2 = u32 __attribute__((ext_vector_type(4)));
+    for (u32 i = threadIdx.x; i < npair; i += kBlock) {
+      const u32 idx = abase + 2u * i;
+      if (idx + 1u < total) {
+        reinterpret_cast<V2*>(lds)[i] = *reinterpret_cast<const V2*>(match + idx);
+      } else {
+        lds[2u * i] = match[idx];
+      }
+    }
+    __syncthreads();
+    u32 lo = 0, s = 0;
+    if (live) {
+      const u32 a = off[g], b = off[g + 1];
+      lo = a - abase;
+      s = b - a;
+      s = s > QB_MAX_SLOTS ? QB_MAX_SLOTS : s;
+    }
+    u64 ci;
+    // Wave-uniform width choice (no divergence inside the network).
+    if (__ballot(s > 8) == 0) {
+      ci = (__ballot(s > 4) == 0) ? csr_ci<4>(lds, lo, s, min_, mout)
+                                  : csr_ci<8>(lds, lo, s, min_, mout);
+    } else {
+      ci = (__ballot(s > 12) == 0) ? csr_ci<12>(lds, lo, s, min_, mout)
+                                   : csr_ci<16>(lds, lo, s, min_, mout);
+    }
+    if (live) commit[g] = ci;
+  }
+  if constexpr (VOTE) {
+    if (live) {
+      const u32 w = votes[g];
+      const u32 vd = w & 0xFFFFu, gr = (w >> 16) & vd;
+      const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & gr), __popc(min_ & vd));
+      const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & gr), __popc(mout & vd));
+      vote[g] = joint_vote(r1, r2);
+    }
+  }
+}
+
+__global__ void k_csr_validate(u64 G, const u32* __restrict__ off, u64* __restrict__ bad) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const u32 a = off[g], b = off[g + 1];
+  bool ok = b >= a && b - a <= QB_MAX_SLOTS;
+  if (g == 0) ok = ok && a == 0;
+  if (!ok) atomicAdd(bad, 1ull);
+}
+
+}  // namespace qb
+
+extern "C" int qb_dev_csr_committed_vote(uint64_t G, const uint32_t* off, const uint64_t* match,
+                                         const uint32_t* cfg, const uint32_t* votes,
+                                         uint64_t* commit_out, uint8_t* vote_out, void* stream) {
+  if (G == 0 || (!commit_out && !vote_out)) return QB_OK;
+  QB_REQUIRE(cfg, "cfg is NULL");
+  QB_REQUIRE(!commit_out || (off && match), "off/match NULL with commit_out set");
+  QB_REQUIRE(!vote_out || votes, "votes NULL with vote_out set");
+  QB_REQUIRE(!match || aligned(match, 16), "match must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  u64* commit = reinterpret_cast<u64*>(commit_out);
+  const dim3 grid(grid_for(G));
+  if (commit_out && vote_out)
+    hipLaunchKernelGGL((k_csr<true, true>), grid, dim3(kBlock), 0, st, G, off,
+                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
+  else if (commit_out)
+    hipLaunchKernelGGL((k_csr<true, false>), grid, dim3(kBlock), 0, st, G, off,
+                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
+  else
+    hipLaunchKernelGGL((k_csr<false, true>), grid, dim3(kBlock), 0, st, G, off,
+                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
+  QB_CHECK_LAUNCH("k_csr");
+  return QB_OK;
+}
+
+extern "C" int qb_dev_csr_validate(uint64_t G, const uint32_t* off, uint64_t* bad_out,
+                                   void* stream) {
+  QB_REQUIRE(off && bad_out, "off/bad_out NULL");
+  if (G == 0) return QB_OK;
+  hipLaunchKernelGGL(k_csr_validate, dim3(grid_for(G)), dim3(kBlock), 0, as_stream(stream), G,
+                     off, reinterpret_cast<u64*>(bad_out));
+  QB_CHECK_LAUNCH("k_csr_validate");
+  return QB_OK;
+}

@@ -1,0 +1,251 @@
+// qb_tracker.hip — ProgressTracker hot path over G groups (gfx950).
+//
+// Reference semantics (paths relative to the reference's raft/):
+//   raft.Step term filter               raft.go:847-921
+//   stepLeader MsgAppResp (quorum part) raft.go:1100-1109, 1237-1259
+//   Progress.MaybeUpdate                tracker/progress.go:144-153
+//   raft.maybeCommit                    raft.go:585-588
+//   raftLog.maybeCommit / commitTo      log.go:328-334, 236-244
+//   ProgressTracker.QuorumActive        tracker/tracker.go:215-225
+#include <type_traits>
+
+#include "qb_common.h"
+
+namespace qb {
+
+// ------------------------------------------------------------ QuorumActive --
+
+__global__ __launch_bounds__(kBlock) void k_quorum_active(u64 G, const u32* __restrict__ cfg,
+                                                          const u16* __restrict__ active,
+                                                          u8* __restrict__ won) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const u32 c = cfg[g];
+  const u32 min_ = c & 0xFFFFu, mout = c >> 16, a = active[g];
+  // Every voter has a Progress, so votes[id] = RecentActive is present for
+  // each: yes = popcount(mask & active), voted = n (tracker.go:216-222).
+  const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & a), __popc(min_));
+  const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & a), __popc(mout));
+  won[g] = joint_vote(r1, r2) == QB_VOTE_WON ? 1 : 0;
+}
+
+// ---------------------------------------------------------- MsgAppResp -----
+
+enum RecClass : int {
+  C_APPLY = 0, C_REJECT = 1, C_STALE = 2, C_NONMEMBER = 3, C_HIGHER = 4, C_BAD = 5,
+};
+
+__device__ __forceinline__ int classify(u32 n, u64 G, u64 g, u32 flags, u64 t,
+                                        const u64* __restrict__ group_term) {
+  if (g >= G) return C_BAD;
+  if ((flags & 0x0Fu) >= n) return C_NONMEMBER;  // pr == nil (raft.go:1100-1104)
+  const u64 gt = group_term[g];
+  if (t < gt) return C_STALE;                    // raft.go:883-921: ignored
+  if (t > gt) return C_HIGHER;                   // raft.go:875-879: becomeFollower
+  return (flags & QB_REC_REJECT) ? C_REJECT : C_APPLY;
+}
+
+// Wave-aggregated counter update: one atomic per category per wave.
+__device__ __forceinline__ void count_class(u64* stats, int cls, bool valid) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if (k == C_HIGHER) continue;  // counted by pass 1
+    const u64 m = __ballot(valid && cls == k);
+    if (lane == 0 && m) {
+      const int slot = k == C_APPLY ? QB_STAT_APPLIED
+                     : k == C_REJECT ? QB_STAT_REJECTED
+                     : k == C_STALE ? QB_STAT_STALE_TERM
+                     : k == C_NONMEMBER ? QB_STAT_NON_MEMBER
+                     : k == C_HIGHER ? QB_STAT_HIGHER_TERM
+                                     : QB_STAT_BAD_GROUP;
+      atomicAdd(stats + slot, u64(__popcll(m)));
+    }
+  }
+}
+
+// Pass 1: the first higher-term record of each group (in batch order) makes
+// the sequential leader step down; later records of that group never reach
+// stepLeader.  Records the batch index of that first record and counts the
+// higher-term records into stats[QB_STAT_HIGHER_TERM], which pass 2 reads as
+// "some group may have stepped down".
+__global__ __launch_bounds__(kBlock) void k_appresp_stepdown(
+    u32 n, u64 G, u64 M, const u32* __restrict__ rg, const u8* __restrict__ rf,
+    const u64* __restrict__ rt, const u64* __restrict__ group_term, u32* __restrict__ stepdown_at,
+    u64* __restrict__ stats) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  bool higher = false;
+  if (i < M) {
+    const u64 g = rg[i];
+    higher = classify(n, G, g, rf[i], rt[i], group_term) == C_HIGHER;
+    if (higher) atomicMin(stepdown_at + g, u32(i));
+  }
+  const u64 m = __ballot(higher);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(stats + QB_STAT_HIGHER_TERM, u64(__popcll(m)));
+}
+
+// Pass 2: MaybeUpdate as atomic max (commutative, so any arrival order gives
+// the sequential end state), RecentActive as atomic or.
+__global__ __launch_bounds__(kBlock) void k_appresp_apply(
+    u32 n, u64 G, u64 M, const u32* __restrict__ rg, const u8* __restrict__ rf,
+    const u64* __restrict__ ri, const u64* __restrict__ rt, const u64* __restrict__ group_term,
+    u64* __restrict__ match, u64* __restrict__ next, u32* __restrict__ active_words,
+    const u32* __restrict__ stepdown_at, u64* __restrict__ stats) {
+  const bool any_higher = stats[QB_STAT_HIGHER_TERM] != 0;  // uniform scalar load
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  const bool valid = i < M;
+  int cls = C_BAD;
+  bool after = false;
+  if (valid) {
+    const u64 g = rg[i];
+    const u32 f = rf[i];
+    cls = classify(n, G, g, f, rt[i], group_term);
+    if (cls == C_APPLY || cls == C_REJECT) {
+      if (any_higher && stepdown_at[g] < u32(i)) {
+        after = true;  // the leader already stepped down at an earlier record
+      } else {
+        const u32 s = f & 0x0Fu;
+        // raft.go:1107: pr.RecentActive = true (reject or not).
+        atomicOr(active_words + (g >> 1), (1u << s) << ((g & 1u) * 16u));
+        if (cls == C_APPLY) {
+          const u64 idx = ri[i];
+          atomicMax(match + u64(s) * G + g, idx);                  // progress.go:146-150
+          if (next) atomicMax(next + u64(s) * G + g, idx + 1ull);  // progress.go:151
+        }
+      }
+    }
+  }
+  count_class(stats, after ? -1 : cls, valid);
+  const u64 m = __ballot(valid && after);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(stats + QB_STAT_AFTER_STEPDOWN, u64(__popcll(m)));
+}
+
+// ------------------------------------------------------- commit advance ----
+
+template <int BYTES> struct RawT;
+template <> struct RawT<8> { using T = u64; };
+template <> struct RawT<16> { using T = u32 __attribute__((ext_vector_type(4))); };
+
+// raft.maybeCommit -> raftLog.maybeCommit for every group.  GPT consecutive
+// groups per thread so every slot row is one 16-byte load.
+template <int N, int GPT>
+__global__ __launch_bounds__(kBlock) void k_commit_advance(u64 G, const u64* __restrict__ match,
+                                                           const u64* __restrict__ term_start,
+                                                           u64* __restrict__ committed,
+                                                           u8* __restrict__ advanced) {
+  static_assert(GPT == 1 || GPT == 2, "GPT");
+  using T = typename RawT<8 * GPT>::T;
+  const u64 g0 = (u64(blockIdx.x) * kBlock + threadIdx.x) * GPT;
+  if (g0 >= G) return;
+  const int cnt = (g0 + GPT <= G) ? GPT : int(G - g0);
+  u64 row[N][GPT], ts[GPT], cm[GPT];
+  if (cnt == GPT) {
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      const T x = *reinterpret_cast<const T*>(match + u64(s) * G + g0);
+      __builtin_memcpy(row[s], &x, 8 * GPT);
+    }
+    const T a = *reinterpret_cast<const T*>(term_start + g0);
+    const T b = *reinterpret_cast<const T*>(committed + g0);
+    __builtin_memcpy(ts, &a, 8 * GPT);
+    __builtin_memcpy(cm, &b, 8 * GPT);
+  } else {
+#pragma unroll
+    for (int k = 0; k < GPT; ++k) {
+      const u64 g = k < cnt ? g0 + k : g0;
+#pragma unroll
+      for (int s = 0; s < N; ++s) row[s][k] = match[u64(s) * G + g];
+      ts[k] = term_start[g];
+      cm[k] = committed[g];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GPT; ++k) {
+    if (k >= cnt) break;
+    u64 v[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) v[s] = row[s][k];
+    const u64 ci = select_quorum<N>(v);
+    // log.go:329: maxIndex > committed && term(maxIndex) == r.Term.
+    const bool adv = ci > cm[k] && ci >= ts[k];
+    if (adv) committed[g0 + k] = ci;  // commitTo never decreases (log.go:238)
+    if (advanced) advanced[g0 + k] = adv ? 1 : 0;
+  }
+}
+
+template <int N>
+static void launch_commit_n(u64 G, const u64* match, const u64* ts, u64* cm, u8* adv,
+                            hipStream_t st) {
+  const bool vec = (G % 2) == 0 && (reinterpret_cast<uintptr_t>(match) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(ts) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(cm) % 16) == 0;
+  if (vec)
+    hipLaunchKernelGGL((k_commit_advance<N, 2>), dim3(grid_for((G + 1) / 2)), dim3(kBlock), 0,
+                       st, G, match, ts, cm, adv);
+  else
+    hipLaunchKernelGGL((k_commit_advance<N, 1>), dim3(grid_for(G)), dim3(kBlock), 0, st, G,
+                       match, ts, cm, adv);
+}
+
+template <int... Ns>
+static void dispatch_commit(std::integer_sequence<int, Ns...>, int n, u64 G, const u64* match,
+                            const u64* ts, u64* cm, u8* adv, hipStream_t st) {
+  ((n == Ns + 1 ? launch_commit_n<Ns + 1>(G, match, ts, cm, adv, st) : void()), ...);
+}
+
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" int qb_dev_csr_quorum_active(uint64_t G, const uint32_t* cfg, const uint16_t* active,
+                                        uint8_t* won_out, void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(cfg && active && won_out, "cfg/active/won_out NULL");
+  hipLaunchKernelGGL(k_quorum_active, dim3(grid_for(G)), dim3(kBlock), 0, as_stream(stream), G,
+                     cfg, active, won_out);
+  QB_CHECK_LAUNCH("k_quorum_active");
+  return QB_OK;
+}
+
+extern "C" int qb_dev_fixed_apply_appresp(uint32_t n, uint64_t G, uint64_t M,
+                                          const uint32_t* rec_group, const uint8_t* rec_flags,
+                                          const uint64_t* rec_index, const uint64_t* rec_term,
+                                          const uint64_t* group_term, uint64_t* match,
+                                          uint64_t* next, uint16_t* active,
+                                          uint32_t* stepdown_at, uint64_t* stats, void* stream) {
+  QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
+  if (M == 0) return QB_OK;
+  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
+  QB_REQUIRE(rec_group && rec_flags && rec_index && rec_term && group_term && match && active &&
+                 stepdown_at && stats,
+             "required pointer is NULL");
+  QB_REQUIRE((reinterpret_cast<uintptr_t>(active) % 4) == 0, "active must be 4-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const dim3 grid(grid_for(M));
+  hipLaunchKernelGGL(k_appresp_stepdown, grid, dim3(kBlock), 0, st, n, G, M, rec_group, rec_flags,
+                     reinterpret_cast<const u64*>(rec_term),
+                     reinterpret_cast<const u64*>(group_term), stepdown_at,
+                     reinterpret_cast<u64*>(stats));
+  QB_CHECK_LAUNCH("k_appresp_stepdown");
+  hipLaunchKernelGGL(k_appresp_apply, grid, dim3(kBlock), 0, st, n, G, M, rec_group, rec_flags,
+                     reinterpret_cast<const u64*>(rec_index),
+                     reinterpret_cast<const u64*>(rec_term),
+                     reinterpret_cast<const u64*>(group_term), reinterpret_cast<u64*>(match),
+                     reinterpret_cast<u64*>(next), reinterpret_cast<u32*>(active), stepdown_at,
+                     reinterpret_cast<u64*>(stats));
+  QB_CHECK_LAUNCH("k_appresp_apply");
+  return QB_OK;
+}
+
+extern "C" int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
+                                           const uint64_t* term_start, uint64_t* committed,
+                                           uint8_t* advanced_out, void* stream) {
+  QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(match && term_start && committed, "required pointer is NULL");
+  dispatch_commit(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), G,
+                  reinterpret_cast<const u64*>(match), reinterpret_cast<const u64*>(term_start),
+                  reinterpret_cast<u64*>(committed), advanced_out, as_stream(stream));
+  QB_CHECK_LAUNCH("k_commit_advance");
+  return QB_OK;
+}

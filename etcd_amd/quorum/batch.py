@@ -1,0 +1,307 @@
+"""raft/quorum/batch — the batch engine's Python face.
+
+Mirror of the Go ``raft/quorum/batch`` package that INTEGRATION.md describes:
+G independent raft groups evaluated per call, state resident in HBM as
+structure-of-arrays, every computation a HIP kernel behind the C ABI
+(include/quorum_batch.h).  torch is used only for device memory, streams and
+host<->device copies.
+
+Device tensors hold uint64 values in int64 storage (bit-identical); use
+``as_u64`` to view them as numpy uint64 after ``.cpu()``.
+
+Reference semantics (paths relative to the reference's raft/):
+  MajorityConfig.CommittedIndex / VoteResult   quorum/majority.go:126-210
+  JointConfig.CommittedIndex / VoteResult      quorum/joint.go:49-75
+  ProgressTracker.QuorumActive                 tracker/tracker.go:215-225
+  Progress.MaybeUpdate                         tracker/progress.go:144-153
+  raft.maybeCommit -> raftLog.maybeCommit      raft.go:585-588, log.go:328-334
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _lib
+
+INDEX_INF = (1 << 64) - 1
+
+
+def as_u64(t: torch.Tensor) -> np.ndarray:
+    """View an int64 tensor (device or host) as numpy uint64."""
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def from_u64(a, device) -> torch.Tensor:
+    """numpy uint64 (or anything np.asarray accepts) -> int64 tensor on device."""
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.uint64)).view(np.int64)
+    return torch.from_numpy(arr.copy()).to(device)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise _lib.QuorumBatchError(f"{what} must be a device (HIP) tensor; there is no CPU path")
+
+
+def mask_dtype(n: int):
+    return torch.uint8 if n <= 8 else torch.int16
+
+
+# ---------------------------------------------------------------- FIXED ---
+
+class FixedGroups:
+    """G groups sharing one n-voter MajorityConfig shape (FIXED layout).
+
+    ``match`` is [n, G] (slot-major), ``voted``/``granted`` are per-group slot
+    bitmasks (uint8 for n <= 8, int16 bits for n <= 16).
+    """
+
+    def __init__(self, n: int, G: int, device="cuda", match=None, voted=None, granted=None):
+        if not 0 <= n <= _lib.QB_MAX_SLOTS:
+            raise ValueError(f"n must be 0..{_lib.QB_MAX_SLOTS}")
+        self.n, self.G, self.device = n, G, torch.device(device)
+        mt = mask_dtype(n)
+        self.match = match if match is not None else torch.zeros((n, G), dtype=torch.int64,
+                                                                  device=self.device)
+        self.voted = voted if voted is not None else torch.zeros(G, dtype=mt, device=self.device)
+        self.granted = granted if granted is not None else torch.zeros(G, dtype=mt,
+                                                                       device=self.device)
+        for t, w in ((self.match, "match"), (self.voted, "voted"), (self.granted, "granted")):
+            _require_device(t, w)
+
+    @classmethod
+    def synth(cls, seed: int, n: int, G: int, g_begin: int = 0, device="cuda",
+              with_term_start: bool = False):
+        """Counter-based synthetic groups (qb_dev_synth_fixed)."""
+        fg = cls(n, G, device, match=torch.empty((n, G), dtype=torch.int64, device=device),
+                 voted=torch.empty(G, dtype=mask_dtype(n), device=device),
+                 granted=torch.empty(G, dtype=mask_dtype(n), device=device))
+        ts = torch.empty(G, dtype=torch.int64, device=device) if with_term_start else None
+        _lib.call("qb_dev_synth_fixed", seed, n, G, g_begin, _ptr(fg.match), _ptr(fg.voted),
+                  _ptr(fg.granted), _ptr(ts), _stream(fg.device))
+        fg.term_start = ts
+        return fg
+
+    def committed_vote(self, commit_out: Optional[torch.Tensor] = None,
+                       vote_out: Optional[torch.Tensor] = None, want_commit=True, want_vote=True):
+        """Enqueue CommittedIndex and/or VoteResult for all G groups."""
+        if want_commit and commit_out is None:
+            commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
+        if want_vote and vote_out is None:
+            vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_fixed_committed_vote", self.n, self.G, _ptr(self.match),
+                  _ptr(self.voted), _ptr(self.granted), _ptr(commit_out if want_commit else None),
+                  _ptr(vote_out if want_vote else None), _stream(self.device))
+        return (commit_out if want_commit else None), (vote_out if want_vote else None)
+
+    def committed_index(self) -> torch.Tensor:
+        return self.committed_vote(want_vote=False)[0]
+
+    def vote_result(self) -> torch.Tensor:
+        return self.committed_vote(want_commit=False)[1]
+
+
+# ------------------------------------------------------------------ CSR ---
+
+@dataclass
+class CompiledConfigs:
+    """Host-side result of compiling per-group configs to the CSR layout.
+
+    slot ids per group are the sorted union of Voters[0], Voters[1] and the
+    learners (MajorityConfig.Slice order, majority.go:106-113)."""
+    off: np.ndarray       # uint32 [G+1]
+    cfg: np.ndarray       # uint32 [G]  mask_in | mask_out << 16
+    slot_ids: np.ndarray  # uint64 [off[G]]
+
+    @property
+    def G(self) -> int:
+        return len(self.cfg)
+
+    def slots(self, g: int) -> np.ndarray:
+        return self.slot_ids[self.off[g]:self.off[g + 1]]
+
+
+def compile_configs(voters_in: Sequence[Iterable[int]], voters_out: Sequence[Iterable[int]] = None,
+                    learners: Sequence[Iterable[int]] = None) -> CompiledConfigs:
+    """tracker.Config (tracker.go:27-78) per group -> CSR slots and masks.
+
+    Learners must not intersect the voters (tracker.go:40-46; enforced by
+    confchange, confchange.go:307-318) — a violation raises ValueError."""
+    G = len(voters_in)
+    voters_out = voters_out if voters_out is not None else [()] * G
+    learners = learners if learners is not None else [()] * G
+    if len(voters_out) != G or len(learners) != G:
+        raise ValueError("voters_in, voters_out and learners must have one entry per group")
+    off = np.zeros(G + 1, dtype=np.uint32)
+    cfg = np.zeros(G, dtype=np.uint32)
+    ids = []
+    for g in range(G):
+        vi, vo, lr = set(voters_in[g]), set(voters_out[g]), set(learners[g])
+        if lr & (vi | vo):
+            raise ValueError(f"group {g}: learners {sorted(lr & (vi | vo))} are also voters")
+        slot = sorted(vi | vo | lr)
+        if len(slot) > _lib.QB_MAX_SLOTS:
+            raise ValueError(f"group {g}: {len(slot)} slots > {_lib.QB_MAX_SLOTS}")
+        m_in = sum(1 << j for j, i in enumerate(slot) if i in vi)
+        m_out = sum(1 << j for j, i in enumerate(slot) if i in vo)
+        cfg[g] = m_in | (m_out << 16)
+        off[g + 1] = off[g] + len(slot)
+        ids.extend(slot)
+    return CompiledConfigs(off, cfg, np.asarray(ids, dtype=np.uint64))
+
+
+class CsrGroups:
+    """G ragged / joint groups (CSR layout) resident on one device."""
+
+    def __init__(self, off: torch.Tensor, cfg: torch.Tensor, match: torch.Tensor,
+                 votes: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None):
+        self.off, self.cfg, self.match = off, cfg, match
+        self.G = cfg.numel()
+        self.device = cfg.device
+        self.votes = votes if votes is not None else torch.zeros(self.G, dtype=torch.int32,
+                                                                 device=self.device)
+        self.active = active
+        for t, w in ((off, "off"), (cfg, "cfg"), (match, "match"), (self.votes, "votes")):
+            _require_device(t, w)
+        if off.dtype != torch.int32 or cfg.dtype != torch.int32 or match.dtype != torch.int64:
+            raise TypeError("off/cfg must be int32 (uint32 bits), match int64 (uint64 bits)")
+
+    @classmethod
+    def from_compiled(cls, cc: CompiledConfigs, match_u64: np.ndarray, votes_u32=None,
+                      active_u16=None, device="cuda"):
+        dev = torch.device(device)
+        off = torch.from_numpy(cc.off.view(np.int32).copy()).to(dev)
+        cfg = torch.from_numpy(cc.cfg.view(np.int32).copy()).to(dev)
+        # keep at least one element so the pointer is valid for an all-empty batch
+        m = np.asarray(match_u64, dtype=np.uint64)
+        match = from_u64(m if m.size else np.zeros(2, np.uint64), dev)
+        votes = None
+        if votes_u32 is not None:
+            votes = torch.from_numpy(np.asarray(votes_u32, np.uint32).view(np.int32).copy()).to(dev)
+        active = None
+        if active_u16 is not None:
+            active = torch.from_numpy(np.asarray(active_u16, np.uint16).view(np.int16).copy()).to(dev)
+        return cls(off, cfg, match, votes, active)
+
+    @classmethod
+    def synth(cls, seed: int, kind: str, G: int, g_begin: int = 0, device="cuda"):
+        """Synthetic ragged ('ragged': 3-9 voters + 0-2 learners) or joint
+        ('joint': 5+5 with overlap 0-5) groups."""
+        k = {"ragged": 0, "joint": 1}[kind]
+        off_h = np.empty(G + 1, dtype=np.uint32)
+        fn = "qb_host_synth_csr_offsets" if k == 0 else "qb_host_synth_joint_offsets"
+        _lib.call(fn, seed, G, g_begin, off_h.ctypes.data)
+        dev = torch.device(device)
+        off = torch.from_numpy(off_h.view(np.int32)).to(dev)
+        total = int(off_h[-1])
+        match = torch.empty(max(total, 2), dtype=torch.int64, device=dev)
+        cfg = torch.empty(G, dtype=torch.int32, device=dev)
+        votes = torch.empty(G, dtype=torch.int32, device=dev)
+        _lib.call("qb_dev_synth_csr", seed, k, G, g_begin, _ptr(off), _ptr(match), _ptr(cfg),
+                  _ptr(votes), _stream(dev))
+        return cls(off, cfg, match, votes)
+
+    def committed_vote(self, commit_out=None, vote_out=None, want_commit=True, want_vote=True):
+        if want_commit and commit_out is None:
+            commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
+        if want_vote and vote_out is None:
+            vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_csr_committed_vote", self.G, _ptr(self.off), _ptr(self.match),
+                  _ptr(self.cfg), _ptr(self.votes), _ptr(commit_out if want_commit else None),
+                  _ptr(vote_out if want_vote else None), _stream(self.device))
+        return (commit_out if want_commit else None), (vote_out if want_vote else None)
+
+    def committed_index(self) -> torch.Tensor:
+        return self.committed_vote(want_vote=False)[0]
+
+    def vote_result(self) -> torch.Tensor:
+        return self.committed_vote(want_commit=False)[1]
+
+    def quorum_active(self, active: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """ProgressTracker.QuorumActive per group (tracker.go:215-225)."""
+        active = active if active is not None else self.active
+        if active is None:
+            raise ValueError("no RecentActive bits given")
+        out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_csr_quorum_active", self.G, _ptr(self.cfg), _ptr(active), _ptr(out),
+                  _stream(self.device))
+        return out
+
+    def validate(self) -> int:
+        bad = torch.zeros(1, dtype=torch.int64, device=self.device)
+        _lib.call("qb_dev_csr_validate", self.G, _ptr(self.off), _ptr(bad), _stream(self.device))
+        return int(bad.item())
+
+
+# -------------------------------------------------------------- tracker ---
+
+@dataclass
+class AppRespBatch:
+    """A batch of MsgAppResp records (raftpb.Message fields the path reads)."""
+    group: torch.Tensor  # int32 (uint32 group index)
+    flags: torch.Tensor  # uint8: slot | 0x80 if Reject
+    index: torch.Tensor  # int64 (uint64 Message.Index)
+    term: torch.Tensor   # int64 (uint64 Message.Term)
+
+    @property
+    def M(self) -> int:
+        return self.group.numel()
+
+    @classmethod
+    def from_numpy(cls, group, slot, index, term, reject=None, device="cuda"):
+        dev = torch.device(device)
+        flags = np.asarray(slot, np.uint8) & 0x0F
+        if reject is not None:
+            flags = flags | (np.asarray(reject, bool).astype(np.uint8) << 7)
+        return cls(torch.from_numpy(np.asarray(group, np.uint32).view(np.int32).copy()).to(dev),
+                   torch.from_numpy(flags.astype(np.uint8)).to(dev),
+                   from_u64(index, dev), from_u64(term, dev))
+
+
+class FixedTracker:
+    """Leader-side ProgressTracker state of G groups with n voters each."""
+
+    def __init__(self, n: int, G: int, device="cuda", track_next: bool = False):
+        self.n, self.G, self.device = n, G, torch.device(device)
+        dev = self.device
+        self.match = torch.zeros((n, G), dtype=torch.int64, device=dev)
+        self.next = torch.ones((n, G), dtype=torch.int64, device=dev) if track_next else None
+        self.active = torch.zeros(G + (G & 1), dtype=torch.int16, device=dev)  # even length
+        self.term = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.term_start = torch.full((G,), -1, dtype=torch.int64, device=dev)  # ∞
+        self.committed = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.stepdown_at = torch.full((G,), -1, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(_lib.QB_STAT_COUNT, dtype=torch.int64, device=dev)
+
+    def apply_appresp(self, batch: AppRespBatch, reset_stats: bool = True):
+        """stepLeader's MsgAppResp handling (quorum part) for a whole batch."""
+        if reset_stats:
+            self.stats.zero_()
+        _lib.call("qb_dev_fixed_apply_appresp", self.n, self.G, batch.M, _ptr(batch.group),
+                  _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(self.term),
+                  _ptr(self.match), _ptr(self.next), _ptr(self.active), _ptr(self.stepdown_at),
+                  _ptr(self.stats), _stream(self.device))
+
+    def commit_advance(self, advanced_out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """raft.maybeCommit for every group; returns the per-group advanced flags."""
+        _lib.call("qb_dev_fixed_commit_advance", self.n, self.G, _ptr(self.match),
+                  _ptr(self.term_start), _ptr(self.committed), _ptr(advanced_out),
+                  _stream(self.device))
+        return advanced_out
+
+    def stats_dict(self) -> dict:
+        v = self.stats.cpu().tolist()
+        return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}
+
+    def stepped_down(self) -> torch.Tensor:
+        return self.stepdown_at != -1

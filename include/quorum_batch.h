@@ -1,0 +1,209 @@
+/*
+ * quorum_batch.h — C ABI of libquorumbatch, the MI355X batched quorum engine.
+ *
+ * This is the drop-in boundary for etcd's raft quorum/tracker hot path
+ * evaluated over G independent raft groups at once.  It is the ABI a
+ * ``raft/quorum/batch`` cgo package binds; every entry
+ * point names the reference interface it replaces (paths relative to the
+ * reference's ``raft/``).  Plain C types only: no torch, no HIP types.
+ *
+ * Conventions (mirroring the reference):
+ *   - Every call returns int: QB_OK (0) or a negative QB_E* code; the text of
+ *     the most recent failure on the calling thread is qb_last_error().
+ *   - Quorum semantics never error: an empty majority config yields
+ *     QB_INDEX_INF (MaxUint64) and VoteWon, exactly as majority.go:128-133 and
+ *     majority.go:179-184.  Only malformed inputs (bad sizes, null required
+ *     pointers, HIP failures) produce an error code.
+ *   - Indexes are quorum.Index (uint64, unsigned compare over the full range);
+ *     vote results are quorum.VoteResult: 1 Pending, 2 Lost, 3 Won
+ *     (quorum.go:45-58).
+ *   - "qb_dev_*" calls take DEVICE pointers and a hipStream_t passed as
+ *     void* (NULL = the null stream); they only enqueue work.  Ownership stays
+ *     with the caller.  One stream per host thread; no internal locking
+ *     (single owner, like raft's RawNode, rawnode.go:31).
+ *
+ * Device layouts (structure of arrays, all little-endian):
+ *
+ *   FIXED  (every group is one n-voter MajorityConfig, 1 <= n <= 16, no
+ *           learners; slot j = the j-th smallest voter ID, MajorityConfig.Slice
+ *           majority.go:106-113):
+ *     match[n][G]   uint64, slot-major: match[j*G + g] = Progress.Match
+ *     voted[G], granted[G]   bitmask per group, bit j = slot j; uint8 when
+ *                   n <= 8, uint16 when n > 8.  granted bits count only where
+ *                   the voted bit is set (votes map: present -> voted).
+ *
+ *   CSR    (ragged: voters + learners, joint configs; 0 <= s_g <= 16 slots;
+ *           s_g == 0 is the empty config):
+ *     off[G+1]      uint32, slots of group g are off[g] .. off[g+1]-1
+ *     match[off[G]] uint64, group-major
+ *     cfg[G]        uint32 = mask_in | mask_out << 16  (JointConfig halves
+ *                   Voters[0] / Voters[1], tracker.go:27-78; a slot with
+ *                   neither bit is a learner; mask_out == 0 is a plain
+ *                   majority config — identical results by joint.go:49-56)
+ *     votes[G]      uint32 = voted | granted << 16
+ *     active[G]     uint16 RecentActive bits (tracker.go:215-225)
+ *
+ *   MsgAppResp batch records (M records, any order):
+ *     rec_group[M]  uint32 group index within the shard
+ *     rec_flags[M]  uint8: bits 0-3 = slot, bit 7 = Reject
+ *     rec_index[M]  uint64 Message.Index
+ *     rec_term[M]   uint64 Message.Term
+ */
+#ifndef QUORUM_BATCH_H
+#define QUORUM_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QB_ABI_VERSION 1
+
+#define QB_OK 0
+#define QB_EINVAL (-1)   /* malformed arguments */
+#define QB_EHIP (-2)     /* HIP runtime error (text in qb_last_error) */
+#define QB_ENOMEM (-3)   /* device allocation failed */
+
+#define QB_INDEX_INF UINT64_MAX  /* quorum.Index "∞", quorum.go:25-30 */
+
+#define QB_VOTE_PENDING 1  /* quorum.VotePending, quorum.go:53 */
+#define QB_VOTE_LOST 2     /* quorum.VoteLost,    quorum.go:55 */
+#define QB_VOTE_WON 3      /* quorum.VoteWon,     quorum.go:57 */
+
+#define QB_MAX_SLOTS 16
+#define QB_REC_REJECT 0x80u
+
+/* Counters filled by qb_dev_fixed_apply_appresp (device memory, uint64 each;
+ * accumulated, so zero them before a batch if per-batch numbers are wanted). */
+enum {
+  QB_STAT_APPLIED = 0,     /* non-reject, same-term, member: MaybeUpdate ran   */
+  QB_STAT_REJECTED = 1,    /* Reject=true: RecentActive only (raft.go:1107-1109) */
+  QB_STAT_STALE_TERM = 2,  /* m.Term < group term: dropped (raft.go:883-921)    */
+  QB_STAT_NON_MEMBER = 3,  /* no Progress for the slot: dropped (raft.go:1100) */
+  QB_STAT_HIGHER_TERM = 4, /* m.Term > group term: leader steps down (raft.go:852-880) */
+  QB_STAT_BAD_GROUP = 5,   /* group index >= G: dropped                        */
+  QB_STAT_AFTER_STEPDOWN = 6, /* same-term record behind a higher-term one     */
+  QB_STAT_COUNT = 8
+};
+
+/* ----------------------------------------------------------------------- */
+/* Library                                                                 */
+/* ----------------------------------------------------------------------- */
+
+int qb_abi_version(void);
+/* Text of the last error on this thread ("" if none). */
+const char* qb_last_error(void);
+/* Number of visible HIP devices (0 without a GPU); never fails. */
+int qb_device_count(void);
+
+/* ----------------------------------------------------------------------- */
+/* Quorum math (raft/quorum)                                               */
+/* ----------------------------------------------------------------------- */
+
+/* CommittedIndex and/or VoteResult for G groups of one n-voter
+ * MajorityConfig shape (FIXED layout).
+ * Replaces MajorityConfig.CommittedIndex (quorum/majority.go:126-172) and
+ * MajorityConfig.VoteResult (quorum/majority.go:178-210).
+ * n == 0 fills commit_out with QB_INDEX_INF and vote_out with VoteWon.
+ * commit_out and/or vote_out may be NULL to skip that result; voted/granted
+ * may be NULL only when vote_out is NULL. */
+int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_t* match,
+                                const void* voted, const void* granted,
+                                uint64_t* commit_out, uint8_t* vote_out,
+                                void* stream);
+
+/* CommittedIndex and/or VoteResult for G ragged/joint groups (CSR layout).
+ * Replaces JointConfig.CommittedIndex (quorum/joint.go:49-56) and
+ * JointConfig.VoteResult (quorum/joint.go:61-75), which reduce to the
+ * MajorityConfig forms when mask_out == 0; learners are slots in neither mask
+ * and never count (tracker.go:273, majority.go:186-200). */
+int qb_dev_csr_committed_vote(uint64_t G, const uint32_t* off,
+                              const uint64_t* match, const uint32_t* cfg,
+                              const uint32_t* votes, uint64_t* commit_out,
+                              uint8_t* vote_out, void* stream);
+
+/* Checks a CSR table (off[0] == 0, 0 <= off[g+1] - off[g] <= 16).  Writes the
+ * number of bad groups to *bad_out (device uint64). */
+int qb_dev_csr_validate(uint64_t G, const uint32_t* off, uint64_t* bad_out,
+                        void* stream);
+
+/* ----------------------------------------------------------------------- */
+/* Progress tracking (raft/tracker)                                        */
+/* ----------------------------------------------------------------------- */
+
+/* ProgressTracker.QuorumActive (tracker/tracker.go:215-225) per group:
+ * won_out[g] = 1 iff VoteResult(votes = RecentActive of every voter) is
+ * VoteWon in both halves. */
+int qb_dev_csr_quorum_active(uint64_t G, const uint32_t* cfg,
+                             const uint16_t* active, uint8_t* won_out,
+                             void* stream);
+
+/* Apply a batch of MsgAppResp records to FIXED-layout leader state — the
+ * quorum-facing part of stepLeader's MsgAppResp case (raft.go:1100-1109,
+ * 1237-1239): Progress.MaybeUpdate (tracker/progress.go:144-153) as an
+ * atomic scatter-max of match (and next, if non-NULL), RecentActive bits,
+ * and the term filter of raft.Step (raft.go:847-921).  Batch-equivalent to
+ * applying the records one by one in index order.
+ *   group_term[G]   the leader's current term per group
+ *   match[n][G], next[n][G] (nullable), active[G] (uint16 bits; the array
+ *                   must be 4-byte aligned and padded to an even length)
+ *   stepdown_at[G]  uint32, must hold UINT32_MAX on entry for every group;
+ *                   on return it holds the batch index of the first
+ *                   higher-term record of a group that must step down
+ *                   (raft.go:875-879), UINT32_MAX otherwise.  Records after
+ *                   it are not applied, as in the sequential reference.
+ *   stats[QB_STAT_COUNT] device uint64 counters (required; zero them per
+ *                   batch — a non-zero HIGHER_TERM count only makes the
+ *                   apply pass consult stepdown_at, it never changes results). */
+int qb_dev_fixed_apply_appresp(uint32_t n, uint64_t G, uint64_t M,
+                               const uint32_t* rec_group,
+                               const uint8_t* rec_flags,
+                               const uint64_t* rec_index,
+                               const uint64_t* rec_term,
+                               const uint64_t* group_term, uint64_t* match,
+                               uint64_t* next, uint16_t* active,
+                               uint32_t* stepdown_at, uint64_t* stats,
+                               void* stream);
+
+/* raft.maybeCommit (raft.go:585-588) -> raftLog.maybeCommit (log.go:328-334)
+ * for every group of the FIXED layout: committed[g] = CI if CI > committed[g]
+ * and term(CI) == Term, where term(CI) == Term <=> CI >= term_start[g]
+ * (term_start = first index of the leader's current term, QB_INDEX_INF if the
+ * leader has none; CI <= lastIndex holds because no voter acks past the
+ * leader's log).  advanced_out[g] (nullable) = 1 where the commit moved
+ * (maybeCommit's return value). */
+int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
+                                const uint64_t* term_start,
+                                uint64_t* committed, uint8_t* advanced_out,
+                                void* stream);
+
+/* ----------------------------------------------------------------------- */
+/* Synthetic workload generators (bench/test inputs)        */
+/* ----------------------------------------------------------------------- */
+
+/* Counter-based, so every shard/device/CPU regenerates identical inputs:
+ * r(g, slot, field) = splitmix64(seed ^ (g << 12 | slot << 4 | field)).
+ * g_begin offsets the global group number (sharding). */
+int qb_dev_synth_fixed(uint64_t seed, uint32_t n, uint64_t G, uint64_t g_begin,
+                       uint64_t* match, void* voted, void* granted,
+                       uint64_t* term_start, void* stream);
+/* Host-side: group sizes and CSR offsets of the ragged config (s_g = n_g +
+ * learners_g).  off has G+1 entries.  Returns QB_OK or QB_EINVAL if the total
+ * overflows uint32. */
+int qb_host_synth_csr_offsets(uint64_t seed, uint64_t G, uint64_t g_begin,
+                              uint32_t* off);
+/* Device fill of the ragged (kind 0) or joint 5+5 (kind 1) config given off. */
+int qb_dev_synth_csr(uint64_t seed, int kind, uint64_t G, uint64_t g_begin,
+                     const uint32_t* off, uint64_t* match, uint32_t* cfg,
+                     uint32_t* votes, void* stream);
+/* Host-side joint offsets: s_g = 10 - overlap_g. */
+int qb_host_synth_joint_offsets(uint64_t seed, uint64_t G, uint64_t g_begin,
+                                uint32_t* off);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QUORUM_BATCH_H */

@@ -1,0 +1,158 @@
+"""ctypes access to the C oracle (oracle/liborc_quorum.so) — tests/bench only.
+
+Builds the library on first use if it is missing (gcc is on both the build
+container and the GPU box).  Also provides numpy-level wrappers so tests can
+compare the HIP engine with the oracle on identical seeded inputs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORC_DIR = os.path.join(ROOT, "oracle")
+ORC_PATH = os.path.join(ORC_DIR, "liborc_quorum.so")
+
+_p, _u64, _u32, _i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+SIG = {
+    "orc_gen_fixed": (None, [_u64, _u32, _u64, _u64, _p, _p, _p, _p]),
+    "orc_gen_csr": (_i32, [_u64, _i32, _u64, _u64, _p, _p, _p, _p]),
+    "orc_csr_eval": (None, [_u64, _p, _p, _p, _p, _p, _p]),
+    "orc_fixed_eval": (None, [_u32, _u64, _p, _p, _p, _p, _p]),
+    "orc_csr_quorum_active": (None, [_u64, _p, _p, _p]),
+    "orc_group_maps_size": (C.c_size_t, []),
+    "orc_faithful_build_fixed": (None, [_u32, _u64, _p, _p, _p, _p]),
+    "orc_faithful_eval": (None, [_u64, _p, _p, _p]),
+    "orc_faithful_eval_mt": (None, [_u64, _p, _p, _p, _i32]),
+    "orc_fixed_eval_mt": (None, [_u32, _u64, _p, _p, _p, _p, _p, _i32]),
+    "orc_csr_eval_mt": (None, [_u64, _p, _p, _p, _p, _p, _p, _i32]),
+    "orc_fixed_appresp_sequential": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                            _p, _p, _p, _p, _p]),
+    "orc_fixed_commit_all": (None, [_u32, _u64, _p, _p, _p, _p]),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORC_DIR, "quorum_oracle.c")
+        if not os.path.exists(ORC_PATH) or os.path.getmtime(ORC_PATH) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORC_DIR])
+        lib = C.CDLL(ORC_PATH)
+        for k, (r, a) in SIG.items():
+            f = getattr(lib, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = lib
+    return _lib
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def mask_np(n):
+    return np.uint8 if n <= 8 else np.uint16
+
+
+def gen_fixed(seed, n, G, g_begin=0):
+    lib = load()
+    match = np.empty((n, G), np.uint64)
+    vd = np.empty(G, mask_np(n))
+    gr = np.empty(G, mask_np(n))
+    ts = np.empty(G, np.uint64)
+    lib.orc_gen_fixed(seed, n, G, g_begin, ptr(match), ptr(vd), ptr(gr), ptr(ts))
+    return match, vd, gr, ts
+
+
+def gen_csr(seed, kind, G, g_begin=0):
+    lib = load()
+    off = np.empty(G + 1, np.uint32)
+    # upper bound on slots: 11 (ragged) / 10 (joint)
+    match = np.empty(G * 11 + 2, np.uint64)
+    cfg = np.empty(G, np.uint32)
+    votes = np.empty(G, np.uint32)
+    rc = lib.orc_gen_csr(seed, {"ragged": 0, "joint": 1}[kind], G, g_begin, ptr(off), ptr(match),
+                         ptr(cfg), ptr(votes))
+    assert rc == 0
+    return off, match[:off[-1]].copy(), cfg, votes
+
+
+def fixed_eval(n, match, vd, gr, threads=1):
+    lib = load()
+    G = match.shape[1] if n else len(vd)
+    commit = np.empty(G, np.uint64)
+    vote = np.empty(G, np.uint8)
+    if threads > 1:
+        lib.orc_fixed_eval_mt(n, G, ptr(match), ptr(vd), ptr(gr), ptr(commit), ptr(vote), threads)
+    else:
+        lib.orc_fixed_eval(n, G, ptr(match), ptr(vd), ptr(gr), ptr(commit), ptr(vote))
+    return commit, vote
+
+
+def csr_eval(off, match, cfg, votes, threads=1):
+    lib = load()
+    G = len(cfg)
+    commit = np.empty(G, np.uint64)
+    vote = np.empty(G, np.uint8)
+    m = match if match.size else np.zeros(1, np.uint64)
+    if threads > 1:
+        lib.orc_csr_eval_mt(G, ptr(off), ptr(m), ptr(cfg), ptr(votes), ptr(commit), ptr(vote),
+                            threads)
+    else:
+        lib.orc_csr_eval(G, ptr(off), ptr(m), ptr(cfg), ptr(votes), ptr(commit), ptr(vote))
+    return commit, vote
+
+
+def quorum_active(cfg, active):
+    lib = load()
+    won = np.empty(len(cfg), np.uint8)
+    lib.orc_csr_quorum_active(len(cfg), ptr(cfg), ptr(active), ptr(won))
+    return won
+
+
+def faithful_maps(n, match, vd, gr):
+    lib = load()
+    G = match.shape[1]
+    maps = np.empty(G * lib.orc_group_maps_size(), np.uint8)
+    lib.orc_faithful_build_fixed(n, G, ptr(match), ptr(vd), ptr(gr), ptr(maps))
+    return maps
+
+
+def faithful_eval(maps, G, threads=1):
+    lib = load()
+    commit = np.empty(G, np.uint64)
+    vote = np.empty(G, np.uint8)
+    if threads > 1:
+        lib.orc_faithful_eval_mt(G, ptr(maps), ptr(commit), ptr(vote), threads)
+    else:
+        lib.orc_faithful_eval(G, ptr(maps), ptr(commit), ptr(vote))
+    return commit, vote
+
+
+def appresp_sequential(n, G, rec, state):
+    """Sequential reference semantics; ``state`` (dict of numpy arrays) is
+    updated in place.  Returns the stats array."""
+    lib = load()
+    stats = np.zeros(8, np.uint64)
+    group, flags, index, term = rec
+    rc = lib.orc_fixed_appresp_sequential(
+        n, G, len(group), ptr(group), ptr(flags), ptr(index), ptr(term), ptr(state["term"]),
+        ptr(state["term_start"]), ptr(state.get("last_index")), ptr(state["match"]),
+        ptr(state.get("next")), ptr(state["active"]), ptr(state["committed"]),
+        ptr(state["stepped_down"]), ptr(stats))
+    assert rc == 0, "a record acked past the leader's last index"
+    return stats
+
+
+def commit_all(n, match, term_start, committed):
+    lib = load()
+    G = len(committed)
+    adv = np.empty(G, np.uint8)
+    lib.orc_fixed_commit_all(n, G, ptr(match), ptr(term_start), ptr(committed), ptr(adv))
+    return adv

@@ -1,0 +1,156 @@
+"""GPU parity for the tracker path: MsgAppResp batches (scatter-max of
+MaybeUpdate, RecentActive, term filter, step-down ordering) followed by the
+commit-advance kernel, against the sequential one-record-at-a-time oracle."""
+import numpy as np
+import pytest
+import torch
+
+from etcd_amd.quorum import batch
+from tests import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MAX = (1 << 64) - 1
+
+
+def _tracker_from(n, st, track_next=True):
+    G = len(st["term"])
+    tr = batch.FixedTracker(n, G, DEV, track_next=track_next)
+    tr.match.copy_(batch.from_u64(st["match"], DEV))
+    if track_next:
+        tr.next.copy_(batch.from_u64(st["next"], DEV))
+    act = np.zeros(G + (G & 1), np.uint16)
+    act[:G] = st["active"]
+    tr.active.copy_(torch.from_numpy(act.view(np.int16)))
+    tr.term.copy_(batch.from_u64(st["term"], DEV))
+    tr.term_start.copy_(batch.from_u64(st["term_start"], DEV))
+    tr.committed.copy_(batch.from_u64(st["committed"], DEV))
+    return tr
+
+
+def _compare(tr, st, n, G):
+    assert np.array_equal(batch.as_u64(tr.match), st["match"])
+    if tr.next is not None:
+        assert np.array_equal(batch.as_u64(tr.next), st["next"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+
+
+def test_progress_update_table(tables):
+    """TestProgressUpdate (tracker/progress_test.go:149-179) through the
+    scatter-max kernel: one group per table row."""
+    t = tables["TestProgressUpdate"]
+    cases = t["cases"]
+    G = len(cases)
+    tr = batch.FixedTracker(1, G, DEV, track_next=True)
+    tr.match.fill_(t["prev_match"])
+    tr.next.fill_(t["prev_next"])
+    tr.term.fill_(1)
+    b = batch.AppRespBatch.from_numpy(np.arange(G), np.zeros(G), [c["update"] for c in cases],
+                                      np.ones(G), device=DEV)
+    tr.apply_appresp(b)
+    assert tr.match[0].cpu().tolist() == [c["wm"] for c in cases]
+    assert tr.next[0].cpu().tolist() == [c["wn"] for c in cases]
+
+
+def test_commit_table(tables):
+    """TestCommit (raft/raft_test.go:1127-1174) via the commit-advance kernel:
+    n voters with the table's matches, term_start = first index of smTerm."""
+    by_n = {}
+    for tc in tables["TestCommit"]["cases"]:
+        by_n.setdefault(len(tc["matches"]), []).append(tc)
+    for n, cases in by_n.items():
+        G = len(cases)
+        tr = batch.FixedTracker(n, G, DEV)
+        m = np.array([c["matches"] for c in cases], np.uint64).T.copy()
+        ts = []
+        for c in cases:
+            same = [i for i, t in c["log"] if t == c["term"]]
+            ts.append(min(same) if same else MAX)
+        tr.match.copy_(batch.from_u64(m, DEV))
+        tr.term_start.copy_(batch.from_u64(ts, DEV))
+        adv = torch.zeros(G, dtype=torch.uint8, device=DEV)
+        tr.commit_advance(adv)
+        assert batch.as_u64(tr.committed).tolist() == [c["want"] for c in cases]
+        assert adv.cpu().tolist() == [int(c["want"] > 0) for c in cases]
+
+
+def _random_state(rng, n, G):
+    match, _, _, ts = oc.gen_fixed(0x5EED0005, n, G)
+    last = match[0].copy()
+    term = rng.integers(2, 9, size=G).astype(np.uint64)
+    st = {"match": match.copy(), "next": (match + np.uint64(1)).copy(),
+          "active": np.zeros(G, np.uint16), "term": term, "term_start": ts,
+          "last_index": last, "committed": np.zeros(G, np.uint64),
+          "stepped_down": np.zeros(G, np.uint8)}
+    oc.commit_all(n, st["match"], ts, st["committed"])  # initial maybeCommit invariant
+    return st
+
+
+def _random_batch(rng, n, G, M, st, stale=0.01, higher=0.0, reject=0.02, nonmember=0.0,
+                  bad=0.0):
+    group = rng.integers(0, G, size=M).astype(np.uint32)
+    slot = rng.integers(1 if n > 1 else 0, n, size=M).astype(np.uint8)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 96, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    term = st["term"][group].copy()
+    u = rng.random(M)
+    term = np.where(u < stale, term - np.uint64(1), term)
+    term = np.where((u >= stale) & (u < stale + higher), term + np.uint64(1), term)
+    rej = rng.random(M) < reject
+    if nonmember:
+        slot = np.where(rng.random(M) < nonmember, np.uint8(n + 1), slot).astype(np.uint8)
+    if bad:
+        group = np.where(rng.random(M) < bad, np.uint32(G + 5), group).astype(np.uint32)
+    flags = (slot | (rej.astype(np.uint8) << 7)).astype(np.uint8)
+    return group, slot, index, term.astype(np.uint64), rej, flags
+
+
+@pytest.mark.parametrize("n,G,M,kw", [
+    (5, 4096, 8192, {}),
+    (5, 1000, 20000, {"higher": 0.002, "nonmember": 0.01, "bad": 0.01}),   # duplicates heavy
+    (3, 20000, 20000, {"reject": 0.2, "stale": 0.1}),
+    (7, 5000, 30000, {"higher": 0.01}),
+    (1, 100, 1000, {"higher": 0.05}),
+])
+def test_appresp_then_commit_vs_sequential(n, G, M, kw):
+    rng = np.random.default_rng(n * 7 + G)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st)
+    seq = {k: v.copy() for k, v in st.items()}
+    for step in range(3):
+        group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, **kw)
+        stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
+        b = batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV)
+        tr.apply_appresp(b)
+        tr.commit_advance()
+        _compare(tr, seq, n, G)
+        got = tr.stats_dict()
+        assert got["applied"] == stats[0] and got["rejected"] == stats[1]
+        assert got["stale_term"] == stats[2] and got["non_member"] == stats[3]
+        assert got["higher_term"] == stats[4] and got["bad_group"] == stats[5]
+        assert got["after_stepdown"] == stats[6]
+        # caller protocol: stepped-down groups are handed to the scalar path
+        # (becomeFollower) and the marker is re-armed before the next batch
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
+
+
+@pytest.mark.timeout(300)
+def test_appresp_full_size_16m():
+    """BASELINE config 5 shape on one GPU (16M 5-voter groups, one MsgAppResp
+    per group on average, 1% stale-term): end state equals the sequential
+    oracle."""
+    n, G = 5, 1 << 24
+    rng = np.random.default_rng(55)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st, track_next=False)
+    st.pop("next")
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, G, st, reject=0.0)
+    oc.appresp_sequential(n, G, (group, flags, index, term), st)
+    tr.apply_appresp(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    tr.commit_advance()
+    assert np.array_equal(batch.as_u64(tr.match), st["match"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
