@@ -9,6 +9,12 @@ outputs) stay resident in HBM and are visited round-robin, so every step
 streams its batch from HBM instead of the 256 MB Infinity Cache (the
 MALL-warm single-batch rate is reported beside it as ``value_mall_warm``).
 
+Launch pipeline: consecutive steps are independent batches, so they are
+issued round-robin on ``--streams`` HIP streams (default 2): the tail of one
+launch overlaps the ramp of the next.  HIP events on the launch streams bracket
+the timed region; the per-launch duration used for the roofline is the
+region's device time / K.
+
 Multi-GPU: one process per GPU (torch.distributed, RCCL), groups sharded by
 global group number (weak scaling, no collective in the timed region); for
 N > 1 the node-wide all-gather of one batch's commit/vote vectors is timed
@@ -125,6 +131,7 @@ def main():
     ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
     ap.add_argument("--voters", type=int, default=5)
     ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -139,58 +146,61 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     n, G, B, K, W = args.voters, args.groups, max(1, args.batches), args.steps, args.warmup
+    S = max(1, args.streams)
     lib = _lib.load()
     fn = lib.qb_dev_fixed_committed_vote
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    main_stream = torch.cuda.current_stream(dev)
+    msp = main_stream.cuda_stream
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
     # B resident batches; global group numbers shard by rank (weak scaling)
     groups = [batch.FixedGroups.synth(SEED, n, G, g_begin=(rank * B + b) * G, device=dev)
               for b in range(B)]
     outs = [(torch.empty(G, dtype=torch.int64, device=dev),
              torch.empty(G, dtype=torch.uint8, device=dev)) for _ in range(B)]
-    call_args = [(n, G, g.match.data_ptr(), g.voted.data_ptr(), g.granted.data_ptr(),
-                  c.data_ptr(), v.data_ptr(), sp) for g, (c, v) in zip(groups, outs)]
+    # per step k: batch k % B on stream k % S (precomputed ctypes argument tuples)
+    call_args = [[(n, G, g.match.data_ptr(), g.voted.data_ptr(), g.granted.data_ptr(),
+                   c.data_ptr(), v.data_ptr(), st.cuda_stream)
+                  for g, (c, v) in zip(groups, outs)] for st in streams]
     torch.cuda.synchronize()
 
-    def launch(k):
-        rc = fn(*call_args[k % B])
-        if rc:
-            _lib.check(rc, "qb_dev_fixed_committed_vote")
-
-    for k in range(W):
-        launch(k)
-    ev = HipEvents(2 * K + 2)
-    rec = ev.record
+    def run_steps(count, fixed_batch=None):
+        for st in streams:
+            st.wait_stream(main_stream)
+        for k in range(count):
+            b = k % B if fixed_batch is None else fixed_batch
+            rc = fn(*call_args[k % S][b])
+            if rc:
+                _lib.check(rc, "qb_dev_fixed_committed_vote")
+        for st in streams:
+            main_stream.wait_stream(st)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    run_steps(W)
+    ev = HipEvents(4)
     barrier()
     t0 = time.perf_counter()
-    for k in range(K):
-        rec(ev.ev[2 * k], sp)
-        launch(k)
-        rec(ev.ev[2 * k + 1], sp)
+    ev.record(ev.ev[0], msp)
+    run_steps(K)
+    ev.record(ev.ev[1], msp)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    kern_ms = [ev.elapsed_ms(2 * k, 2 * k + 1) for k in range(K)]
-    ev.close()
-    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    avg_kernel_s = ev.elapsed_ms(0, 1) / 1e3 / K
 
     # MALL-warm single-batch rate (informational)
-    for _ in range(W):
-        launch(0)
+    run_steps(W, fixed_batch=0)
     torch.cuda.synchronize()
     tw = time.perf_counter()
-    for _ in range(K):
-        launch(0)
+    run_steps(K, fixed_batch=0)
     torch.cuda.synchronize()
     warm_elapsed = time.perf_counter() - tw
+    ev.close()
 
     allgather_ms = None
     if world > 1:
@@ -237,7 +247,8 @@ def main():
                 "workload": "BASELINE configs[1]: 1M groups x 5 voters CommittedIndex + "
                             "VoteResult, uint64 indexes, one MI355X per shard",
                 "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA",
-                "batches_resident": B, "parallelism": f"groups sharded by id over {world} GPU(s)",
+                "batches_resident": B, "streams": S,
+                "parallelism": f"groups sharded by id over {world} GPU(s)",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -246,6 +257,9 @@ def main():
                 "kernel": f"k_fixed<{n},4,true,true>",
                 "bytes_per_group": bpg,
                 "avg_kernel_us": avg_kernel_s * 1e6,
+                "timing": (f"HIP events around the timed region on the launch streams; per-launch "
+                           f"duration = region device time / K with {S} stream(s) overlapping "
+                           f"consecutive launches"),
             },
             "value_mall_warm": world * G * K / warm_elapsed,
             "allgather_ms": allgather_ms,

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from two rocprofv3 PMC passes of the bench command.
+
+Recipe (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
+  pass 1: rocprofv3 --pmc FETCH_SIZE --output-format csv -d D1 -o run -- python3 bench.py ...
+  pass 2: rocprofv3 --pmc WRITE_SIZE --output-format csv -d D2 -o run -- python3 bench.py ...
+(separate passes: FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).
+Counter values are KiB.  gfx950 correction: FETCH_SIZE reports exactly half
+of the bytes of a wide (16 B/lane) coalesced streaming read, so the read side
+is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.  The narrow
+(2 B/lane) mask loads and vote stores are a small uncalibrated share (4 of the
+51 bytes per group) and are treated like the wide ones.
+
+Only the timed HBM-rotating dispatches are used: dispatches [W, W+K) of the
+kernel in launch order.
+
+    python tools/pmc_traffic.py --fetch D1/run_counter_collection.csv \
+        --write D2/run_counter_collection.csv --kernel k_fixed --warmup 5 --steps 50 \
+        --key fixed_n5_G1048576 --algo-bytes 53477376 --out profiles/pmc_traffic.json
+"""
+import argparse
+import csv
+import json
+import os
+
+import numpy as np
+
+
+def per_dispatch(path, kernel, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if kernel not in r.get("Kernel_Name", ""):
+            continue
+        if r.get("Counter_Name") != counter:
+            continue
+        d = int(r["Dispatch_Id"])
+        vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--kernel", default="k_fixed")
+    ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--key", required=True)
+    ap.add_argument("--algo-bytes", type=float, required=True, help="algorithmic bytes/launch")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f = per_dispatch(a.fetch, a.kernel, "FETCH_SIZE")[a.warmup:a.warmup + a.steps]
+    w = per_dispatch(a.write, a.kernel, "WRITE_SIZE")[a.warmup:a.warmup + a.steps]
+    if not f or not w:
+        raise SystemExit("no matching dispatches")
+    fk, wk = float(np.median(f)), float(np.median(w))
+    read_b = 2.0 * fk * 1024.0   # gfx950 FETCH_SIZE x2 correction
+    write_b = wk * 1024.0
+    rec = {
+        "kernel": a.kernel, "dispatches": len(f),
+        "fetch_size_kib_median_raw": fk, "write_size_kib_median": wk,
+        "read_bytes_corrected": read_b, "write_bytes": write_b,
+        "hbm_bytes_per_launch": read_b + write_b,
+        "algorithmic_bytes_per_launch": a.algo_bytes,
+        "traffic_over_algorithmic": (read_b + write_b) / a.algo_bytes,
+        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; "
+                  "FETCH_SIZE x2 (gfx950 wide-read correction); KiB->bytes x1024",
+    }
+    doc = {}
+    if os.path.exists(a.out):
+        doc = json.load(open(a.out))
+    doc[a.key] = rec
+    with open(a.out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
