@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 from etcd_amd import _lib  # noqa: E402
 from etcd_amd.quorum import batch  # noqa: E402
+from etcd_amd.shard import allgather_results  # noqa: E402
 
 METRIC = "raft groups quorum-evaluated/sec (1 and 8 GPUs) + % peak HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -207,19 +208,16 @@ def main():
         t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, warm_elapsed, avg_kernel_s = (float(x) for x in t.tolist())
-        # node-wide result: all-gather one batch's commit (u64) and vote (u8) vectors
+        # node-wide result: all-gather one batch's commit (u64) and vote (u8)
+        # vectors over RCCL (etcd_amd.shard)
         c, v = outs[0]
-        call = torch.empty(world * G, dtype=torch.int64, device=dev)
-        vall = torch.empty(world * G, dtype=torch.uint8, device=dev)
         for _ in range(3):
-            dist.all_gather_into_tensor(call, c)
-            dist.all_gather_into_tensor(vall, v)
+            allgather_results(c, v, world * G)
         barrier()
         ta = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            dist.all_gather_into_tensor(call, c)
-            dist.all_gather_into_tensor(vall, v)
+            allgather_results(c, v, world * G)
         barrier()
         allgather_ms = (time.perf_counter() - ta) / reps * 1e3
 

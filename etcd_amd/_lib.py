@@ -37,6 +37,15 @@ SIGNATURES = {
     "qb_abi_version": (_i32, []),
     "qb_last_error": (C.c_char_p, []),
     "qb_device_count": (_i32, []),
+    "qb_set_device": (_i32, [_i32]),
+    "qb_malloc": (_i32, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    "qb_free": (_i32, [_p]),
+    "qb_memset_async": (_i32, [_p, _i32, C.c_size_t, _p]),
+    "qb_copy_h2d_async": (_i32, [_p, _p, C.c_size_t, _p]),
+    "qb_copy_d2h_async": (_i32, [_p, _p, C.c_size_t, _p]),
+    "qb_stream_create": (_i32, [C.POINTER(C.c_void_p)]),
+    "qb_stream_destroy": (_i32, [_p]),
+    "qb_stream_sync": (_i32, [_p]),
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_committed_vote": (_i32, [_u64, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_validate": (_i32, [_u64, _p, _p, _p]),

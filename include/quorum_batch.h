@@ -98,6 +98,20 @@ const char* qb_last_error(void);
 /* Number of visible HIP devices (0 without a GPU); never fails. */
 int qb_device_count(void);
 
+/* Device memory and streams for callers without their own HIP runtime
+ * bindings (the Go cgo package).  Thin wrappers over hipMalloc / hipFree /
+ * hipMemcpyAsync / hipStreamCreate; *_async copies are ordered on the stream
+ * and the host buffer must stay alive until qb_stream_sync returns. */
+int qb_set_device(int device);
+int qb_malloc(size_t bytes, void** out);
+int qb_free(void* ptr);
+int qb_memset_async(void* dst, int value, size_t bytes, void* stream);
+int qb_copy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
+int qb_copy_d2h_async(void* dst, const void* src, size_t bytes, void* stream);
+int qb_stream_create(void** out);
+int qb_stream_destroy(void* stream);
+int qb_stream_sync(void* stream);
+
 /* ----------------------------------------------------------------------- */
 /* Quorum math (raft/quorum)                                               */
 /* ----------------------------------------------------------------------- */

@@ -1,0 +1,80 @@
+"""N > 1 path on CPU: world_size 2 (and 3) gloo processes each evaluate their
+shard of the counter-generated groups and all-gather the node-wide result.
+
+No GPU exists here, so each rank's shard is evaluated by the C oracle as a
+stand-in for the kernel; what is under test is the sharding (ranges, global
+group numbering, independent regeneration per shard) and the gather."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from etcd_amd.shard import shard_range
+
+SEED = 0x5EED0003
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, kind, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.shard import allgather_results
+        from tests import oracle_c as oc
+        b, e = shard_range(total, world, rank)
+        if kind == "fixed":
+            match, vd, gr, _ = oc.gen_fixed(SEED, 5, e - b, g_begin=b)
+            c, v = oc.fixed_eval(5, match, vd, gr)
+        else:
+            off, m, cfg, votes = oc.gen_csr(SEED, kind, e - b, g_begin=b)
+            c, v = oc.csr_eval(off, m, cfg, votes)
+        gc, gv = allgather_results(torch.from_numpy(c.view(np.int64)), torch.from_numpy(v), total)
+        if rank == 0:
+            q.put((gc.numpy().view(np.uint64).copy(), gv.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partition():
+    for total in (0, 1, 7, 100, 1 << 20):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(total, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in rs]
+            assert max(sizes) - min(sizes) <= 1 and sizes[0] == max(sizes)
+
+
+@pytest.mark.parametrize("world,total,kind", [(2, 10001, "fixed"), (2, 4096, "ragged"),
+                                              (3, 5000, "joint")])
+def test_sharded_eval_allgather_equals_single_process(world, total, kind):
+    from tests import oracle_c as oc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, kind, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    gc, gv = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    if kind == "fixed":
+        match, vd, gr, _ = oc.gen_fixed(SEED, 5, total)
+        ec, ev = oc.fixed_eval(5, match, vd, gr)
+    else:
+        off, m, cfg, votes = oc.gen_csr(SEED, kind, total)
+        ec, ev = oc.csr_eval(off, m, cfg, votes)
+    assert np.array_equal(gc, ec) and np.array_equal(gv, ev)
