@@ -47,8 +47,8 @@ SIGNATURES = {
     "qb_stream_destroy": (_i32, [_p]),
     "qb_stream_sync": (_i32, [_p]),
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
-    "qb_dev_csr_committed_vote": (_i32, [_u64, _p, _p, _p, _p, _p, _p, _p]),
-    "qb_dev_csr_validate": (_i32, [_u64, _p, _p, _p]),
+    "qb_dev_csr_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p]),
+    "qb_dev_csr_validate": (_i32, [_u64, _u32, _p, _p, _p]),
     "qb_dev_csr_quorum_active": (_i32, [_u64, _p, _p, _p, _p]),
     "qb_dev_fixed_apply_appresp": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                           _p, _p, _p]),

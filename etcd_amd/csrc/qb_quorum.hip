@@ -215,21 +215,26 @@ extern "C" int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_
 //
 // A workgroup owns kBlock consecutive groups.  Their slots are one contiguous
 // run of match[] (group-major CSR), so the run is staged into LDS with
-// coalesced 16-byte loads and each thread then reads its own <= 16 slots from
-// LDS.  Non-member slots (learners, other half) are fed as 0: zeros sort to
-// the bottom and leave the q-th largest unchanged for q <= n, exactly the
-// fill-with-zero of majority.go:149-161.  The network width W is chosen per
-// wave (uniform branch) from the wave's widest group.
+// coalesced 16-byte nontemporal loads and each thread then reads its own
+// slots from LDS.  Non-member slots (learners, the other half) are fed as 0:
+// zeros sort to the bottom and leave the q-th largest unchanged for q <= n,
+// exactly the fill-with-zero of majority.go:149-161.
+//
+// Occupancy is what sets this kernel's speed: the table's
+// max_slots bound (WMAX) caps both the LDS run buffer (kBlock * WMAX u64) and
+// the widest compare-exchange network compiled in, which sets the VGPR count.
+// Within that bound the network width W in {4, 8, 12, 16} is chosen per wave
+// from the wave's widest group (uniform branch).  Majority-only waves run one
+// masked sort; a wave with a joint group runs one sort of all slots carrying
+// 2-bit membership tags and reads both halves' q-th largest from it.
 
 namespace qb {
 
-constexpr int kCsrLds = kBlock * QB_MAX_SLOTS + 2;  // +2: 16-byte head alignment
-
 template <int W>
-__device__ __forceinline__ u64 csr_select(const u64* lds, u32 lo, u32 s, u32 mask) {
+__device__ __forceinline__ u64 csr_select(const u64* src, u32 s, u32 mask) {
   u64 v[W];
 #pragma unroll
-  for (int j = 0; j < W; ++j) v[j] = (u32(j) < s && ((mask >> j) & 1u)) ? lds[lo + j] : 0ull;
+  for (int j = 0; j < W; ++j) v[j] = (u32(j) < s && ((mask >> j) & 1u)) ? src[j] : 0ull;
   sort_net<W>(v);
   const int n = __popc(mask);
   if (n == 0) return kInf;  // majority.go:128-133
@@ -240,17 +245,82 @@ __device__ __forceinline__ u64 csr_select(const u64* lds, u32 lo, u32 s, u32 mas
   return r;
 }
 
-template <int W>
-__device__ __forceinline__ u64 csr_ci(const u64* lds, u32 lo, u32 s, u32 min_, u32 mout) {
-  u64 ci = csr_select<W>(lds, lo, s, min_);
-  if (mout != 0) {  // joint.go:49-56; an empty half is ∞ and drops out of the min
-    const u64 c2 = csr_select<W>(lds, lo, s, mout);
-    ci = c2 < ci ? c2 : ci;
-  }
-  return ci;
+__device__ __forceinline__ void cmpx_tag(u64& a, u64& b, u32& ta, u32& tb) {
+  const bool sw = b < a;
+  const u64 lo = sw ? b : a, hi = sw ? a : b;
+  const u32 tl = sw ? tb : ta, th = sw ? ta : tb;
+  a = lo;
+  b = hi;
+  ta = tl;
+  tb = th;
 }
 
-template <bool CI, bool VOTE>
+template <class Net, int... K>
+__device__ __forceinline__ void run_net_tag(u64* v, u32* t, std::integer_sequence<int, K...>) {
+  ((cmpx_tag(v[Net::A[K]], v[Net::B[K]], t[Net::A[K]], t[Net::B[K]])), ...);
+}
+
+// JointConfig.CommittedIndex (joint.go:49-56): one ascending sort of all
+// slots, tag bit 0 = incoming member, bit 1 = outgoing member; walking down
+// from the largest, the q-th member of a half is that half's CommittedIndex.
+// An empty half is ∞ and drops out of the min.
+template <int W>
+__device__ __forceinline__ u64 csr_joint(const u64* src, u32 s, u32 min_, u32 mout) {
+  u64 v[W];
+  u32 t[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const bool live = u32(j) < s;
+    v[j] = live ? src[j] : 0ull;
+    t[j] = live ? (((min_ >> j) & 1u) | (((mout >> j) & 1u) << 1)) : 0u;
+  }
+  run_net_tag<SortNet<W>>(v, t, std::make_integer_sequence<int, SortNet<W>::K>{});
+  const int qi = __popc(min_) / 2 + 1, qo = __popc(mout) / 2 + 1;
+  int ci = 0, co = 0;
+  u64 ri = kInf, ro = kInf;
+#pragma unroll
+  for (int j = W - 1; j >= 0; --j) {
+    ci += int(t[j] & 1u);
+    co += int(t[j] >> 1);
+    ri = (ci == qi && (t[j] & 1u)) ? v[j] : ri;
+    ro = (co == qo && (t[j] >> 1)) ? v[j] : ro;
+  }
+  return ro < ri ? ro : ri;
+}
+
+template <int W>
+__device__ __forceinline__ u64 csr_ci(const u64* src, u32 s, u32 min_, u32 mout) {
+  if (__ballot(mout != 0) == 0) return csr_select<W>(src, s, min_);
+  return csr_joint<W>(src, s, min_, mout);
+}
+
+__device__ __forceinline__ u32 wave_max(u32 x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const u32 y = u32(__shfl_xor(int(x), o, 64));
+    x = y > x ? y : x;
+  }
+  return __builtin_amdgcn_readfirstlane(x);  // wave-uniform, scalar branch
+}
+
+// Network width = the wave's widest group (exact, 4..WMAX): e.g. W = 11 for
+// a ragged wave with an 11-slot group (38 compare-exchanges vs 42 at 12).
+template <int W, int WMAX>
+__device__ __forceinline__ u64 csr_ci_width(u32 wmax, const u64* src, u32 s, u32 min_, u32 mout) {
+  if constexpr (W >= WMAX) {
+    return csr_ci<WMAX>(src, s, min_, mout);
+  } else {
+    if (wmax <= u32(W)) return csr_ci<W>(src, s, min_, mout);
+    return csr_ci_width<W + 1, WMAX>(wmax, src, s, min_, mout);
+  }
+}
+
+template <int WMAX>
+__device__ __forceinline__ u64 csr_ci_dispatch(const u64* src, u32 s, u32 min_, u32 mout) {
+  return csr_ci_width<(WMAX < 4 ? WMAX : 4), WMAX>(wave_max(s), src, s, min_, mout);
+}
+
+template <int WMAX, bool CI, bool VOTE>
 __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ off,
                                                 const u64* __restrict__ match,
                                                 const u32* __restrict__ cfg,
@@ -260,46 +330,43 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
   const u64 g0 = u64(blockIdx.x) * kBlock;
   const u64 g = g0 + threadIdx.x;
   const bool live = g < G;
-  const u32 c = live ? cfg[g] : 0u;
+  const u32 c = live ? ld_nt(cfg + g) : 0u;
   const u32 min_ = c & 0xFFFFu, mout = c >> 16;
 
   if constexpr (CI) {
-    __shared__ __attribute__((aligned(16))) u64 lds[kCsrLds];
+    constexpr u32 kCap = kBlock * WMAX + 2;  // +2: 16-byte head alignment
+    __shared__ __attribute__((aligned(16))) u64 lds[kCap];
     const u64 gend = (g0 + kBlock < G) ? g0 + kBlock : G;
     const u32 base = off[g0], end = off[gend], total = off[G];
     const u32 abase = base & ~1u;
-    const u32 npair = (end - abase + 1u) >> 1;
-    using V2 = u32 __attribute__((ext_vector_type(4)));
+    // A table that breaks its max_slots bound must not write past the LDS run
+    // buffer (results for such a table are unspecified, never out of bounds).
+    const u32 span = end - abase < kCap ? end - abase : kCap;
+    const u32 npair = (span + 1u) >> 1;
+    using V = u32 __attribute__((ext_vector_type(4)));
     for (u32 i = threadIdx.x; i < npair; i += kBlock) {
       const u32 idx = abase + 2u * i;
       if (idx + 1u < total) {
-        reinterpret_cast<V2*>(lds)[i] = *reinterpret_cast<const V2*>(match + idx);
+        reinterpret_cast<V*>(lds)[i] = ld_nt(reinterpret_cast<const V*>(match + idx));
       } else {
         lds[2u * i] = match[idx];
       }
     }
-    __syncthreads();
     u32 lo = 0, s = 0;
     if (live) {
       const u32 a = off[g], b = off[g + 1];
       lo = a - abase;
       s = b - a;
-      s = s > QB_MAX_SLOTS ? QB_MAX_SLOTS : s;
+      s = s > WMAX ? WMAX : s;
+      lo = lo + s <= kCap ? lo : 0;
     }
-    u64 ci;
-    // Wave-uniform width choice (no divergence inside the network).
-    if (__ballot(s > 8) == 0) {
-      ci = (__ballot(s > 4) == 0) ? csr_ci<4>(lds, lo, s, min_, mout)
-                                  : csr_ci<8>(lds, lo, s, min_, mout);
-    } else {
-      ci = (__ballot(s > 12) == 0) ? csr_ci<12>(lds, lo, s, min_, mout)
-                                   : csr_ci<16>(lds, lo, s, min_, mout);
-    }
-    if (live) commit[g] = ci;
+    __syncthreads();
+    const u64 ci = csr_ci_dispatch<WMAX>(lds + lo, s, min_, mout);
+    if (live) st_nt(commit + g, ci);
   }
   if constexpr (VOTE) {
     if (live) {
-      const u32 w = votes[g];
+      const u32 w = ld_nt(votes + g);
       const u32 vd = w & 0xFFFFu, gr = (w >> 16) & vd;
       const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & gr), __popc(min_ & vd));
       const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & gr), __popc(mout & vd));
@@ -308,47 +375,64 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
   }
 }
 
-__global__ void k_csr_validate(u64 G, const u32* __restrict__ off, u64* __restrict__ bad) {
+template <int WMAX>
+static void launch_csr_w(u64 G, const u32* off, const u64* match, const u32* cfg,
+                         const u32* votes, u64* commit, u8* vote, hipStream_t st) {
+  const dim3 grid(grid_for(G));
+  if (commit && vote)
+    hipLaunchKernelGGL((k_csr<WMAX, true, true>), grid, dim3(kBlock), 0, st, G, off, match, cfg,
+                       votes, commit, vote);
+  else if (commit)
+    hipLaunchKernelGGL((k_csr<WMAX, true, false>), grid, dim3(kBlock), 0, st, G, off, match,
+                       cfg, votes, commit, vote);
+  else
+    hipLaunchKernelGGL((k_csr<WMAX, false, true>), grid, dim3(kBlock), 0, st, G, off, match,
+                       cfg, votes, commit, vote);
+}
+
+__global__ void k_csr_validate(u64 G, u32 max_slots, const u32* __restrict__ off,
+                               u64* __restrict__ bad) {
   const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (g >= G) return;
   const u32 a = off[g], b = off[g + 1];
-  bool ok = b >= a && b - a <= QB_MAX_SLOTS;
+  bool ok = b >= a && b - a <= max_slots;
   if (g == 0) ok = ok && a == 0;
   if (!ok) atomicAdd(bad, 1ull);
 }
 
 }  // namespace qb
 
-extern "C" int qb_dev_csr_committed_vote(uint64_t G, const uint32_t* off, const uint64_t* match,
-                                         const uint32_t* cfg, const uint32_t* votes,
-                                         uint64_t* commit_out, uint8_t* vote_out, void* stream) {
+extern "C" int qb_dev_csr_committed_vote(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                                         const uint64_t* match, const uint32_t* cfg,
+                                         const uint32_t* votes, uint64_t* commit_out,
+                                         uint8_t* vote_out, void* stream) {
   if (G == 0 || (!commit_out && !vote_out)) return QB_OK;
+  QB_REQUIRE(max_slots <= QB_MAX_SLOTS, "max_slots must be 0..%d", QB_MAX_SLOTS);
   QB_REQUIRE(cfg, "cfg is NULL");
   QB_REQUIRE(!commit_out || (off && match), "off/match NULL with commit_out set");
   QB_REQUIRE(!vote_out || votes, "votes NULL with vote_out set");
   QB_REQUIRE(!match || aligned(match, 16), "match must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
   u64* commit = reinterpret_cast<u64*>(commit_out);
-  const dim3 grid(grid_for(G));
-  if (commit_out && vote_out)
-    hipLaunchKernelGGL((k_csr<true, true>), grid, dim3(kBlock), 0, st, G, off,
-                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
-  else if (commit_out)
-    hipLaunchKernelGGL((k_csr<true, false>), grid, dim3(kBlock), 0, st, G, off,
-                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
-  else
-    hipLaunchKernelGGL((k_csr<false, true>), grid, dim3(kBlock), 0, st, G, off,
-                       reinterpret_cast<const u64*>(match), cfg, votes, commit, vote_out);
+  const u64* m = reinterpret_cast<const u64*>(match);
+  const u32 w = max_slots == 0 ? QB_MAX_SLOTS : max_slots;
+  if (!commit) launch_csr_w<4>(G, off, m, cfg, votes, commit, vote_out, st);  // no LDS used
+  else if (w <= 4) launch_csr_w<4>(G, off, m, cfg, votes, commit, vote_out, st);
+  else if (w <= 8) launch_csr_w<8>(G, off, m, cfg, votes, commit, vote_out, st);
+  else if (w <= 12) launch_csr_w<12>(G, off, m, cfg, votes, commit, vote_out, st);
+  else launch_csr_w<16>(G, off, m, cfg, votes, commit, vote_out, st);
   QB_CHECK_LAUNCH("k_csr");
   return QB_OK;
 }
 
-extern "C" int qb_dev_csr_validate(uint64_t G, const uint32_t* off, uint64_t* bad_out,
-                                   void* stream) {
+extern "C" int qb_dev_csr_validate(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                                   uint64_t* bad_out, void* stream) {
   QB_REQUIRE(off && bad_out, "off/bad_out NULL");
+  QB_REQUIRE(max_slots <= QB_MAX_SLOTS, "max_slots must be 0..%d", QB_MAX_SLOTS);
   if (G == 0) return QB_OK;
   hipLaunchKernelGGL(k_csr_validate, dim3(grid_for(G)), dim3(kBlock), 0, as_stream(stream), G,
-                     off, reinterpret_cast<u64*>(bad_out));
+                     max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots, off,
+                     reinterpret_cast<u64*>(bad_out));
   QB_CHECK_LAUNCH("k_csr_validate");
   return QB_OK;
 }

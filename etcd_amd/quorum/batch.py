@@ -164,10 +164,14 @@ class CsrGroups:
     """G ragged / joint groups (CSR layout) resident on one device."""
 
     def __init__(self, off: torch.Tensor, cfg: torch.Tensor, match: torch.Tensor,
-                 votes: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None):
+                 votes: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None,
+                 max_slots: Optional[int] = None):
         self.off, self.cfg, self.match = off, cfg, match
         self.G = cfg.numel()
         self.device = cfg.device
+        if max_slots is None:  # the table's bound on s_g sizes the kernel
+            max_slots = int((off[1:].long() - off[:-1].long()).max().item()) if self.G else 0
+        self.max_slots = max(1, min(int(max_slots), _lib.QB_MAX_SLOTS))
         self.votes = votes if votes is not None else torch.zeros(self.G, dtype=torch.int32,
                                                                  device=self.device)
         self.active = active
@@ -209,14 +213,16 @@ class CsrGroups:
         votes = torch.empty(G, dtype=torch.int32, device=dev)
         _lib.call("qb_dev_synth_csr", seed, k, G, g_begin, _ptr(off), _ptr(match), _ptr(cfg),
                   _ptr(votes), _stream(dev))
-        return cls(off, cfg, match, votes)
+        smax = int(np.diff(off_h.astype(np.int64)).max()) if G else 0
+        return cls(off, cfg, match, votes, max_slots=smax)
 
     def committed_vote(self, commit_out=None, vote_out=None, want_commit=True, want_vote=True):
         if want_commit and commit_out is None:
             commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
         if want_vote and vote_out is None:
             vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
-        _lib.call("qb_dev_csr_committed_vote", self.G, _ptr(self.off), _ptr(self.match),
+        _lib.call("qb_dev_csr_committed_vote", self.G, self.max_slots, _ptr(self.off),
+                  _ptr(self.match),
                   _ptr(self.cfg), _ptr(self.votes), _ptr(commit_out if want_commit else None),
                   _ptr(vote_out if want_vote else None), _stream(self.device))
         return (commit_out if want_commit else None), (vote_out if want_vote else None)
@@ -237,9 +243,13 @@ class CsrGroups:
                   _stream(self.device))
         return out
 
-    def validate(self) -> int:
+    def validate(self, max_slots: Optional[int] = None) -> int:
+        """Number of groups breaking the CSR invariants (off[0] == 0,
+        0 <= s_g <= max_slots; default: this table's bound)."""
         bad = torch.zeros(1, dtype=torch.int64, device=self.device)
-        _lib.call("qb_dev_csr_validate", self.G, _ptr(self.off), _ptr(bad), _stream(self.device))
+        ms = self.max_slots if max_slots is None else max_slots
+        _lib.call("qb_dev_csr_validate", self.G, ms, _ptr(self.off), _ptr(bad),
+                  _stream(self.device))
         return int(bad.item())
 
 

@@ -132,16 +132,22 @@ int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_t* match,
  * Replaces JointConfig.CommittedIndex (quorum/joint.go:49-56) and
  * JointConfig.VoteResult (quorum/joint.go:61-75), which reduce to the
  * MajorityConfig forms when mask_out == 0; learners are slots in neither mask
- * and never count (tracker.go:273, majority.go:186-200). */
-int qb_dev_csr_committed_vote(uint64_t G, const uint32_t* off,
-                              const uint64_t* match, const uint32_t* cfg,
-                              const uint32_t* votes, uint64_t* commit_out,
-                              uint8_t* vote_out, void* stream);
+ * and never count (tracker.go:273, majority.go:186-200).
+ * max_slots bounds every s_g of the table (0 = QB_MAX_SLOTS); it sizes the
+ * kernel (LDS and networks), so pass the table's true bound: a group above it
+ * gives an unspecified (never out-of-bounds) result, which
+ * qb_dev_csr_validate detects. */
+int qb_dev_csr_committed_vote(uint64_t G, uint32_t max_slots,
+                              const uint32_t* off, const uint64_t* match,
+                              const uint32_t* cfg, const uint32_t* votes,
+                              uint64_t* commit_out, uint8_t* vote_out,
+                              void* stream);
 
-/* Checks a CSR table (off[0] == 0, 0 <= off[g+1] - off[g] <= 16).  Writes the
- * number of bad groups to *bad_out (device uint64). */
-int qb_dev_csr_validate(uint64_t G, const uint32_t* off, uint64_t* bad_out,
-                        void* stream);
+/* Checks a CSR table: off[0] == 0 and 0 <= off[g+1] - off[g] <= max_slots
+ * (0 = QB_MAX_SLOTS).  Writes the number of bad groups to *bad_out (device
+ * uint64). */
+int qb_dev_csr_validate(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                        uint64_t* bad_out, void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Progress tracking (raft/tracker)                                        */

@@ -142,7 +142,45 @@ def test_csr_validate_flags_bad_tables():
     off = np.array([0, 3, 2, 30], np.uint32)  # decreasing, then 28 slots
     cc = batch.CompiledConfigs(off, np.zeros(3, np.uint32), np.zeros(30, np.uint64))
     grp = batch.CsrGroups.from_compiled(cc, np.zeros(30, np.uint64), device=DEV)
-    assert grp.validate() == 2
+    assert grp.validate(max_slots=16) == 2
+    off = np.array([0, 3, 8, 12], np.uint32)
+    cc = batch.CompiledConfigs(off, np.zeros(3, np.uint32), np.zeros(12, np.uint64))
+    grp = batch.CsrGroups.from_compiled(cc, np.zeros(12, np.uint64), device=DEV)
+    assert grp.max_slots == 5 and grp.validate() == 0 and grp.validate(max_slots=4) == 1
+
+
+@pytest.mark.parametrize("max_slots", [4, 8, 12, 16])
+def test_csr_every_kernel_width_bound(max_slots):
+    """Each WMAX instantiation (LDS run buffer + widest network) is exact for
+    tables within its bound, including blocks whose runs fill the buffer."""
+    rng = random.Random(100 + max_slots)
+    off, vals, cfg, votes = _random_csr(rng, 12000, max_slots)
+    cc = batch.CompiledConfigs(off, cfg, np.zeros(len(vals), np.uint64))
+    grp = batch.CsrGroups.from_compiled(cc, vals, votes_u32=votes, device=DEV)
+    grp.max_slots = max_slots
+    c, v = grp.committed_vote()
+    ec, ev = oc.csr_eval(off, vals, cfg, votes)
+    assert np.array_equal(batch.as_u64(c), ec)
+    assert np.array_equal(v.cpu().numpy(), ev)
+
+
+def test_csr_full_width_blocks():
+    """Every group at exactly 16 slots: the LDS buffer is completely full."""
+    rng = random.Random(9)
+    G = 3000
+    groups_vals = [[rng.randrange(0, MAX) for _ in range(16)] for _ in range(G)]
+    off = np.arange(0, 16 * G + 1, 16, dtype=np.uint32)
+    vals = np.asarray([x for gv in groups_vals for x in gv], np.uint64)
+    cfg = np.array([rng.getrandbits(16) | (rng.getrandbits(16) << 16 if g % 3 == 0 else 0)
+                    for g in range(G)], np.uint32)
+    votes = np.array([rng.getrandbits(32) for _ in range(G)], np.uint32)
+    cc = batch.CompiledConfigs(off, cfg, np.zeros(len(vals), np.uint64))
+    grp = batch.CsrGroups.from_compiled(cc, vals, votes_u32=votes, device=DEV)
+    assert grp.max_slots == 16
+    c, v = grp.committed_vote()
+    ec, ev = oc.csr_eval(off, vals, cfg, votes)
+    assert np.array_equal(batch.as_u64(c), ec)
+    assert np.array_equal(v.cpu().numpy(), ev)
 
 
 def test_datadriven_golden_through_api(golden):

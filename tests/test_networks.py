@@ -56,7 +56,7 @@ def test_selection_networks(n):
         assert run(net, bits)[pos] == sorted(bits)[pos]
 
 
-@pytest.mark.parametrize("w", [4, 8, 12, 16])
+@pytest.mark.parametrize("w", range(2, 17))
 def test_sorting_networks(w):
     _, srt = parse()
     for bits in itertools.product((0, 1), repeat=w):

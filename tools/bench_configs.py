@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Throughput of every BASELINE config on one GPU (bench.py measures only
+configs[1]; these are the parity-test configs, measured the same way).
+
+  config 3  16M groups ragged 3-9 voters + 0-2 learners (CSR)
+  config 4  joint 5+5 (overlap 0-5), 8M groups = one GPU's shard of 64M
+  config 5  streaming tracker: 16M 5-voter groups, one MsgAppResp per group
+            per step on average (1% stale term), apply + commit advance
+
+Prints one JSON line per config: groups/s (group-steps/s for config 5),
+per-launch device time (HIP events around R back-to-back launches / R),
+algorithmic GB/s and fraction of the 8 TB/s HBM peak.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import HBM_PEAK_GBS, HipEvents  # noqa: E402
+from etcd_amd.quorum import batch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+
+
+def time_region(fn, reps, warm=3):
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warm):
+        fn()
+    ev = HipEvents(2)
+    torch.cuda.synchronize()
+    ev.record(ev.ev[0], sp)
+    for _ in range(reps):
+        fn()
+    ev.record(ev.ev[1], sp)
+    torch.cuda.synchronize()
+    t = ev.elapsed_ms(0, 1) / 1e3 / reps
+    ev.close()
+    return t
+
+
+def report(name, groups, t, algo_bytes, extra=None):
+    gbs = algo_bytes / t / 1e9
+    d = {"config": name, "groups_per_s": groups / t, "per_launch_us": t * 1e6,
+         "algo_bytes_per_launch": algo_bytes, "algo_bytes_per_group": algo_bytes / groups,
+         "achieved_GBs": gbs, "frac_hbm_peak": gbs / HBM_PEAK_GBS}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def csr_config(kind, G, reps):
+    grp = batch.CsrGroups.synth(0x5EED0003 if kind == "ragged" else 0x5EED0004, kind, G,
+                                device=dev)
+    slots = int(grp.off[-1].item())
+    c = torch.empty(G, dtype=torch.int64, device=dev)
+    v = torch.empty(G, dtype=torch.uint8, device=dev)
+    t = time_region(lambda: grp.committed_vote(c, v), reps)
+    # off (4) + cfg (4) + votes (4) + match (8 s) + commit (8) + vote (1)
+    algo = G * (4 + 4 + 4 + 8 + 1) + 8 * slots + 4
+    report(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G})
+
+
+def tracker_config(G, reps, seed=55):
+    n = 5
+    rng = np.random.default_rng(seed)
+    tr = batch.FixedTracker(n, G, dev)
+    fg = batch.FixedGroups.synth(0x5EED0005, n, G, device=dev, with_term_start=True)
+    tr.match.copy_(fg.match)
+    tr.term_start.copy_(fg.term_start)
+    tr.term.fill_(7)
+    tr.commit_advance()
+    last = batch.as_u64(fg.match[0])
+    del fg
+    batches = []
+    for r in range(2):
+        group = rng.integers(0, G, size=G).astype(np.uint32)
+        slot = rng.integers(1, n, size=G).astype(np.uint8)
+        lag = rng.integers(0, 96, size=G).astype(np.uint64)
+        lg = last[group]
+        index = np.where(lag < lg, lg - lag, np.uint64(0))
+        term = np.where(rng.random(G) < 0.01, 6, 7).astype(np.uint64)
+        batches.append(batch.AppRespBatch.from_numpy(group, slot, index, term, device=dev))
+    k = [0]
+
+    def step():
+        b = batches[k[0] % 2]
+        k[0] += 1
+        tr.apply_appresp(b)
+        tr.commit_advance()
+
+    t = time_region(step, reps)
+    t_apply = time_region(lambda: tr.apply_appresp(batches[0]), reps)
+    t_commit = time_region(lambda: tr.commit_advance(), reps)
+    # record 21 B + match RMW 16 B per message; commit advance
+    # reads match 40 + term_start 8 + committed 8, writes committed 8 per group
+    algo = G * (21 + 16) + G * 64
+    report("streaming tracker (apply + commit advance)", G, t, algo,
+           {"apply_us": t_apply * 1e6, "commit_advance_us": t_commit * 1e6,
+            "unit": "group-steps/s"})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="3,4,5")
+    a = ap.parse_args()
+    which = set(a.only.split(","))
+    if "3" in which:
+        csr_config("ragged", 1 << 24, a.reps)
+    if "4" in which:
+        csr_config("joint", 1 << 23, a.reps)
+    if "5" in which:
+        tracker_config(1 << 24, a.reps)
+
+
+if __name__ == "__main__":
+    main()
