@@ -53,6 +53,8 @@ SIGNATURES = {
     "qb_dev_fixed_apply_appresp": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                           _p, _p, _p]),
     "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
+    "qb_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
+    "qb_dev_fixed_tracker_step": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
     "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
     "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),

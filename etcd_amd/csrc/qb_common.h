@@ -103,6 +103,37 @@ __host__ __device__ __forceinline__ u8 joint_vote(u8 r1, u8 r2) {
   return QB_VOTE_PENDING;
 }
 
+// ------------------------------------------------------------- counters ---
+// Statistics are tallied per wave (a wave-uniform popcount of a ballot, kept
+// in a register), reduced per block in LDS, and flushed with ONE global
+// atomic per counter per block: same-address global atomics saturate at
+// ~88 per us chip-wide (MI355X_MICROARCH.md, fanin/dequeue rows), so a
+// per-wave flush of a 16M-record batch would cost milliseconds.
+__device__ __forceinline__ u32 wave_popc(bool p) { return u32(__popcll(__ballot(p))); }
+
+template <int K>
+struct BlockTally {
+  u32 t[K];  // wave-uniform running counts
+  __device__ __forceinline__ BlockTally() {
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = 0;
+  }
+  __device__ __forceinline__ void add(int k, bool p) { t[k] += wave_popc(p); }
+  // Every thread of the block must call this (it synchronises).  lds: K u32.
+  // dst[slot[k]] += block total of counter k.
+  __device__ __forceinline__ void flush(u32* lds, u64* dst, const int (&slot)[K]) {
+    if (threadIdx.x < K) lds[threadIdx.x] = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (t[k]) atomicAdd(&lds[k], t[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x < K && lds[threadIdx.x]) atomicAdd(dst + slot[threadIdx.x], u64(lds[threadIdx.x]));
+  }
+};
+
 inline unsigned grid_for(u64 threads, unsigned block = kBlock) {
   return unsigned((threads + block - 1) / block);
 }

@@ -45,23 +45,12 @@ __device__ __forceinline__ int classify(u32 n, u64 G, u64 g, u32 flags, u64 t,
   return (flags & QB_REC_REJECT) ? C_REJECT : C_APPLY;
 }
 
-// Wave-aggregated counter update: one atomic per category per wave.
-__device__ __forceinline__ void count_class(u64* stats, int cls, bool valid) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    if (k == C_HIGHER) continue;  // counted by pass 1
-    const u64 m = __ballot(valid && cls == k);
-    if (lane == 0 && m) {
-      const int slot = k == C_APPLY ? QB_STAT_APPLIED
-                     : k == C_REJECT ? QB_STAT_REJECTED
-                     : k == C_STALE ? QB_STAT_STALE_TERM
-                     : k == C_NONMEMBER ? QB_STAT_NON_MEMBER
-                     : k == C_HIGHER ? QB_STAT_HIGHER_TERM
-                                     : QB_STAT_BAD_GROUP;
-      atomicAdd(stats + slot, u64(__popcll(m)));
-    }
-  }
+// Grid for the record kernels: grid-stride over M with at most kRecBlocks
+// blocks, so the per-block counter flush stays cheap (BlockTally).
+constexpr unsigned kRecBlocks = 2048;
+inline unsigned rec_grid(u64 M) {
+  const unsigned g = grid_for(M);
+  return g < kRecBlocks ? g : kRecBlocks;
 }
 
 // Pass 1: the first higher-term record of each group (in batch order) makes
@@ -73,15 +62,17 @@ __global__ __launch_bounds__(kBlock) void k_appresp_stepdown(
     u32 n, u64 G, u64 M, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ rt, const u64* __restrict__ group_term, u32* __restrict__ stepdown_at,
     u64* __restrict__ stats) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  bool higher = false;
-  if (i < M) {
+  __shared__ u32 lds[1];
+  BlockTally<1> tally;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < M; i += stride) {
     const u64 g = rg[i];
-    higher = classify(n, G, g, rf[i], rt[i], group_term) == C_HIGHER;
+    const bool higher = classify(n, G, g, rf[i], rt[i], group_term) == C_HIGHER;
     if (higher) atomicMin(stepdown_at + g, u32(i));
+    tally.add(0, higher);
   }
-  const u64 m = __ballot(higher);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(stats + QB_STAT_HIGHER_TERM, u64(__popcll(m)));
+  const int slot[1] = {QB_STAT_HIGHER_TERM};
+  tally.flush(lds, stats, slot);
 }
 
 // Pass 2: MaybeUpdate as atomic max (commutative, so any arrival order gives
@@ -91,15 +82,15 @@ __global__ __launch_bounds__(kBlock) void k_appresp_apply(
     const u64* __restrict__ ri, const u64* __restrict__ rt, const u64* __restrict__ group_term,
     u64* __restrict__ match, u64* __restrict__ next, u32* __restrict__ active_words,
     const u32* __restrict__ stepdown_at, u64* __restrict__ stats) {
+  __shared__ u32 lds[6];
   const bool any_higher = stats[QB_STAT_HIGHER_TERM] != 0;  // uniform scalar load
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  const bool valid = i < M;
-  int cls = C_BAD;
-  bool after = false;
-  if (valid) {
+  BlockTally<6> tally;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < M; i += stride) {
     const u64 g = rg[i];
     const u32 f = rf[i];
-    cls = classify(n, G, g, f, rt[i], group_term);
+    const int cls = classify(n, G, g, f, rt[i], group_term);
+    bool after = false;
     if (cls == C_APPLY || cls == C_REJECT) {
       if (any_higher && stepdown_at[g] < u32(i)) {
         after = true;  // the leader already stepped down at an earlier record
@@ -114,10 +105,16 @@ __global__ __launch_bounds__(kBlock) void k_appresp_apply(
         }
       }
     }
+    tally.add(0, !after && cls == C_APPLY);
+    tally.add(1, !after && cls == C_REJECT);
+    tally.add(2, cls == C_STALE);
+    tally.add(3, cls == C_NONMEMBER);
+    tally.add(4, cls == C_BAD);
+    tally.add(5, after);
   }
-  count_class(stats, after ? -1 : cls, valid);
-  const u64 m = __ballot(valid && after);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(stats + QB_STAT_AFTER_STEPDOWN, u64(__popcll(m)));
+  const int slot[6] = {QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_STALE_TERM,
+                       QB_STAT_NON_MEMBER, QB_STAT_BAD_GROUP, QB_STAT_AFTER_STEPDOWN};
+  tally.flush(lds, stats, slot);
 }
 
 // ------------------------------------------------------- commit advance ----
@@ -221,7 +218,7 @@ extern "C" int qb_dev_fixed_apply_appresp(uint32_t n, uint64_t G, uint64_t M,
              "required pointer is NULL");
   QB_REQUIRE((reinterpret_cast<uintptr_t>(active) % 4) == 0, "active must be 4-byte aligned");
   hipStream_t st = as_stream(stream);
-  const dim3 grid(grid_for(M));
+  const dim3 grid(rec_grid(M));
   hipLaunchKernelGGL(k_appresp_stepdown, grid, dim3(kBlock), 0, st, n, G, M, rec_group, rec_flags,
                      reinterpret_cast<const u64*>(rec_term),
                      reinterpret_cast<const u64*>(group_term), stepdown_at,

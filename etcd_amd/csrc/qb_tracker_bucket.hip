@@ -1,0 +1,679 @@
+// qb_tracker_bucket.hip — one leader tick over G groups (FIXED layout):
+// a batch of MsgAppResp records applied and the commit advanced, with the
+// records bucketed by group so every update is an LDS atomic instead of a
+// random-address HBM atomic.
+//
+// Reference semantics, identical to qb_tracker.hip (paths relative to raft/):
+//   raft.Step term filter               raft.go:847-921
+//   stepLeader MsgAppResp (quorum part) raft.go:1100-1109, 1237-1259
+//   Progress.MaybeUpdate                tracker/progress.go:144-153
+//   raft.maybeCommit / raftLog.maybeCommit  raft.go:585-588, log.go:328-334
+//
+// Pipeline (records are any-order; M ~ G at the BASELINE config 5):
+//   K1 k_bk_hist     per tile of kTile records: LDS histogram over super-
+//                    buckets (kChunksPerSb chunks of CH groups each); invalid
+//                    records (group >= G, slot >= n) are counted and dropped
+//   K2 k_scan_*      exclusive scan of the bin-major [super-bucket][tile]
+//                    histogram (three small kernels)
+//   K3 k_bk_scatter  per tile: counting sort by super-bucket in LDS; every
+//                    payload column is loaded coalesced into LDS, permuted
+//                    there and written out as per-bucket contiguous runs
+//   K3b k_bk_parts   cut every super-bucket into parts of <= kTile records
+//   K4 k_bk_split    per part: the same LDS counting sort by chunk, written
+//                    in place (same range), plus the part's chunk run starts
+//   K5 k_bk_apply<N> one workgroup per chunk of CH groups (its records are
+//                    one short run per part of its super-bucket): classify (term
+//                    filter, step-down ordering via an LDS atomic min of the
+//                    batch index), MaybeUpdate as LDS atomic max, RecentActive
+//                    as LDS atomic or, then maybeCommit for the chunk's groups
+//                    and a coalesced write-back of match/next/active/committed.
+#include "qb_common.h"
+
+namespace qb {
+namespace bk {
+
+constexpr int kTile = 4096;          // records per histogram/scatter/split tile
+constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
+constexpr int kScanPer = 4096;       // elements per scan block (1024 x 4)
+constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
+
+// Bucketed record payload, structure of arrays (three u64 columns of M), so
+// every scatter store is one contiguous wave-wide write:
+//   index, term, and mr = meta | ridx << 32 with
+//   meta = lg (bits 0-9) | chunk-low (10-16) | slot (17-20) | reject (21),
+//   ridx = batch index of the record (step-down ordering).
+struct Cols {
+  u64* index;
+  u64* term;
+  u64* mr;
+};
+
+__host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
+
+struct Geometry {
+  u64 G, M;
+  u32 n, CH, NC, NSB, NT;
+  u64 nbins() const { return u64(NSB) * NT; }
+};
+
+inline Geometry geometry(u32 n, u64 G, u64 M) {
+  Geometry g{};
+  g.G = G;
+  g.M = M;
+  g.n = n;
+  g.CH = chunk_groups(n);
+  g.NC = u32((G + g.CH - 1) / g.CH);
+  g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
+  g.NT = u32((M + kTile - 1) / kTile);
+  return g;
+}
+
+// Workspace carve (all offsets 256-byte aligned).
+struct Carve {
+  size_t shards, hist, bsum, parts, chunk_start, buf1, buf2, total;
+};
+// Upper bound on parts: every super-bucket contributes at most one partial.
+inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
+inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+inline Carve carve(const Geometry& g) {
+  Carve c{};
+  size_t o = 0;
+  c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
+  c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
+  c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
+  // part table: pfirst[NSB+1], part_sb[max_parts], nparts
+  c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
+  c.chunk_start = o;  o += up256(sizeof(u32) * max_parts(g) * (kChunksPerSb + 1));
+  c.buf1 = o;  o += 3 * up256(sizeof(u64) * g.M);
+  c.buf2 = o;  o += 3 * up256(sizeof(u64) * g.M);
+  c.total = o;
+  return c;
+}
+
+inline Cols cols_at(char* base, u64 M) {
+  const size_t col = up256(sizeof(u64) * M);
+  return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
+              reinterpret_cast<u64*>(base + 2 * col)};
+}
+
+// Counters of block b go to shard b % kShards (QB_STAT_COUNT u64 each, one
+// cache line), folded into the caller's stats by k_stats_fold.
+__device__ __forceinline__ u64* shard_of(u64* shards) {
+  return shards + u64(blockIdx.x % kShards) * QB_STAT_COUNT;
+}
+
+__global__ void k_stats_fold(const u64* __restrict__ shards, u64* __restrict__ stats) {
+  const int k = threadIdx.x;  // one thread per counter
+  if (k >= QB_STAT_COUNT) return;
+  u64 s = 0;
+  for (int i = 0; i < kShards; ++i) s += shards[i * QB_STAT_COUNT + k];
+  stats[k] += s;
+}
+
+// ---------------------------------------------------------------- K1 ----
+__global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __restrict__ rg,
+                                                    const u8* __restrict__ rf,
+                                                    u32* __restrict__ hist,
+                                                    u64* __restrict__ shards) {
+  extern __shared__ __attribute__((aligned(16))) u32 lh[];  // NSB counters
+  __shared__ u32 tl[2];
+  BlockTally<2> tally;
+  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) lh[b] = 0;
+  __syncthreads();
+  const u64 t0 = u64(blockIdx.x) * kTile;
+  const u32 sbgroups = geo.CH * kChunksPerSb;
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
+    bool bad = false, nonmember = false;
+    if (i < geo.M) {
+      const u32 g = rg[i];
+      bad = g >= geo.G;
+      nonmember = !bad && (rf[i] & 0x0Fu) >= geo.n;
+      if (!bad && !nonmember) atomicAdd(&lh[g / sbgroups], 1u);
+    }
+    tally.add(0, bad);
+    tally.add(1, nonmember);
+  }
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) hist[u64(b) * geo.NT + blockIdx.x] = lh[b];
+  const int slot[2] = {QB_STAT_BAD_GROUP, QB_STAT_NON_MEMBER};
+  tally.flush(tl, shard_of(shards), slot);
+}
+
+// ---------------------------------------------------------------- K2 ----
+// In-place exclusive scan of n u32 values; data[n] receives the total.
+__device__ __forceinline__ u32 block_exclusive_scan_1024(u32 v, u32* sh, u32* total) {
+  // sh: 1024 + 32 u32 of LDS
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  u32 x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = u32(__shfl_up(int(x), o, 64));
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[1024 + w] = x;
+  __syncthreads();
+  if (w == 0) {
+    u32 s = lane < 16 ? sh[1024 + lane] : 0u;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const u32 y = u32(__shfl_up(int(s), o, 64));
+      if (lane >= o) s += y;
+    }
+    if (lane < 16) sh[1024 + lane] = s;  // inclusive wave sums
+  }
+  __syncthreads();
+  const u32 before = w ? sh[1024 + w - 1] : 0u;
+  *total = sh[1024 + 15];
+  return before + x - v;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_local(u32* __restrict__ data, u64 n,
+                                                     u32* __restrict__ bsum) {
+  __shared__ u32 sh[1024 + 32];
+  const u64 base = u64(blockIdx.x) * kScanPer + u64(threadIdx.x) * 4;
+  u32 v[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = base + k < n ? data[base + k] : 0u;
+    s += v[k];
+  }
+  u32 total;
+  u32 ex = block_exclusive_scan_1024(s, sh, &total);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (base + k < n) data[base + k] = ex;
+    ex += v[k];
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_sums(u32* __restrict__ bsum, u32 nb,
+                                                    u32* __restrict__ data_total_slot) {
+  __shared__ u32 sh[1024 + 32];
+  u32 carry = 0;
+  for (u32 base = 0; base < nb; base += 1024) {
+    const u32 i = base + threadIdx.x;
+    const u32 v = i < nb ? bsum[i] : 0u;
+    u32 total;
+    const u32 ex = block_exclusive_scan_1024(v, sh, &total);
+    if (i < nb) bsum[i] = ex + carry;
+    carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *data_total_slot = carry;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_add(u32* __restrict__ data, u64 n,
+                                                   const u32* __restrict__ bsum) {
+  const u64 base = u64(blockIdx.x) * kScanPer + u64(threadIdx.x) * 4;
+  const u32 add = bsum[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + k < n) data[base + k] += add;
+}
+
+// ------------------------------------------------ LDS tile partition ----
+// Counting sort of one tile (<= kTile records) by a small key, in LDS.  The
+// caller provides each record's bin (or kNoBin); afterwards perm[e] is the
+// tile index of the e-th record in bin order and start[b] the first e of
+// bin b.  Payload columns are then moved with tile_move: coalesced global
+// load into LDS, permuted LDS read, coalesced global store.
+constexpr u16 kNoBin = 0xFFFF;
+constexpr int kPartThreads = 1024;
+
+struct TileLds {
+  u16 bin[kTile];
+  u16 rank[kTile];
+  u16 perm[kTile];
+  u64 stage[kTile];
+  u32 wsum[kPartThreads / 64];
+};
+
+// Exclusive scan of cnt[0..nb) in place (per-thread serial runs + wave
+// shuffles + one LDS pass); returns the number of binned records.
+__device__ __forceinline__ u32 tile_scan_bins(u32* cnt, u32 nb, u32* wsum) {
+  const u32 T = blockDim.x;
+  const u32 per = (nb + T - 1) / T;
+  u32 run = 0;
+  for (u32 j = 0; j < per; ++j) {
+    const u32 b = threadIdx.x * per + j;
+    if (b < nb) run += cnt[b];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = int(T >> 6);
+  u32 x = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = u32(__shfl_up(int(x), o, 64));
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  u32 before = 0, total = 0;
+  for (int q = 0; q < nw; ++q) {
+    total += wsum[q];
+    if (q < w) before += wsum[q];
+  }
+  u32 acc = before + x - run;
+  for (u32 j = 0; j < per; ++j) {
+    const u32 b = threadIdx.x * per + j;
+    if (b < nb) {
+      const u32 c = cnt[b];
+      cnt[b] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
+__device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec) {
+  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
+    const u16 b = L.bin[k];
+    if (b != kNoBin) L.perm[start[b] + L.rank[k]] = u16(k);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- K3 ----
+// Level 1: one block per tile of the original records; bins = super-buckets;
+// each bin's run goes to gstart[bin] (from the level-1 scan).
+__global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
+    Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
+    const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
+    Cols out) {
+  extern __shared__ __attribute__((aligned(16))) u32 dyn[];
+  u32* start = dyn;               // NSB: count, then local exclusive start
+  u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
+  __shared__ TileLds L;
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+    start[b] = 0;
+    gstart[b] = offsets[u64(b) * geo.NT + blockIdx.x];
+  }
+  __syncthreads();
+  const u64 t0 = u64(blockIdx.x) * kTile;
+  const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
+  const u32 sbgroups = geo.CH * kChunksPerSb;
+  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
+    const u32 g = rg[t0 + k];
+    u16 b = kNoBin;
+    if (g < geo.G && (rf[t0 + k] & 0x0Fu) < geo.n) {
+      b = u16(g / sbgroups);
+      L.rank[k] = u16(atomicAdd(&start[b], 1u));
+    }
+    L.bin[k] = b;
+  }
+  __syncthreads();
+  const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
+  tile_perm(L, start, nrec);
+  // three payload columns: index, term, mr = meta | ridx << 32
+  for (int col = 0; col < 3; ++col) {
+    for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
+      const u64 i = t0 + k;
+      u64 v;
+      if (col == 0) {
+        v = ri[i];
+      } else if (col == 1) {
+        v = rt[i];
+      } else {
+        const u32 g = rg[i], f = rf[i];
+        const u32 chunk = g / geo.CH;
+        const u32 meta = (g - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
+                         ((f & 0x0Fu) << 17) | (((f & QB_REC_REJECT) ? 1u : 0u) << 21);
+        v = u64(meta) | (u64(u32(i)) << 32);
+      }
+      L.stage[k] = v;
+    }
+    __syncthreads();
+    u64* dst = col == 0 ? out.index : col == 1 ? out.term : out.mr;
+    for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+      const u32 k = L.perm[e];
+      const u32 b = L.bin[k];
+      dst[gstart[b] + (e - start[b])] = L.stage[k];
+    }
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------- K3b ----
+// Parts: super-bucket sb (records [lo, hi) of buf1) is cut into
+// ceil((hi - lo) / kTile) parts.  pfirst[sb] = first part of sb,
+// part_sb[p] = its super-bucket, nparts = pfirst[NSB].
+__global__ __launch_bounds__(1024) void k_bk_parts(Geometry geo, const u32* __restrict__ offsets,
+                                                   u32* __restrict__ pt) {
+  u32* pfirst = pt;                  // NSB + 1
+  u32* part_sb = pt + geo.NSB + 2;   // max_parts
+  __shared__ u32 cnt[4096];
+  __shared__ u32 wsum[16];
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+    const u32 n = offsets[u64(b + 1) * geo.NT] - offsets[u64(b) * geo.NT];
+    cnt[b] = (n + kTile - 1) / kTile;
+  }
+  __syncthreads();
+  const u32 total = tile_scan_bins(cnt, geo.NSB, wsum);
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+    pfirst[b] = cnt[b];
+    const u32 n = (b + 1 < geo.NSB ? cnt[b + 1] : total) - cnt[b];
+    for (u32 q = 0; q < n; ++q) part_sb[cnt[b] + q] = b;
+  }
+  if (threadIdx.x == 0) pfirst[geo.NSB] = total;
+}
+
+// ---------------------------------------------------------------- K4 ----
+// Level 2: one block per part; counting sort of the part by chunk-low,
+// written to the SAME range of buf2; cs[p][c] = first record of chunk-low c
+// in part p (cs[p][128] = part end).
+__global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
+                                                           const u32* __restrict__ offsets,
+                                                           const u32* __restrict__ pt, Cols in,
+                                                           Cols out, u32* __restrict__ cs) {
+  const u32* pfirst = pt;
+  const u32* part_sb = pt + geo.NSB + 2;
+  const u32 p = blockIdx.x;
+  if (p >= pfirst[geo.NSB]) return;  // fewer parts than the launch bound
+  __shared__ TileLds L;
+  __shared__ u32 start[kChunksPerSb];
+  const u32 sb = part_sb[p];
+  const u32 sb_lo = offsets[u64(sb) * geo.NT], sb_hi = offsets[u64(sb + 1) * geo.NT];
+  const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
+  const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
+  const u32 nrec = hi - lo;
+  if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
+  __syncthreads();
+  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
+    const u64 mr = in.mr[lo + k];
+    const u16 b = u16((u32(mr) >> 10) & 127u);
+    L.bin[k] = b;
+    L.rank[k] = u16(atomicAdd(&start[b], 1u));
+    L.stage[k] = mr;
+  }
+  __syncthreads();
+  tile_scan_bins(start, kChunksPerSb, L.wsum);
+  if (threadIdx.x <= kChunksPerSb)
+    cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
+        lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
+  tile_perm(L, start, nrec);
+  for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
+  __syncthreads();
+  for (int col = 0; col < 2; ++col) {
+    const u64* src = col == 0 ? in.index : in.term;
+    u64* dst = col == 0 ? out.index : out.term;
+    for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) L.stage[k] = src[lo + k];
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) dst[lo + e] = L.stage[L.perm[e]];
+    __syncthreads();
+  }
+}
+
+// Run table of one chunk: the chunk's run in each of up to kRuns parts,
+// with an inclusive prefix of run lengths so flattened record f maps to a
+// buffer index by binary search.
+struct RunTable {
+  static constexpr u32 kRuns = 64;
+  u32 lo[kRuns];
+  u32 pre[kRuns + 1];
+  u32 nr;
+  // Every thread calls; returns the number of records in parts [pb, min(p1, pb+kRuns)).
+  __device__ __forceinline__ u32 build(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
+    __syncthreads();  // earlier readers of the table are done
+    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
+    if (threadIdx.x < 64) {  // one wave: inclusive scan of the run lengths
+      const u32 r = threadIdx.x;
+      u32 l = 0, len = 0;
+      if (r < n) {
+        const u64 row = u64(pb + r) * (kChunksPerSb + 1) + cl;
+        l = cs[row];
+        len = cs[row + 1] - l;
+      }
+      u32 x = len;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = u32(__shfl_up(int(x), o, 64));
+        if (r >= u32(o)) x += y;
+      }
+      if (r < n) {
+        lo[r] = l;
+        pre[r + 1] = x;
+      }
+      if (r == 0) {
+        pre[0] = 0;
+        nr = n;
+      }
+    }
+    __syncthreads();
+    return pre[n];
+  }
+  __device__ __forceinline__ u32 locate(u32 f) const {
+    u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
+    while (b - a > 1) {
+      const u32 m = (a + b) >> 1;
+      if (pre[m] <= f) a = m;
+      else b = m;
+    }
+    return lo[a] + (f - pre[a]);
+  }
+};
+
+// ---------------------------------------------------------------- K5 ----
+// LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
+// first_hi[CH] u32, act[CH] u32.
+template <int N, bool NEXT>
+__global__ __launch_bounds__(kBlock) void k_bk_apply(
+    Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
+    const u64* __restrict__ group_term, const u64* __restrict__ term_start,
+    u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
+    u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
+    u64* __restrict__ shards) {
+  constexpr u32 CH = chunk_groups(N);
+  __shared__ u32 tl[5];
+  BlockTally<5> tally;
+  __shared__ u64 acc_m[N * CH];
+  __shared__ u64 acc_n[NEXT ? N * CH : 1];
+  __shared__ u64 gterm[CH];
+  __shared__ u32 first_hi[CH];
+  __shared__ u32 act[CH];
+  const u32 c = blockIdx.x;
+  const u64 g0 = u64(c) * CH;
+  const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
+  for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
+    acc_m[k] = 0;
+    if constexpr (NEXT) acc_n[k] = 0;
+  }
+  for (u32 k = threadIdx.x; k < CH; k += kBlock) {
+    gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
+    first_hi[k] = 0xFFFFFFFFu;
+    act[k] = 0;
+  }
+  // This chunk's records: one short run per part of its super-bucket,
+  // flattened into one index space (RunTable) so every thread has a record
+  // in flight at once.
+  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
+  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  __shared__ RunTable rt;
+  // Pass 1: term filter; the first higher-term record of a group (batch
+  // order) makes the sequential leader step down (raft.go:875-879).
+  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
+    const u32 total = rt.build(cs, pb, p1, cl);
+    for (u32 f0 = 0; f0 < total; f0 += kBlock) {
+      const u32 f = f0 + threadIdx.x;
+      bool stale = false, higher = false;
+      if (f < total) {
+        const u32 i = rt.locate(f);
+        const u64 mr = recs.mr[i], term = recs.term[i];
+        const u32 lg = u32(mr) & 1023u;
+        const u64 gt = gterm[lg];
+        stale = term < gt;
+        higher = term > gt;
+        if (higher) atomicMin(&first_hi[lg], u32(mr >> 32));
+      }
+      tally.add(0, stale);
+      tally.add(1, higher);
+    }
+  }
+  __syncthreads();
+  // Pass 2: MaybeUpdate (max is commutative: any order = batch order) and
+  // RecentActive, for same-term records before the group's step-down.
+  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
+    const u32 total = rt.build(cs, pb, p1, cl);
+    for (u32 f0 = 0; f0 < total; f0 += kBlock) {
+      const u32 f = f0 + threadIdx.x;
+      bool applied = false, rejected = false, after = false;
+      if (f < total) {
+        const u32 i = rt.locate(f);
+        const u64 mr = recs.mr[i];
+        const u32 meta = u32(mr), ridx = u32(mr >> 32);
+        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+        if (recs.term[i] == gterm[lg]) {
+          if (ridx > first_hi[lg]) {
+            after = true;
+          } else {
+            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+            if (meta & (1u << 21)) {
+              rejected = true;                              // raft.go:1109: not MaybeUpdate
+            } else {
+              applied = true;
+              const u64 idx = recs.index[i];
+              atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
+              if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
+            }
+          }
+        }
+      }
+      tally.add(2, applied);
+      tally.add(3, rejected);
+      tally.add(4, after);
+    }
+  }
+  __syncthreads();
+  // maybeCommit for every group of the chunk + write-back (coalesced rows).
+  for (u32 lg = threadIdx.x; lg < ng; lg += kBlock) {
+    const u64 g = g0 + lg;
+    u64 v[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      u64* p = match + u64(s) * geo.G + g;
+      const u64 old = *p, a = acc_m[s * CH + lg];
+      v[s] = a > old ? a : old;
+      if (a > old) *p = a;
+      if constexpr (NEXT) {
+        u64* q = next + u64(s) * geo.G + g;
+        const u64 nn = acc_n[s * CH + lg];
+        if (nn > *q) *q = nn;
+      }
+    }
+    const u64 ci = select_quorum<N>(v);
+    const u64 cm = committed[g];
+    const bool adv = ci > cm && ci >= term_start[g];  // log.go:328-334
+    if (adv) committed[g] = ci;
+    if (advanced) advanced[g] = adv ? 1 : 0;
+    stepdown_at[g] = first_hi[lg];
+    if (act[lg]) active[g] = u16(active[g] | act[lg]);
+  }
+  const int slot[5] = {QB_STAT_STALE_TERM, QB_STAT_HIGHER_TERM, QB_STAT_APPLIED,
+                       QB_STAT_REJECTED, QB_STAT_AFTER_STEPDOWN};
+  tally.flush(tl, shard_of(shards), slot);
+}
+
+template <int N>
+void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs, const u64* gt,
+                  const u64* ts, u64* match, u64* next, u16* active, u64* committed,
+                  u32* stepdown, u8* adv, u64* stats, hipStream_t st) {
+  if (next)
+    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
+                       cs, gt, ts, match, next, active, committed, stepdown, adv, stats);
+  else
+    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
+                       cs, gt, ts, match, next, active, committed, stepdown, adv, stats);
+}
+
+template <int... Ns>
+void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
+                    Cols recs, const u32* pt, const u32* cs, const u64* gt, const u64* ts,
+                    u64* match,
+                    u64* next, u16* active, u64* committed, u32* stepdown, u8* adv, u64* stats,
+                    hipStream_t st) {
+  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, gt, ts, match, next, active,
+                                       committed, stepdown, adv, stats, st)
+                : void()),
+   ...);
+}
+
+}  // namespace bk
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
+  if (n < 1 || n > QB_MAX_SLOTS) return 0;
+  return bk::carve(bk::geometry(n, G, M)).total;
+}
+
+extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
+                                         const uint32_t* rec_group, const uint8_t* rec_flags,
+                                         const uint64_t* rec_index, const uint64_t* rec_term,
+                                         const uint64_t* group_term, const uint64_t* term_start,
+                                         uint64_t* match, uint64_t* next, uint16_t* active,
+                                         uint64_t* committed, uint32_t* stepdown_at,
+                                         uint8_t* advanced_out, uint64_t* stats,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
+  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
+  QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
+             "required state pointer is NULL");
+  QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
+             "record pointer is NULL");
+  const bk::Geometry geo = bk::geometry(n, G, M);
+  const bk::Carve cv = bk::carve(geo);
+  QB_REQUIRE(workspace && workspace_bytes >= cv.total,
+             "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv.total);
+  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
+             (unsigned long long)G);
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
+  u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
+  u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
+  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
+  const bk::Cols buf1 = bk::cols_at(ws + cv.buf1, M);
+  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M);
+  u64* stt = reinterpret_cast<u64*>(stats);
+  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
+  const size_t lds_bins = sizeof(u32) * geo.NSB;
+  hipError_t e0 = hipMemsetAsync(shards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
+  if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(stat shards)");
+
+  if (M > 0) {
+    hipLaunchKernelGGL(bk::k_bk_hist, dim3(geo.NT), dim3(kBlock), lds_bins, st, geo, rec_group,
+                       rec_flags, hist, shards);
+    QB_CHECK_LAUNCH("k_bk_hist");
+    const u64 nb = geo.nbins();
+    const u32 nblk = u32((nb + bk::kScanPer - 1) / bk::kScanPer);
+    hipLaunchKernelGGL(bk::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+    hipLaunchKernelGGL(bk::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
+    hipLaunchKernelGGL(bk::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+    QB_CHECK_LAUNCH("k_scan");
+    hipLaunchKernelGGL(bk::k_bk_scatter, dim3(geo.NT), dim3(bk::kPartThreads), 2 * lds_bins, st,
+                       geo, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
+                       reinterpret_cast<const u64*>(rec_term), hist, buf1);
+    QB_CHECK_LAUNCH("k_bk_scatter");
+    hipLaunchKernelGGL(bk::k_bk_parts, dim3(1), dim3(1024), 0, st, geo, hist, pt);
+    QB_CHECK_LAUNCH("k_bk_parts");
+    hipLaunchKernelGGL(bk::k_bk_split, dim3(unsigned(bk::max_parts(geo))), dim3(bk::kPartThreads),
+                       0, st, geo, hist, pt, buf1, buf2, cs);
+    QB_CHECK_LAUNCH("k_bk_split");
+  } else {
+    hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(parts)");
+  }
+  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs,
+                     reinterpret_cast<const u64*>(group_term),
+                     reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
+                     reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed),
+                     stepdown_at, advanced_out, shards, st);
+  QB_CHECK_LAUNCH("k_bk_apply");
+  hipLaunchKernelGGL(bk::k_stats_fold, dim3(1), dim3(64), 0, st, shards, stt);
+  QB_CHECK_LAUNCH("k_stats_fold");
+  return QB_OK;
+}

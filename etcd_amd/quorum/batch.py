@@ -309,6 +309,22 @@ class FixedTracker:
                   _stream(self.device))
         return advanced_out
 
+    def step(self, batch: AppRespBatch, advanced_out: Optional[torch.Tensor] = None,
+             reset_stats: bool = True) -> Optional[torch.Tensor]:
+        """One leader tick: apply the batch and run maybeCommit for every group
+        (qb_dev_fixed_tracker_step: records bucketed by group, LDS atomics)."""
+        if reset_stats:
+            self.stats.zero_()
+        need = _lib.load().qb_fixed_tracker_workspace_bytes(self.n, self.G, batch.M)
+        if getattr(self, "_ws", None) is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_fixed_tracker_step", self.n, self.G, batch.M, _ptr(batch.group),
+                  _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(self.term),
+                  _ptr(self.term_start), _ptr(self.match), _ptr(self.next), _ptr(self.active),
+                  _ptr(self.committed), _ptr(self.stepdown_at), _ptr(advanced_out),
+                  _ptr(self.stats), _ptr(self._ws), self._ws.numel(), _stream(self.device))
+        return advanced_out
+
     def stats_dict(self) -> dict:
         v = self.stats.cpu().tolist()
         return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}

@@ -199,6 +199,31 @@ int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
                                 uint64_t* committed, uint8_t* advanced_out,
                                 void* stream);
 
+/* One leader tick for G groups of the FIXED layout: a batch of MsgAppResp
+ * records applied (same semantics as qb_dev_fixed_apply_appresp) and
+ * maybeCommit run for every group (as qb_dev_fixed_commit_advance), fused.
+ * The records are bucketed by group on the device (counting sort into
+ * LDS-sized chunks) so every MaybeUpdate is an LDS atomic; this is the path
+ * for large batches (M ~ G).  Differences from the two-call form:
+ *   - stepdown_at[g] is written for every group (no entry requirement);
+ *   - workspace: device scratch of qb_fixed_tracker_workspace_bytes(n, G, M)
+ *     bytes (caller-owned, reusable across calls of the same or smaller
+ *     size; no allocation inside, so the call can be graph-captured).
+ * Requires G, M < 2^32. */
+size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M);
+int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
+                              const uint32_t* rec_group,
+                              const uint8_t* rec_flags,
+                              const uint64_t* rec_index,
+                              const uint64_t* rec_term,
+                              const uint64_t* group_term,
+                              const uint64_t* term_start, uint64_t* match,
+                              uint64_t* next, uint16_t* active,
+                              uint64_t* committed, uint32_t* stepdown_at,
+                              uint8_t* advanced_out, uint64_t* stats,
+                              void* workspace, size_t workspace_bytes,
+                              void* stream);
+
 /* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */
 /* ----------------------------------------------------------------------- */

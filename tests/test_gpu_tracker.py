@@ -108,14 +108,22 @@ def _random_batch(rng, n, G, M, st, stale=0.01, higher=0.0, reject=0.02, nonmemb
     return group, slot, index, term.astype(np.uint64), rej, flags
 
 
-@pytest.mark.parametrize("n,G,M,kw", [
+CASES = [
     (5, 4096, 8192, {}),
     (5, 1000, 20000, {"higher": 0.002, "nonmember": 0.01, "bad": 0.01}),   # duplicates heavy
     (3, 20000, 20000, {"reject": 0.2, "stale": 0.1}),
     (7, 5000, 30000, {"higher": 0.01}),
     (1, 100, 1000, {"higher": 0.05}),
-])
-def test_appresp_then_commit_vs_sequential(n, G, M, kw):
+    (9, 3000, 6000, {"higher": 0.01, "nonmember": 0.02}),    # 256-group chunks
+    (16, 777, 5000, {"reject": 0.1, "higher": 0.01}),
+    (5, 70001, 70001, {"higher": 0.001}),                    # > 1 super-bucket... tail chunk
+    (5, 1, 50, {"higher": 0.1}),
+]
+
+
+@pytest.mark.parametrize("mode", ["two_call", "step"])
+@pytest.mark.parametrize("n,G,M,kw", CASES)
+def test_appresp_then_commit_vs_sequential(mode, n, G, M, kw):
     rng = np.random.default_rng(n * 7 + G)
     st = _random_state(rng, n, G)
     tr = _tracker_from(n, st)
@@ -124,8 +132,11 @@ def test_appresp_then_commit_vs_sequential(n, G, M, kw):
         group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, **kw)
         stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
         b = batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV)
-        tr.apply_appresp(b)
-        tr.commit_advance()
+        if mode == "step":
+            tr.step(b)
+        else:
+            tr.apply_appresp(b)
+            tr.commit_advance()
         _compare(tr, seq, n, G)
         got = tr.stats_dict()
         assert got["applied"] == stats[0] and got["rejected"] == stats[1]
@@ -136,6 +147,38 @@ def test_appresp_then_commit_vs_sequential(n, G, M, kw):
         # (becomeFollower) and the marker is re-armed before the next batch
         tr.stepdown_at.fill_(-1)
         seq["stepped_down"][:] = 0
+
+
+def test_step_empty_batch_is_commit_advance():
+    n, G = 5, 3000
+    rng = np.random.default_rng(3)
+    st = _random_state(rng, n, G)
+    st["committed"][:] = 0       # break the invariant on purpose: commit must catch up
+    tr = _tracker_from(n, st)
+    adv = torch.zeros(G, dtype=torch.uint8, device=DEV)
+    empty = batch.AppRespBatch.from_numpy(np.zeros(0), np.zeros(0), np.zeros(0), np.zeros(0),
+                                          device=DEV)
+    tr.step(empty, adv)
+    want_adv = oc.commit_all(n, st["match"], st["term_start"], st["committed"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(adv.cpu().numpy(), want_adv)
+
+
+@pytest.mark.timeout(300)
+def test_step_full_size_16m():
+    """BASELINE config 5 on one GPU through the bucketed step."""
+    n, G = 5, 1 << 24
+    rng = np.random.default_rng(56)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st, track_next=False)
+    st.pop("next")
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, G, st, reject=0.0,
+                                                         higher=0.0001)
+    oc.appresp_sequential(n, G, (group, flags, index, term), st)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    assert np.array_equal(batch.as_u64(tr.match), st["match"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
 
 
 @pytest.mark.timeout(300)
