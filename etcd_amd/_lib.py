@@ -24,6 +24,9 @@ QB_REC_REJECT = 0x80
 QB_STAT_NAMES = ("applied", "rejected", "stale_term", "non_member", "higher_term",
                  "bad_group", "after_stepdown")
 QB_STAT_COUNT = 8
+QB_VSTAT_NAMES = ("recorded", "duplicate", "stale_term", "higher_term", "after_stepdown", "bad")
+QB_VOTE_MODE_VOTE = 0
+QB_VOTE_MODE_PREVOTE = 1
 
 
 class QuorumBatchError(RuntimeError):
@@ -55,6 +58,10 @@ SIGNATURES = {
     "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
     "qb_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
     "qb_dev_fixed_tracker_step": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
+    "qb_votes_workspace_bytes": (C.c_size_t, [_u64]),
+    "qb_dev_record_votes": (_i32, [_i32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                   C.c_size_t, _p]),
+    "qb_dev_csr_tally_votes": (_i32, [_u64, _p, _p, _p, _p, _p, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
     "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
     "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),

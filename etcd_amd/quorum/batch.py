@@ -243,6 +243,34 @@ class CsrGroups:
                   _stream(self.device))
         return out
 
+    def tally_votes(self):
+        """ProgressTracker.TallyVotes per group (tracker.go:267-288):
+        (granted, rejected, VoteResult) as uint8 device tensors."""
+        gr = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        rj = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        res = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_csr_tally_votes", self.G, _ptr(self.cfg), _ptr(self.votes), _ptr(gr),
+                  _ptr(rj), _ptr(res), _stream(self.device))
+        return gr, rj, res
+
+    def record_votes(self, batch: "AppRespBatch", group_term: torch.Tensor, prevote: bool = False,
+                     stepdown_at: Optional[torch.Tensor] = None,
+                     stats: Optional[torch.Tensor] = None):
+        """RecordVote for a batch of MsgVoteResp (or MsgPreVoteResp) records,
+        first vote wins in batch order (tracker.go:258-263, raft.go:847-921).
+        Returns (stepdown_at, stats)."""
+        if stepdown_at is None:
+            stepdown_at = torch.full((self.G,), -1, dtype=torch.int32, device=self.device)
+        if stats is None:
+            stats = torch.zeros(8, dtype=torch.int64, device=self.device)
+        need = _lib.load().qb_votes_workspace_bytes(batch.M)
+        ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_record_votes", _lib.QB_VOTE_MODE_PREVOTE if prevote else
+                  _lib.QB_VOTE_MODE_VOTE, self.G, batch.M, _ptr(batch.group), _ptr(batch.flags),
+                  _ptr(batch.term), _ptr(group_term), _ptr(self.votes), _ptr(stepdown_at),
+                  _ptr(stats), _ptr(ws), ws.numel(), _stream(self.device))
+        return stepdown_at, stats
+
     def validate(self, max_slots: Optional[int] = None) -> int:
         """Number of groups breaking the CSR invariants (off[0] == 0,
         0 <= s_g <= max_slots; default: this table's bound)."""

@@ -88,6 +88,20 @@ enum {
   QB_STAT_COUNT = 8
 };
 
+/* Counters filled by qb_dev_record_votes (device uint64 each, accumulated). */
+enum {
+  QB_VSTAT_RECORDED = 0,       /* RecordVote stored the slot's first vote        */
+  QB_VSTAT_DUPLICATE = 1,      /* the slot had already voted (first vote wins)   */
+  QB_VSTAT_STALE_TERM = 2,     /* m.Term < group term: dropped                   */
+  QB_VSTAT_HIGHER_TERM = 3,    /* the candidate steps down (raft.go:872-879)     */
+  QB_VSTAT_AFTER_STEPDOWN = 4, /* polled record behind the group's step-down     */
+  QB_VSTAT_BAD = 5,            /* group index >= G                               */
+  QB_VSTAT_COUNT = 8
+};
+
+#define QB_VOTE_MODE_VOTE 0     /* MsgVoteResp to a candidate (raft.go:1391) */
+#define QB_VOTE_MODE_PREVOTE 1  /* MsgPreVoteResp to a pre-candidate         */
+
 /* ----------------------------------------------------------------------- */
 /* Library                                                                 */
 /* ----------------------------------------------------------------------- */
@@ -223,6 +237,32 @@ int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                               uint8_t* advanced_out, uint64_t* stats,
                               void* workspace, size_t workspace_bytes,
                               void* stream);
+
+/* Elections.  A batch of vote responses of one kind (mode), records
+ * {group, flags = slot | reject << 7, term} in batch order, applied to the
+ * CSR votes words (voted | granted << 16) exactly as the sequential
+ * (pre-)candidate does: raft.Step's term filter (raft.go:847-921, with the
+ * MsgPreVoteResp exception of raft.go:866-871), stepCandidate -> poll ->
+ * RecordVote with first-vote-wins (tracker/tracker.go:258-263), and nothing
+ * after the group's first step-down (stepdown_at as in
+ * qb_dev_fixed_apply_appresp: UINT32_MAX on entry).  VoteResult is monotone
+ * once decided, so qb_dev_csr_tally_votes after the batch gives the outcome
+ * the sequential candidate reaches (raft.go:1402-1414).
+ * workspace: qb_votes_workspace_bytes(M) bytes of device scratch. */
+size_t qb_votes_workspace_bytes(uint64_t M);
+int qb_dev_record_votes(int mode, uint64_t G, uint64_t M,
+                        const uint32_t* rec_group, const uint8_t* rec_flags,
+                        const uint64_t* rec_term, const uint64_t* group_term,
+                        uint32_t* votes, uint32_t* stepdown_at, uint64_t* stats,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* ProgressTracker.TallyVotes (tracker/tracker.go:267-288) per group:
+ * granted / rejected among the voters of either half (learners never count)
+ * and JointConfig.VoteResult.  Any output may be NULL. */
+int qb_dev_csr_tally_votes(uint64_t G, const uint32_t* cfg,
+                           const uint32_t* votes, uint8_t* granted_out,
+                           uint8_t* rejected_out, uint8_t* result_out,
+                           void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */

@@ -340,3 +340,44 @@ def datadriven_inputs(case):
     vl = _make_lookuper(case["votes"], ids, idsj)
     votes = {k: v != 1 for k, v in vl.items()}
     return set(ids), set(idsj), acked, votes
+
+
+# --------------------------------------------------------------------------
+# Vote responses, one record at a time (the sequential (pre-)candidate)
+# --------------------------------------------------------------------------
+
+STAT_RECORDED, STAT_DUPLICATE, STAT_STALE, STAT_HIGHER, STAT_AFTER, STAT_BAD = range(6)
+
+
+def vote_response_sequential(prevote: bool, group_term: int, stepped_down: bool,
+                             votes: dict, slot: int, reject: bool, term: int):
+    """One MsgVoteResp / MsgPreVoteResp reaching a (pre-)candidate whose
+    Votes map is ``votes`` (slot -> granted).  Returns (stat, stepped_down).
+
+    raft.go:847-921 — Step's term handling: a lower term is ignored; a higher
+    term makes the node becomeFollower, except a granted MsgPreVoteResp
+    (raft.go:866-871); after stepping down the node is a follower and no later
+    response reaches poll.  raft.go:1391-1400 — stepCandidate polls
+    myVoteRespType; poll (raft.go:837-845) -> RecordVote, first vote wins
+    (tracker.go:258-263)."""
+    if term < group_term:
+        return STAT_STALE, stepped_down
+    if term > group_term and (reject or not prevote):
+        return STAT_HIGHER, True
+    if stepped_down:
+        return STAT_AFTER, stepped_down
+    if slot in votes:
+        return STAT_DUPLICATE, stepped_down
+    votes[slot] = not reject
+    return STAT_RECORDED, stepped_down
+
+
+def tally_votes_slots(mask_in: int, mask_out: int, votes: dict):
+    """TallyVotes (tracker.go:267-288) on slot-indexed votes: (granted,
+    rejected, JointConfig.VoteResult)."""
+    voters = mask_in | mask_out
+    granted = sum(1 for s, v in votes.items() if (voters >> s) & 1 and v)
+    rejected = sum(1 for s, v in votes.items() if (voters >> s) & 1 and not v)
+    c0 = {s for s in range(16) if (mask_in >> s) & 1}
+    c1 = {s for s in range(16) if (mask_out >> s) & 1}
+    return granted, rejected, joint_vote_result(c0, c1, votes)
