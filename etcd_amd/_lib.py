@@ -20,6 +20,7 @@ QB_EHIP = -2
 QB_ENOMEM = -3
 
 QB_MAX_SLOTS = 16
+QB_WIDE_MAX_SLOTS = 1024
 QB_REC_REJECT = 0x80
 QB_STAT_NAMES = ("applied", "rejected", "stale_term", "non_member", "higher_term",
                  "bad_group", "after_stepdown")
@@ -52,6 +53,8 @@ SIGNATURES = {
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_validate": (_i32, [_u64, _u32, _p, _p, _p]),
+    "qb_dev_wide_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p]),
+    "qb_dev_wide_validate": (_i32, [_u64, _u32, _p, _p, _p]),
     "qb_dev_csr_quorum_active": (_i32, [_u64, _p, _p, _p, _p]),
     "qb_dev_fixed_apply_appresp": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                           _p, _p, _p]),

@@ -160,6 +160,82 @@ def compile_configs(voters_in: Sequence[Iterable[int]], voters_out: Sequence[Ite
     return CompiledConfigs(off, cfg, np.asarray(ids, dtype=np.uint64))
 
 
+@dataclass
+class CompiledWide:
+    """Per-slot flags layout for configs wider than 16 slots (WIDE)."""
+    off: np.ndarray       # uint32 [G+1]
+    flags: np.ndarray     # uint8 [off[G]]: 1 incoming, 2 outgoing (+4 voted, 8 granted)
+    slot_ids: np.ndarray  # uint64 [off[G]]
+
+    @property
+    def G(self) -> int:
+        return len(self.off) - 1
+
+    def slots(self, g: int) -> np.ndarray:
+        return self.slot_ids[self.off[g]:self.off[g + 1]]
+
+
+def compile_configs_wide(voters_in, voters_out=None, learners=None) -> CompiledWide:
+    """tracker.Config per group -> WIDE layout (any number of slots up to
+    QB_WIDE_MAX_SLOTS); same slot order and learner rule as compile_configs."""
+    G = len(voters_in)
+    voters_out = voters_out if voters_out is not None else [()] * G
+    learners = learners if learners is not None else [()] * G
+    off = np.zeros(G + 1, dtype=np.uint32)
+    flags, ids = [], []
+    for g in range(G):
+        vi, vo, lr = set(voters_in[g]), set(voters_out[g]), set(learners[g])
+        if lr & (vi | vo):
+            raise ValueError(f"group {g}: learners {sorted(lr & (vi | vo))} are also voters")
+        slot = sorted(vi | vo | lr)
+        if len(slot) > _lib.QB_WIDE_MAX_SLOTS:
+            raise ValueError(f"group {g}: {len(slot)} slots > {_lib.QB_WIDE_MAX_SLOTS}")
+        flags += [(1 if i in vi else 0) | (2 if i in vo else 0) for i in slot]
+        ids += slot
+        off[g + 1] = off[g] + len(slot)
+    return CompiledWide(off, np.asarray(flags, np.uint8), np.asarray(ids, np.uint64))
+
+
+class WideGroups:
+    """G groups of the WIDE layout resident on one device."""
+
+    def __init__(self, off: torch.Tensor, match: torch.Tensor, flags: torch.Tensor,
+                 max_slots: Optional[int] = None):
+        for t, w in ((off, "off"), (match, "match"), (flags, "flags")):
+            _require_device(t, w)
+        self.off, self.match, self.flags = off, match, flags
+        self.G = off.numel() - 1
+        self.device = off.device
+        if max_slots is None:
+            max_slots = int((off[1:].long() - off[:-1].long()).max().item()) if self.G else 0
+        self.max_slots = max(1, min(int(max_slots), _lib.QB_WIDE_MAX_SLOTS))
+
+    @classmethod
+    def from_compiled(cls, cw: CompiledWide, match_u64, voted=None, granted=None,
+                      device="cuda"):
+        """voted / granted: optional bool arrays per slot (the votes map)."""
+        dev = torch.device(device)
+        fl = cw.flags.copy()
+        if voted is not None:
+            fl |= (np.asarray(voted, bool).astype(np.uint8) << 2)
+        if granted is not None:
+            fl |= ((np.asarray(granted, bool) & np.asarray(voted, bool)).astype(np.uint8) << 3)
+        m = np.asarray(match_u64, np.uint64)
+        return cls(torch.from_numpy(cw.off.view(np.int32).copy()).to(dev),
+                   from_u64(m if m.size else np.zeros(2, np.uint64), dev),
+                   torch.from_numpy(fl if fl.size else np.zeros(1, np.uint8)).to(dev))
+
+    def committed_vote(self, commit_out=None, vote_out=None, want_commit=True, want_vote=True):
+        if want_commit and commit_out is None:
+            commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
+        if want_vote and vote_out is None:
+            vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_wide_committed_vote", self.G, self.max_slots, _ptr(self.off),
+                  _ptr(self.match), _ptr(self.flags), _ptr(commit_out if want_commit else None),
+                  _ptr(vote_out if want_vote else None), _stream(self.device))
+        return (commit_out if want_commit else None), (vote_out if want_vote else None)
+
+
 class CsrGroups:
     """G ragged / joint groups (CSR layout) resident on one device."""
 

@@ -43,6 +43,12 @@
  *     votes[G]      uint32 = voted | granted << 16
  *     active[G]     uint16 RecentActive bits (tracker.go:215-225)
  *
+ *   WIDE   (configs with more than 16 slots, up to QB_WIDE_MAX_SLOTS; one
+ *           wavefront per group):
+ *     off[G+1]      uint32, match[off[G]] uint64 as CSR
+ *     flags[off[G]] uint8 per slot: bit 0 incoming voter, bit 1 outgoing
+ *                   voter, bit 2 voted, bit 3 granted
+ *
  *   MsgAppResp batch records (M records, any order):
  *     rec_group[M]  uint32 group index within the shard
  *     rec_flags[M]  uint8: bits 0-3 = slot, bit 7 = Reject
@@ -73,6 +79,7 @@ extern "C" {
 #define QB_VOTE_WON 3      /* quorum.VoteWon,     quorum.go:57 */
 
 #define QB_MAX_SLOTS 16
+#define QB_WIDE_MAX_SLOTS 1024
 #define QB_REC_REJECT 0x80u
 
 /* Counters filled by qb_dev_fixed_apply_appresp (device memory, uint64 each;
@@ -162,6 +169,17 @@ int qb_dev_csr_committed_vote(uint64_t G, uint32_t max_slots,
  * uint64). */
 int qb_dev_csr_validate(uint64_t G, uint32_t max_slots, const uint32_t* off,
                         uint64_t* bad_out, void* stream);
+
+/* CommittedIndex and/or VoteResult for G WIDE groups (JointConfig
+ * semantics as qb_dev_csr_committed_vote, quorum/joint.go:49-75 over
+ * quorum/majority.go:126-210).  max_slots bounds every s_g (0 =
+ * QB_WIDE_MAX_SLOTS) and sizes the per-lane register tile. */
+int qb_dev_wide_committed_vote(uint64_t G, uint32_t max_slots,
+                               const uint32_t* off, const uint64_t* match,
+                               const uint8_t* flags, uint64_t* commit_out,
+                               uint8_t* vote_out, void* stream);
+int qb_dev_wide_validate(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                         uint64_t* bad_out, void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Progress tracking (raft/tracker)                                        */

@@ -238,6 +238,50 @@ void orc_fixed_eval(u32 n, u64 G, const u64* match, const void* voted, const voi
   }
 }
 
+/* WIDE layout: per-slot flags (1 in, 2 out, 4 voted, 8 granted), any size.
+ * The reference sorts with insertionSort (majority.go:115-122); for wide
+ * halves the oracle uses qsort beyond 64 members — srt[n-(n/2+1)] of an
+ * ascending sort does not depend on the sorting algorithm. */
+static int cmp_u64(const void* a, const void* b) {
+  u64 x = *(const u64*)a, y = *(const u64*)b;
+  return x < y ? -1 : x > y;
+}
+static u64 wide_half_ci(const u64* m, const u8* fl, u32 s, u32 bit, u64* scratch) {
+  int n = 0;
+  for (u32 j = 0; j < s; ++j)
+    if ((fl[j] >> bit) & 1) scratch[n++] = m[j];
+  if (n == 0) return INF;
+  if (n <= 64) insertion_sort(scratch, n);
+  else qsort(scratch, (size_t)n, sizeof(u64), cmp_u64);
+  return scratch[n - (n / 2 + 1)];
+}
+static u8 wide_half_vote(const u8* fl, u32 s, u32 bit) {
+  int n = 0, yes = 0, no = 0;
+  for (u32 j = 0; j < s; ++j) {
+    if (!((fl[j] >> bit) & 1)) continue;
+    ++n;
+    if (fl[j] & 4) {
+      if (fl[j] & 8) ++yes;
+      else ++no;
+    }
+  }
+  return majority_vote(n, yes, no);
+}
+void orc_wide_eval(u64 G, const u32* off, const u64* match, const u8* flags, u64* commit,
+                   u8* vote) {
+  u64* scratch = (u64*)malloc(sizeof(u64) * 4096);
+  for (u64 g = 0; g < G; ++g) {
+    u32 a = off[g], s = off[g + 1] - a;
+    if (commit) {
+      u64 c0 = wide_half_ci(match + a, flags + a, s, 0, scratch);
+      u64 c1 = wide_half_ci(match + a, flags + a, s, 1, scratch);
+      commit[g] = c0 < c1 ? c0 : c1;
+    }
+    if (vote) vote[g] = joint_vote(wide_half_vote(flags + a, s, 0), wide_half_vote(flags + a, s, 1));
+  }
+  free(scratch);
+}
+
 void orc_csr_quorum_active(u64 G, const u32* cfg, const u16* active, u8* won) {
   for (u64 g = 0; g < G; ++g) { /* tracker.go:215-225: every voter "voted" */
     u32 min_ = cfg[g] & 0xFFFF, mout = cfg[g] >> 16, a = active[g];

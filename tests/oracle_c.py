@@ -23,6 +23,7 @@ SIG = {
     "orc_csr_eval": (None, [_u64, _p, _p, _p, _p, _p, _p]),
     "orc_fixed_eval": (None, [_u32, _u64, _p, _p, _p, _p, _p]),
     "orc_csr_quorum_active": (None, [_u64, _p, _p, _p]),
+    "orc_wide_eval": (None, [_u64, _p, _p, _p, _p, _p]),
     "orc_group_maps_size": (C.c_size_t, []),
     "orc_faithful_build_fixed": (None, [_u32, _u64, _p, _p, _p, _p]),
     "orc_faithful_eval": (None, [_u64, _p, _p, _p]),
@@ -106,6 +107,17 @@ def csr_eval(off, match, cfg, votes, threads=1):
                             threads)
     else:
         lib.orc_csr_eval(G, ptr(off), ptr(m), ptr(cfg), ptr(votes), ptr(commit), ptr(vote))
+    return commit, vote
+
+
+def wide_eval(off, match, flags):
+    lib = load()
+    G = len(off) - 1
+    commit = np.empty(G, np.uint64)
+    vote = np.empty(G, np.uint8)
+    m = match if match.size else np.zeros(1, np.uint64)
+    f = flags if flags.size else np.zeros(1, np.uint8)
+    lib.orc_wide_eval(G, ptr(off), ptr(m), ptr(f), ptr(commit), ptr(vote))
     return commit, vote
 
 

@@ -174,3 +174,34 @@ def test_sequential_appresp_matches_python():
     assert st["committed"].tolist() == com
     assert st["stepped_down"].astype(bool).tolist() == down
     assert int(stats.sum()) == M
+
+
+def _random_wide(rng, G, smax, big=True):
+    off = [0]
+    vals, flags = [], []
+    for _ in range(G):
+        s = rng.randrange(0, smax + 1)
+        for _ in range(s):
+            hi = (1 << 64) - 1 if big and rng.random() < 0.3 else 50
+            vals.append(rng.randrange(0, hi + 1))
+            f = rng.getrandbits(2)
+            if rng.random() < 0.7:
+                f |= 4 | (8 if rng.random() < 0.6 else 0)
+            flags.append(f)
+        off.append(off[-1] + s)
+    return (np.asarray(off, np.uint32), np.asarray(vals, np.uint64),
+            np.asarray(flags, np.uint8))
+
+
+def test_wide_eval_matches_python():
+    rng = random.Random(21)
+    off, vals, flags = _random_wide(rng, 400, 150)
+    c, v = oc.wide_eval(off, vals, flags)
+    for g in range(len(off) - 1):
+        a, b = int(off[g]), int(off[g + 1])
+        c0 = {j for j in range(a, b) if flags[j] & 1}
+        c1 = {j for j in range(a, b) if flags[j] & 2}
+        acked = {j: int(vals[j]) for j in range(a, b)}
+        votes = {j: bool(flags[j] & 8) for j in range(a, b) if flags[j] & 4}
+        assert int(c[g]) == q.joint_committed_index(c0, c1, acked)
+        assert int(v[g]) == q.joint_vote_result(c0, c1, votes)
