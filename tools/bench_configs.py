@@ -44,6 +44,18 @@ def time_region(fn, reps, warm=3):
     return t
 
 
+def cpu_rate(fn, groups, seconds=2.0):
+    """groups/s of a CPU oracle call repeated for ~seconds."""
+    import time
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return reps * groups / dt
+
+
 def report(name, groups, t, algo_bytes, extra=None):
     gbs = algo_bytes / t / 1e9
     d = {"config": name, "groups_per_s": groups / t, "per_launch_us": t * 1e6,
@@ -63,7 +75,17 @@ def csr_config(kind, G, reps):
     t = time_region(lambda: grp.committed_vote(c, v), reps)
     # off (4) + cfg (4) + votes (4) + match (8 s) + commit (8) + vote (1)
     algo = G * (4 + 4 + 4 + 8 + 1) + 8 * slots + 4
-    report(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G})
+    # CPU beside it: the oracle's SoA C restatement on a bounded sample
+    from tests import oracle_c as oc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    Gs = 1 << 20
+    off, m, cfg, votes = oc.gen_csr(0x5EED0003 if kind == "ragged" else 0x5EED0004, kind, Gs)
+    cpu = cpu_rate(lambda: oc.csr_eval(off, m, cfg, votes, threads=threads), Gs)
+    cpu1 = cpu_rate(lambda: oc.csr_eval(off, m, cfg, votes), Gs)
+    report(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G,
+           "cpu_baseline": {"value": cpu, "unit": "groups/s", "cores": threads, "kind": "port",
+                            "value_1thread": cpu1,
+                            "sample": f"{Gs} groups, C SoA restatement (oracle)"}})
 
 
 def tracker_config(G, reps, seed=55):
@@ -107,9 +129,27 @@ def tracker_config(G, reps, seed=55):
     # record 21 B + match RMW 16 B per message; commit advance
     # reads match 40 + term_start 8 + committed 8, writes committed 8 per group
     algo = G * (21 + 16) + G * 64
+    # CPU beside it: the sequential one-record-at-a-time oracle (the Go
+    # stepLeader loop restated) on a bounded sample, 1 thread
+    from tests import oracle_c as oc
+    Gs = 1 << 20
+    m0, _, _, ts0 = oc.gen_fixed(0x5EED0005, n, Gs)
+    st = {"match": m0, "active": np.zeros(Gs, np.uint16), "term": np.full(Gs, 7, np.uint64),
+          "term_start": ts0, "committed": np.zeros(Gs, np.uint64),
+          "stepped_down": np.zeros(Gs, np.uint8)}
+    oc.commit_all(n, st["match"], ts0, st["committed"])
+    grp_ = rng.integers(0, Gs, size=Gs).astype(np.uint32)
+    flg = rng.integers(1, n, size=Gs).astype(np.uint8)
+    lag = rng.integers(0, 96, size=Gs).astype(np.uint64)
+    lst = m0[0][grp_]
+    idx = np.where(lag < lst, lst - lag, np.uint64(0))
+    trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
+    cpu1 = cpu_rate(lambda: oc.appresp_sequential(n, Gs, (grp_, flg, idx, trm), st), Gs)
     report("streaming tracker (bucketed step)", G, t, algo,
            {"two_call_us": t_two * 1e6, "atomic_apply_us": t_apply * 1e6,
-            "commit_advance_us": t_commit * 1e6, "unit": "group-steps/s"})
+            "commit_advance_us": t_commit * 1e6, "unit": "group-steps/s",
+            "cpu_baseline": {"value": cpu1, "unit": "group-steps/s", "cores": 1, "kind": "port",
+                             "sample": f"{Gs} records on {Gs} groups, sequential C restatement"}})
 
 
 def main():
