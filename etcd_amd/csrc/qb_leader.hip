@@ -1,0 +1,760 @@
+// qb_leader.hip — the leader inbox step over G raft groups (gfx950).
+//
+// A batch of responses (MsgAppResp, MsgHeartbeatResp, MsgSnapStatus,
+// MsgUnreachable) is applied with the reference's sequential per-message
+// semantics: every group's records in batch order, groups independent.
+// Reference (paths relative to raft/):
+//   raft.Step term filter                 raft.go:847-921
+//   stepLeader                            raft.go:1099-1342
+//   maybeSendAppend / bcastAppend         raft.go:423-492, 515-522
+//   maybeCommit                           raft.go:585-588, log.go:328-334
+//   raftLog.term / entries                log.go:268-299 (slice bounds 338-398)
+//   findConflictByTerm                    log.go:150-171
+//   Progress                              tracker/progress.go:85-212
+//   Inflights                             tracker/inflights.go:55-132
+//   readOnly.recvAck / advance            read_only.go:68-121
+//   responseToReadIndexReq                raft.go:1737-1752
+//
+// Pipeline:
+//   L1 k_ld_count    per record: atomic count per group (bad groups counted)
+//   L2 scan          exclusive scan of the counts -> each group's record run
+//   L3 k_ld_scatter  per record: its batch index into its group's run
+//   L4 k_ld_step     one thread per group: sort its run by batch index
+//                    (records arrive in any order), then the sequential
+//                    stepLeader over its Progress / log view / read queue;
+//                    messages into an 8-slot per-group area of the workspace,
+//                    spilling into 32-message chunks from a shared pool
+//   L5 scan          exclusive scan of the message counts
+//   L6 k_ld_emit     one thread per group copies its messages to their final
+//                    place (group order, emission order within a group)
+// Only L4 is control-heavy; it touches a group's state only if the group has
+// records.
+#include "qb_common.h"
+#include "qb_scan.h"
+
+namespace qb {
+namespace ld {
+
+constexpr u32 kFix = 8;         // messages per group kept in the fixed area
+constexpr u32 kChunk = 32;      // messages per overflow chunk
+constexpr u32 kNone = 0xFFFFFFFFu;
+constexpr u8 kNoSlot = 0xFF;
+
+struct Msg {
+  u64 index, log_term, commit, aux;
+  u32 group;
+  u8 to, type;
+  u16 reserved;
+};
+static_assert(sizeof(Msg) == sizeof(qb_msg_out), "qb_msg_out layout");
+
+inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// The ABI's uint64_t is unsigned long; HIP atomics and qb helpers use u64.
+__host__ __device__ __forceinline__ u64* U(uint64_t* p) { return reinterpret_cast<u64*>(p); }
+__host__ __device__ __forceinline__ const u64* U(const uint64_t* p) {
+  return reinterpret_cast<const u64*>(p);
+}
+
+struct Carve {
+  size_t cnt, bsum, cursor, perm, mcnt, mbsum, fix, chead, cnext, chunks, pool, shards, total;
+  u64 nchunks;
+};
+inline Carve carve(u64 G, u64 M) {
+  Carve c{};
+  size_t o = 0;
+  c.cnt = o;    o += up256(sizeof(u32) * (G + 1));
+  c.bsum = o;   o += up256(sizeof(u32) * (scan::blocks(G) + 1));
+  c.cursor = o; o += up256(sizeof(u32) * (G + 1));
+  c.perm = o;   o += up256(sizeof(u32) * (M + 1));
+  c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
+  c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
+  c.fix = o;    o += up256(sizeof(Msg) * kFix * G);
+  c.chead = o;  o += up256(sizeof(u32) * (G + 1));
+  c.nchunks = M / 8 + 1024;  // 4 spilled messages per record on average
+  c.cnext = o;  o += up256(sizeof(u32) * c.nchunks);
+  c.chunks = o; o += up256(sizeof(Msg) * kChunk * c.nchunks);
+  c.pool = o;   o += up256(sizeof(u32) * 2);
+  c.shards = o; o += up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
+  c.total = o;
+  return c;
+}
+
+struct Args {
+  qb_leader_groups lg;
+  qb_leader_inbox in;
+  const u32* cnt;     // exclusive scan of per-group record counts, [G+1]
+  u32* perm;          // batch indexes grouped by group
+  u32* mcnt;          // messages per group
+  Msg* fix;           // [G * kFix]
+  u32* chead;         // first overflow chunk per group
+  u32* cnext;         // chunk links
+  Msg* chunks;        // [nchunks * kChunk]
+  u32* pool;          // [0] = next free chunk
+  u64 nchunks;
+  u64* shards;        // [64][QB_LSTAT_COUNT]
+  u32* stepdown_at;
+  u8* gflags;
+};
+
+// ------------------------------------------------------------ L1 / L3 ----
+__global__ __launch_bounds__(kBlock) void k_ld_count(u64 G, u64 M, const u32* __restrict__ rg,
+                                                     u32* __restrict__ cnt, u64* __restrict__ shards) {
+  __shared__ u32 lds[1];
+  BlockTally<1> tally;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < M; i += stride) {
+    const u32 g = rg[i];
+    const bool bad = g >= G;
+    if (!bad) atomicAdd(cnt + g, 1u);
+    tally.add(0, bad);
+  }
+  const int slot[1] = {QB_LSTAT_BAD_GROUP};
+  tally.flush(lds, shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ld_scatter(u64 G, u64 M, const u32* __restrict__ rg,
+                                                       u32* __restrict__ cursor,
+                                                       u32* __restrict__ perm) {
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < M; i += stride) {
+    const u32 g = rg[i];
+    if (g < G) perm[atomicAdd(cursor + g, 1u)] = u32(i);
+  }
+}
+
+// ------------------------------------------------------------------ L4 ----
+// Per-group view of the leader (one thread).
+struct Group {
+  u64 g;
+  u32 s0, ns;           // first slot, number of slots
+  u32 mask_in, mask_out;
+  u32 meta;
+  u64 term, committed, first, last, snap_i, snap_t, max_ents;
+  u32 nruns;
+  u32 nmsg, stored;     // messages generated / stored (the pool can run out)
+  u32 chunk;            // current overflow chunk
+  bool dropped;
+};
+
+__device__ __forceinline__ u32 leader_slot(const Group& G_) { return G_.meta & 0xFFu; }
+__device__ __forceinline__ u32 transferee(const Group& G_) { return (G_.meta >> 8) & 0xFFu; }
+
+// raftLog.term (log.go:268-288, zeroTermOnErrCompacted): 0 outside
+// [firstIndex-1, lastIndex]; otherwise the term of the run holding i.
+__device__ u64 log_term(const Args& A, const Group& G_, u64 i) {
+  const u64 dummy = G_.first - 1;
+  if (i < dummy || i > G_.last) return 0;
+  u64 t = 0;
+  const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
+  const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
+  for (u32 r = 0; r < G_.nruns; ++r)
+    if (rs[r] <= i) t = rt[r];
+  return t;
+}
+
+// log.go:150-171, one run at a time instead of one index at a time: inside a
+// run every index has the run's term, so when that term is above `term` the
+// whole run (down to the dummy entry) is skipped.
+__device__ u64 find_conflict_by_term(const Args& A, const Group& G_, u64 index, u64 term) {
+  if (index > G_.last) return index;
+  const u64 dummy = G_.first - 1;
+  const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
+  const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
+  for (;;) {
+    if (index < dummy || index > G_.last) return index;  // term 0 <= term
+    u64 t = 0, start = 0;
+    for (u32 r = 0; r < G_.nruns; ++r)
+      if (rs[r] <= index) {
+        t = rt[r];
+        start = rs[r];
+      }
+    if (t <= term) return index;
+    const u64 lo = start > dummy ? start : dummy;
+    index = lo - 1;  // wraps at 0 exactly like the reference's index--
+  }
+}
+
+__device__ void emit(const Args& A, Group& G_, u8 type, u32 to, u64 index, u64 log_term_,
+                     u64 commit, u64 aux) {
+  Msg m;
+  m.index = index;
+  m.log_term = log_term_;
+  m.commit = commit;
+  m.aux = aux;
+  m.group = u32(G_.g);
+  m.to = u8(to);
+  m.type = type;
+  m.reserved = 0;
+  const u32 k = G_.nmsg++;
+  if (G_.dropped) return;
+  if (k < kFix) {
+    A.fix[G_.g * kFix + k] = m;
+    G_.stored = k + 1;
+    return;
+  }
+  const u32 kk = k - kFix;
+  if (kk % kChunk == 0) {  // needs a new chunk
+    const u32 c = atomicAdd(A.pool, 1u);
+    if (c >= A.nchunks) {
+      G_.dropped = true;
+      return;
+    }
+    if (kk == 0) A.chead[G_.g] = c;
+    else A.cnext[G_.chunk] = c;
+    G_.chunk = c;
+  }
+  A.chunks[u64(G_.chunk) * kChunk + kk % kChunk] = m;
+  G_.stored = k + 1;
+}
+
+// Progress accessors (slot j of the group).
+struct Pr {
+  u64* match;
+  u64* next;
+  u64* psnap;
+  u8* st;
+  u32* ipos;
+  u64* ibuf;
+  u32 K;
+};
+__device__ __forceinline__ Pr pr_of(const Args& A, const Group& G_, u32 j) {
+  const u64 p = u64(G_.s0) + j;
+  return Pr{U(A.lg.match) + p, U(A.lg.next) + p, U(A.lg.pending_snapshot) + p, A.lg.pstate + p,
+            A.lg.infl_pos + p, U(A.lg.infl_buf) + p * A.lg.inflight_cap, A.lg.inflight_cap};
+}
+__device__ __forceinline__ u32 st_state(u8 s) { return s & 3u; }
+
+// inflights.go
+__device__ __forceinline__ bool infl_full(const Pr& p) { return (*p.ipos >> 16) == p.K; }
+__device__ __forceinline__ void infl_reset(const Pr& p) { *p.ipos = 0; }
+__device__ void infl_add(const Pr& p, u64 v) {
+  const u32 pos = *p.ipos;
+  const u32 start = pos & 0xFFFFu, count = pos >> 16;
+  u32 nxt = start + count;
+  if (nxt >= p.K) nxt -= p.K;
+  p.ibuf[nxt] = v;
+  *p.ipos = start | ((count + 1) << 16);
+}
+__device__ void infl_free_le(const Pr& p, u64 to) {
+  const u32 pos = *p.ipos;
+  const u32 start = pos & 0xFFFFu, count = pos >> 16;
+  if (count == 0 || to < p.ibuf[start]) return;
+  u32 idx = start, i = 0;
+  for (; i < count; ++i) {
+    if (to < p.ibuf[idx]) break;
+    if (++idx >= p.K) idx -= p.K;
+  }
+  const u32 c2 = count - i;
+  *p.ipos = c2 == 0 ? 0u : (idx | (c2 << 16));
+}
+
+// progress.go
+__device__ __forceinline__ void reset_state(const Pr& p, u32 state) {
+  *p.st = u8((*p.st & QB_PR_RECENT_ACTIVE) | state);  // ProbeSent = false
+  *p.psnap = 0;
+  infl_reset(p);
+}
+__device__ void become_probe(const Pr& p) {
+  const u64 m1 = *p.match + 1;
+  if (st_state(*p.st) == QB_PR_SNAPSHOT) {
+    const u64 ps1 = *p.psnap + 1;
+    reset_state(p, QB_PR_PROBE);
+    *p.next = m1 > ps1 ? m1 : ps1;
+  } else {
+    reset_state(p, QB_PR_PROBE);
+    *p.next = m1;
+  }
+}
+__device__ __forceinline__ void become_replicate(const Pr& p) {
+  reset_state(p, QB_PR_REPLICATE);
+  *p.next = *p.match + 1;
+}
+__device__ __forceinline__ void become_snapshot(const Pr& p, u64 snapi) {
+  reset_state(p, QB_PR_SNAPSHOT);
+  *p.psnap = snapi;
+}
+__device__ __forceinline__ bool is_paused(const Pr& p) {
+  const u8 s = *p.st;
+  switch (st_state(s)) {
+    case QB_PR_PROBE: return (s & QB_PR_PROBE_SENT) != 0;
+    case QB_PR_REPLICATE: return infl_full(p);
+    default: return true;
+  }
+}
+__device__ bool maybe_update(const Pr& p, u64 n) {
+  bool updated = false;
+  if (*p.match < n) {
+    *p.match = n;
+    updated = true;
+    *p.st = u8(*p.st & ~QB_PR_PROBE_SENT);
+  }
+  const u64 n1 = n + 1;
+  if (*p.next < n1) *p.next = n1;
+  return updated;
+}
+__device__ bool maybe_decr_to(const Pr& p, u64 rejected, u64 hint) {
+  if (st_state(*p.st) == QB_PR_REPLICATE) {
+    if (rejected <= *p.match) return false;
+    *p.next = *p.match + 1;
+    return true;
+  }
+  if (*p.next - 1 != rejected) return false;
+  const u64 h1 = hint + 1;
+  const u64 mn = rejected < h1 ? rejected : h1;
+  *p.next = mn > 1 ? mn : 1;
+  *p.st = u8(*p.st & ~QB_PR_PROBE_SENT);
+  return true;
+}
+
+// raft.go:432-492
+__device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if_empty) {
+  const Pr p = pr_of(A, G_, to);
+  if (is_paused(p)) return false;
+  const u64 nx = *p.next;
+  const u64 term = log_term(A, G_, nx - 1);
+  u64 n = 0;
+  bool compacted = false;
+  if (nx <= G_.last) {
+    if (nx < G_.first) compacted = true;
+    else {
+      const u64 avail = G_.last - nx + 1;
+      n = avail < G_.max_ents ? avail : G_.max_ents;
+    }
+  }
+  if (n == 0 && !send_if_empty) return false;
+  if (compacted) {
+    if (!(*p.st & QB_PR_RECENT_ACTIVE)) return false;
+    if (G_.snap_i == 0) return false;  // ErrSnapshotTemporarilyUnavailable
+    emit(A, G_, QB_MSG_SNAP, to, G_.snap_i, G_.snap_t, 0, 0);
+    become_snapshot(p, G_.snap_i);
+    return true;
+  }
+  emit(A, G_, QB_MSG_APP, to, nx - 1, term, G_.committed, n);
+  if (n != 0) {
+    const u32 s = st_state(*p.st);
+    if (s == QB_PR_REPLICATE) {
+      const u64 last = nx + n - 1;
+      *p.next = last + 1;
+      infl_add(p, last);
+    } else if (s == QB_PR_PROBE) {
+      *p.st = u8(*p.st | QB_PR_PROBE_SENT);
+    }
+  }
+  return true;
+}
+
+// tracker.go:177-179 -> joint.go:49-56 -> majority.go:126-172: the q-th
+// largest match among a half's voters = the largest member value v with
+// #{members >= v} >= q.
+__device__ u64 half_ci(const u64 (&m)[QB_MAX_SLOTS], u32 mask) {
+  if (mask == 0) return kInf;
+  const int q = __popc(mask) / 2 + 1;
+  u64 best = 0;
+#pragma unroll
+  for (int i = 0; i < QB_MAX_SLOTS; ++i) {
+    if (!((mask >> i) & 1u)) continue;
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < QB_MAX_SLOTS; ++j) c += ((mask >> j) & 1u) && m[j] >= m[i];
+    if (c >= q && m[i] > best) best = m[i];
+  }
+  return best;
+}
+
+__device__ bool maybe_commit(const Args& A, Group& G_) {
+  u64 m[QB_MAX_SLOTS];
+  const u64* mp = U(A.lg.match) + G_.s0;
+#pragma unroll
+  for (int j = 0; j < QB_MAX_SLOTS; ++j) m[j] = u32(j) < G_.ns ? mp[j] : 0ull;
+  const u64 a = half_ci(m, G_.mask_in), b = half_ci(m, G_.mask_out);
+  const u64 mci = a < b ? a : b;
+  if (mci > G_.committed && log_term(A, G_, mci) == G_.term) {
+    G_.committed = mci;
+    return true;
+  }
+  return false;
+}
+
+__device__ void bcast_append(const Args& A, Group& G_) {
+  for (u32 s = 0; s < G_.ns; ++s)
+    if (s != leader_slot(G_)) maybe_send_append(A, G_, s, true);
+}
+
+// joint.go:61-75 over majority.go:178-210 with votes = acks (all true).
+__device__ __forceinline__ u8 acks_vote(const Group& G_, u32 acks) {
+  const u8 r1 = vote_from_counts(__popc(G_.mask_in), __popc(G_.mask_in & acks),
+                                 __popc(G_.mask_in & acks));
+  const u8 r2 = vote_from_counts(__popc(G_.mask_out), __popc(G_.mask_out & acks),
+                                 __popc(G_.mask_out & acks));
+  return joint_vote(r1, r2);
+}
+
+__device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 ctx) {
+  *p.st = u8((*p.st | QB_PR_RECENT_ACTIVE) & ~QB_PR_PROBE_SENT);
+  if (st_state(*p.st) == QB_PR_REPLICATE && infl_full(p)) {
+    const u32 start = *p.ipos & 0xFFFFu;
+    infl_free_le(p, p.ibuf[start]);  // FreeFirstOne
+  }
+  if (*p.match < G_.last) maybe_send_append(A, G_, slot, true);
+  if (A.lg.read_only != QB_READ_ONLY_SAFE || ctx == 0) return;
+  // read_only.go:68-79 recvAck
+  const u32 cap = A.lg.readq_cap;
+  const u32 qlen = (G_.meta >> 20) & 0x1Fu;
+  u64* qctx = U(A.lg.rq_ctx) + G_.g * cap;
+  u64* qidx = U(A.lg.rq_index) + G_.g * cap;
+  u32* qmeta = A.lg.rq_meta + G_.g * cap;
+  u32 found = kNone;
+  for (u32 k = 0; k < qlen; ++k)
+    if (qctx[k] == ctx) {
+      found = k;
+      break;
+    }
+  u32 acks = 0;  // a nil map when the context is unknown
+  if (found != kNone) {
+    qmeta[found] |= 1u << slot;
+    acks = qmeta[found] & 0xFFFFu;
+  }
+  if (acks_vote(G_, acks) != QB_VOTE_WON) return;
+  if (found == kNone) return;  // advance finds nothing (read_only.go:113-121)
+  // read_only.go:84-112 advance + raft.go:1304-1308 responses, oldest first.
+  for (u32 k = 0; k <= found; ++k) {
+    const u32 from = qmeta[k] >> 16;
+    if (from == kNoSlot || from == leader_slot(G_))
+      emit(A, G_, QB_READ_STATE, kNoSlot, qidx[k], 0, 0, qctx[k]);
+    else
+      emit(A, G_, QB_MSG_READ_INDEX_RESP, from, qidx[k], 0, 0, qctx[k]);
+  }
+  const u32 rest = qlen - (found + 1);
+  for (u32 k = 0; k < rest; ++k) {
+    qctx[k] = qctx[k + found + 1];
+    qidx[k] = qidx[k + found + 1];
+    qmeta[k] = qmeta[k + found + 1];
+  }
+  G_.meta = (G_.meta & ~(0x1Fu << 20)) | (rest << 20);
+}
+
+__device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 index, bool reject,
+                         u64 hint, u64 hint_term, u8& gfl) {
+  *p.st = u8(*p.st | QB_PR_RECENT_ACTIVE);
+  if (reject) {
+    u64 next_probe = hint;
+    if (hint_term > 0) next_probe = find_conflict_by_term(A, G_, hint, hint_term);
+    if (maybe_decr_to(p, index, next_probe)) {
+      if (st_state(*p.st) == QB_PR_REPLICATE) become_probe(p);
+      maybe_send_append(A, G_, slot, true);
+    }
+    return;
+  }
+  const bool old_paused = is_paused(p);
+  if (!maybe_update(p, index)) return;
+  const u32 s = st_state(*p.st);
+  if (s == QB_PR_PROBE) {
+    become_replicate(p);
+  } else if (s == QB_PR_SNAPSHOT && *p.match >= *p.psnap) {
+    become_probe(p);
+    become_replicate(p);
+  } else if (s == QB_PR_REPLICATE) {
+    infl_free_le(p, index);
+  }
+  if (maybe_commit(A, G_)) {
+    gfl |= QB_LFLAG_ADVANCED;
+    if (G_.meta & QB_META_PENDING_READINDEX) {
+      // releasePendingReadIndexMessages (raft.go:1813-1825) is the host's.
+      G_.meta &= ~QB_META_PENDING_READINDEX;
+      gfl |= QB_LFLAG_RELEASE_READS;
+    }
+    bcast_append(A, G_);
+  } else if (old_paused) {
+    maybe_send_append(A, G_, slot, true);
+  }
+  while (maybe_send_append(A, G_, slot, false)) {
+  }
+  if (slot == transferee(G_) && *p.match == G_.last)
+    emit(A, G_, QB_MSG_TIMEOUT_NOW, slot, 0, 0, 0, 0);
+}
+
+__device__ void snap_status(const Pr& p, bool reject) {
+  if (st_state(*p.st) != QB_PR_SNAPSHOT) return;
+  if (reject) *p.psnap = 0;
+  become_probe(p);
+  *p.st = u8(*p.st | QB_PR_PROBE_SENT);
+}
+
+// Sort a group's run of batch indexes ascending (runs are short: insertion
+// sort; long runs: heapsort, both in place).
+__device__ void sort_run(u32* a, u32 n) {
+  if (n <= 32) {
+    for (u32 i = 1; i < n; ++i) {
+      const u32 v = a[i];
+      u32 j = i;
+      while (j > 0 && a[j - 1] > v) {
+        a[j] = a[j - 1];
+        --j;
+      }
+      a[j] = v;
+    }
+    return;
+  }
+  auto sift = [&](u32 root, u32 end) {
+    for (;;) {
+      u32 c = 2 * root + 1;
+      if (c >= end) return;
+      if (c + 1 < end && a[c + 1] > a[c]) ++c;
+      if (a[root] >= a[c]) return;
+      const u32 t = a[root];
+      a[root] = a[c];
+      a[c] = t;
+      root = c;
+    }
+  };
+  for (u32 i = n / 2; i-- > 0;) sift(i, n);
+  for (u32 e = n - 1; e > 0; --e) {
+    const u32 t = a[0];
+    a[0] = a[e];
+    a[e] = t;
+    sift(0, e);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
+  __shared__ u32 lds[7];
+  BlockTally<7> tally;
+  const u64 G = A.lg.G;
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  u32 napplied = 0, nstale = 0, nhigher = 0, nnon = 0, nafter = 0;
+  u32 nmsg = 0, nstored = 0;
+  if (g < G) {
+    const u32 r0 = A.cnt[g], r1 = A.cnt[g + 1];
+    u32 stepdown = kNone;
+    u8 gfl = 0;
+    if (r1 > r0) {
+      Group G_;
+      G_.g = g;
+      G_.s0 = A.lg.off[g];
+      G_.ns = A.lg.off[g + 1] - G_.s0;
+      const u32 c = A.lg.cfg[g];
+      G_.mask_in = c & 0xFFFFu;
+      G_.mask_out = c >> 16;
+      G_.meta = A.lg.meta[g];
+      G_.term = A.lg.term[g];
+      G_.committed = A.lg.committed[g];
+      G_.first = A.lg.first_index[g];
+      G_.last = A.lg.last_index[g];
+      G_.snap_i = A.lg.snap_index[g];
+      G_.snap_t = A.lg.snap_term[g];
+      G_.max_ents = A.lg.max_ents[g];
+      G_.nruns = (G_.meta >> 16) & 0xFu;
+      G_.nmsg = 0;
+      G_.stored = 0;
+      G_.chunk = 0;
+      G_.dropped = false;
+      u32* run = A.perm + r0;
+      sort_run(run, r1 - r0);
+      for (u32 k = r0; k < r1; ++k) {
+        const u32 i = A.perm[k];
+        if (stepdown != kNone) {
+          ++nafter;
+          continue;
+        }
+        const u64 t = A.in.term[i];
+        const u32 f = A.in.flags[i];
+        if (t != 0 && t > G_.term) {  // raft.go:852-880: becomeFollower
+          stepdown = i;
+          ++nhigher;
+          continue;
+        }
+        if (t != 0 && t < G_.term) {  // raft.go:883-921: ignored
+          ++nstale;
+          continue;
+        }
+        const u32 slot = f & 0x0Fu;
+        if (slot >= G_.ns) {  // raft.go:1099-1104: no progress
+          ++nnon;
+          continue;
+        }
+        ++napplied;
+        const Pr p = pr_of(A, G_, slot);
+        const u32 kind = (f >> 4) & 3u;
+        const bool reject = (f & QB_REC_REJECT) != 0;
+        if (kind == QB_IN_APP_RESP) {
+          const u64 hint = reject && A.in.hint ? A.in.hint[i] : 0;
+          const u64 ht = reject && A.in.log_term ? A.in.log_term[i] : 0;
+          app_resp(A, G_, slot, p, A.in.index[i], reject, hint, ht, gfl);
+        } else if (kind == QB_IN_HEARTBEAT_RESP) {
+          heartbeat_resp(A, G_, slot, p, A.in.index[i]);
+        } else if (kind == QB_IN_SNAP_STATUS) {
+          snap_status(p, reject);
+        } else if (st_state(*p.st) == QB_PR_REPLICATE) {  // MsgUnreachable
+          become_probe(p);
+        }
+      }
+      if (stepdown != kNone) gfl |= QB_LFLAG_STEPPED_DOWN;
+      A.lg.committed[g] = G_.committed;
+      A.lg.meta[g] = G_.meta;
+      nmsg = G_.nmsg;
+      nstored = G_.stored;
+    }
+    A.mcnt[g] = nstored;
+    if (A.stepdown_at) A.stepdown_at[g] = stepdown;
+    if (A.gflags) A.gflags[g] = gfl;
+  }
+  // Per-wave sums of per-thread counts, then one flush per block.
+  auto wsum = [](u32 v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  tally.t[0] += wsum(napplied);
+  tally.t[1] += wsum(nstale);
+  tally.t[2] += wsum(nhigher);
+  tally.t[3] += wsum(nnon);
+  tally.t[4] += wsum(nafter);
+  tally.t[5] += wsum(nmsg);
+  tally.t[6] += wsum(nmsg - nstored);
+  const int slot[7] = {QB_LSTAT_APPLIED, QB_LSTAT_STALE_TERM, QB_LSTAT_HIGHER_TERM,
+                       QB_LSTAT_NON_MEMBER, QB_LSTAT_AFTER_STEPDOWN, QB_LSTAT_MSGS,
+                       QB_LSTAT_MSGS_DROPPED};
+  tally.flush(lds, A.shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+}
+
+// ------------------------------------------------------------------ L6 ----
+__global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict__ moff,
+                                                    const Msg* __restrict__ fix,
+                                                    const u32* __restrict__ chead,
+                                                    const u32* __restrict__ cnext,
+                                                    const Msg* __restrict__ chunks,
+                                                    Msg* __restrict__ out, u64 cap,
+                                                    u32* __restrict__ msg_off,
+                                                    u64* __restrict__ msg_total,
+                                                    u64* __restrict__ shards) {
+  __shared__ u32 lds[1];
+  BlockTally<1> tally;
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  u32 dropped = 0;
+  if (g < G) {
+    const u64 o = moff[g];
+    const u32 n = moff[g + 1] - moff[g];
+    if (msg_off) msg_off[g] = u32(o);
+    if (g == G - 1) {
+      if (msg_off) msg_off[G] = moff[G];
+      *msg_total = moff[G];
+    }
+    u32 chunk = n > kFix ? chead[g] : 0;
+    for (u32 k = 0; k < n; ++k) {
+      const Msg* src;
+      if (k < kFix) {
+        src = fix + g * kFix + k;
+      } else {
+        const u32 kk = k - kFix;
+        if (kk && kk % kChunk == 0) chunk = cnext[chunk];
+        src = chunks + u64(chunk) * kChunk + kk % kChunk;
+      }
+      if (o + k < cap) out[o + k] = *src;
+      else ++dropped;
+    }
+  }
+  for (int o2 = 32; o2 > 0; o2 >>= 1) dropped += __shfl_xor(dropped, o2, 64);
+  tally.t[0] = dropped;
+  const int slot[1] = {QB_LSTAT_MSGS_DROPPED};
+  tally.flush(lds, shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+}
+
+__global__ void k_ld_fold(const u64* __restrict__ shards, u64* __restrict__ stats) {
+  const int k = threadIdx.x;
+  if (k >= QB_LSTAT_COUNT) return;
+  u64 s = 0;
+  for (int i = 0; i < 64; ++i) s += shards[i * QB_LSTAT_COUNT + k];
+  stats[k] += s;
+}
+
+}  // namespace ld
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" size_t qb_leader_workspace_bytes(uint64_t G, uint64_t M) {
+  return ld::carve(G, M).total;
+}
+
+extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
+                                  qb_msg_out* msgs, uint64_t msg_cap, uint64_t* msg_total,
+                                  uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags,
+                                  uint64_t* stats, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  QB_REQUIRE(lg && in, "qb_dev_leader_step: lg and in are required");
+  const u64 G = lg->G, M = in->M;
+  QB_REQUIRE(G < (1ull << 32) && M < (1ull << 32), "qb_dev_leader_step: G and M must be < 2^32");
+  QB_REQUIRE(lg->inflight_cap >= 1 && lg->inflight_cap <= 4096,
+             "qb_dev_leader_step: inflight_cap must be 1..4096");
+  QB_REQUIRE(lg->readq_cap <= QB_LEADER_MAX_READQ, "qb_dev_leader_step: readq_cap must be 0..16");
+  QB_REQUIRE(msg_total && stats, "qb_dev_leader_step: msg_total and stats are required");
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(lg->off && lg->cfg && lg->meta && lg->term && lg->committed && lg->first_index &&
+                 lg->last_index && lg->snap_index && lg->snap_term && lg->max_ents &&
+                 lg->run_start && lg->run_term && lg->match && lg->next &&
+                 lg->pending_snapshot && lg->pstate && lg->infl_pos && lg->infl_buf,
+             "qb_dev_leader_step: a required group/progress array is NULL");
+  QB_REQUIRE(lg->readq_cap == 0 || (lg->rq_ctx && lg->rq_index && lg->rq_meta),
+             "qb_dev_leader_step: read queue arrays are required when readq_cap > 0");
+  QB_REQUIRE(M == 0 || (in->group && in->flags && in->index && in->term),
+             "qb_dev_leader_step: inbox group/flags/index/term are required");
+  QB_REQUIRE(msg_cap == 0 || msgs, "qb_dev_leader_step: msgs is NULL");
+  const ld::Carve c = ld::carve(G, M);
+  QB_REQUIRE(workspace && workspace_bytes >= c.total,
+             "qb_dev_leader_step: workspace needs %zu bytes", c.total);
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  u32* cnt = reinterpret_cast<u32*>(ws + c.cnt);
+  u32* bsum = reinterpret_cast<u32*>(ws + c.bsum);
+  u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);
+  u32* perm = reinterpret_cast<u32*>(ws + c.perm);
+  u32* mcnt = reinterpret_cast<u32*>(ws + c.mcnt);
+  u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
+  u32* pool = reinterpret_cast<u32*>(ws + c.pool);
+  u64* shards = reinterpret_cast<u64*>(ws + c.shards);
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(u32) * (G + 1), st);
+  if (e == hipSuccess) e = hipMemsetAsync(pool, 0, sizeof(u32) * 2, st);
+  if (e == hipSuccess) e = hipMemsetAsync(shards, 0, sizeof(u64) * QB_LSTAT_COUNT * 64, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
+  const unsigned rgrid = M ? (grid_for(M) < 2048 ? grid_for(M) : 2048) : 1;
+  if (M) {
+    hipLaunchKernelGGL(ld::k_ld_count, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group, cnt,
+                       shards);
+    QB_CHECK_LAUNCH("k_ld_count");
+  }
+  scan::launch(cnt, G, bsum, st);
+  QB_CHECK_LAUNCH("scan(records)");
+  if (M) {
+    e = hipMemcpyAsync(cursor, cnt, sizeof(u32) * G, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(cursor)");
+    hipLaunchKernelGGL(ld::k_ld_scatter, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group,
+                       cursor, perm);
+    QB_CHECK_LAUNCH("k_ld_scatter");
+  }
+  ld::Args A{};
+  A.lg = *lg;
+  A.in = *in;
+  A.cnt = cnt;
+  A.perm = perm;
+  A.mcnt = mcnt;
+  A.fix = reinterpret_cast<ld::Msg*>(ws + c.fix);
+  A.chead = reinterpret_cast<u32*>(ws + c.chead);
+  A.cnext = reinterpret_cast<u32*>(ws + c.cnext);
+  A.chunks = reinterpret_cast<ld::Msg*>(ws + c.chunks);
+  A.pool = pool;
+  A.nchunks = c.nchunks;
+  A.shards = shards;
+  A.stepdown_at = stepdown_at;
+  A.gflags = gflags;
+  hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  QB_CHECK_LAUNCH("k_ld_step");
+  scan::launch(mcnt, G, mbsum, st);
+  QB_CHECK_LAUNCH("scan(messages)");
+  hipLaunchKernelGGL(ld::k_ld_emit, dim3(grid_for(G)), dim3(kBlock), 0, st, G, mcnt, A.fix,
+                     A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
+                     msg_cap, msg_off, ld::U(msg_total), shards);
+  QB_CHECK_LAUNCH("k_ld_emit");
+  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64), 0, st, shards, ld::U(stats));
+  QB_CHECK_LAUNCH("k_ld_fold");
+  return QB_OK;
+}

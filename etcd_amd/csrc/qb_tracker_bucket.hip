@@ -28,13 +28,14 @@
 //                    as LDS atomic or, then maybeCommit for the chunk's groups
 //                    and a coalesced write-back of match/next/active/committed.
 #include "qb_common.h"
+#include "qb_scan.h"
 
 namespace qb {
 namespace bk {
 
 constexpr int kTile = 4096;          // records per histogram/scatter/split tile
 constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
-constexpr int kScanPer = 4096;       // elements per scan block (1024 x 4)
+using scan::kScanPer;
 constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
 
 // Bucketed record payload, structure of arrays (three u64 columns of M), so
@@ -140,78 +141,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
   tally.flush(tl, shard_of(shards), slot);
 }
 
-// ---------------------------------------------------------------- K2 ----
-// In-place exclusive scan of n u32 values; data[n] receives the total.
-__device__ __forceinline__ u32 block_exclusive_scan_1024(u32 v, u32* sh, u32* total) {
-  // sh: 1024 + 32 u32 of LDS
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  u32 x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u32 y = u32(__shfl_up(int(x), o, 64));
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sh[1024 + w] = x;
-  __syncthreads();
-  if (w == 0) {
-    u32 s = lane < 16 ? sh[1024 + lane] : 0u;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const u32 y = u32(__shfl_up(int(s), o, 64));
-      if (lane >= o) s += y;
-    }
-    if (lane < 16) sh[1024 + lane] = s;  // inclusive wave sums
-  }
-  __syncthreads();
-  const u32 before = w ? sh[1024 + w - 1] : 0u;
-  *total = sh[1024 + 15];
-  return before + x - v;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_local(u32* __restrict__ data, u64 n,
-                                                     u32* __restrict__ bsum) {
-  __shared__ u32 sh[1024 + 32];
-  const u64 base = u64(blockIdx.x) * kScanPer + u64(threadIdx.x) * 4;
-  u32 v[4], s = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[k] = base + k < n ? data[base + k] : 0u;
-    s += v[k];
-  }
-  u32 total;
-  u32 ex = block_exclusive_scan_1024(s, sh, &total);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (base + k < n) data[base + k] = ex;
-    ex += v[k];
-  }
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_sums(u32* __restrict__ bsum, u32 nb,
-                                                    u32* __restrict__ data_total_slot) {
-  __shared__ u32 sh[1024 + 32];
-  u32 carry = 0;
-  for (u32 base = 0; base < nb; base += 1024) {
-    const u32 i = base + threadIdx.x;
-    const u32 v = i < nb ? bsum[i] : 0u;
-    u32 total;
-    const u32 ex = block_exclusive_scan_1024(v, sh, &total);
-    if (i < nb) bsum[i] = ex + carry;
-    carry += total;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *data_total_slot = carry;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_add(u32* __restrict__ data, u64 n,
-                                                   const u32* __restrict__ bsum) {
-  const u64 base = u64(blockIdx.x) * kScanPer + u64(threadIdx.x) * 4;
-  const u32 add = bsum[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (base + k < n) data[base + k] += add;
-}
+// K2 is scan::k_scan_* (qb_scan.h).
 
 // ------------------------------------------------ LDS tile partition ----
 // Counting sort of one tile (<= kTile records) by a small key, in LDS.  The
@@ -650,9 +580,9 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
     QB_CHECK_LAUNCH("k_bk_hist");
     const u64 nb = geo.nbins();
     const u32 nblk = u32((nb + bk::kScanPer - 1) / bk::kScanPer);
-    hipLaunchKernelGGL(bk::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
-    hipLaunchKernelGGL(bk::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
-    hipLaunchKernelGGL(bk::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+    hipLaunchKernelGGL(scan::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+    hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
+    hipLaunchKernelGGL(scan::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
     QB_CHECK_LAUNCH("k_scan");
     hipLaunchKernelGGL(bk::k_bk_scatter, dim3(geo.NT), dim3(bk::kPartThreads), 2 * lds_bins, st,
                        geo, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),

@@ -1,0 +1,210 @@
+"""The leader inbox step (include/quorum_batch.h ``qb_dev_leader_step``).
+
+Device-resident leader state of G raft groups — Progress per slot (CSR, as
+``CsrGroups``), the leader's log view, the pending ReadIndex queue — and a
+batch of responses applied with the reference's sequential semantics
+(raft.go:847-921 Step's term filter, raft.go:1099-1342 stepLeader).  Every
+computation runs in the HIP library; torch only holds device memory.
+
+Array names and meanings (all numpy dtypes little-endian):
+  off[G+1] u32, cfg[G] u32 (mask_in | mask_out << 16), meta[G] u32 (leader
+  slot | transferee << 8 | runs << 16 | readq length << 20 | pending-read bit
+  25), term/committed/first_index/last_index/snap_index/snap_term/max_ents[G]
+  u64, run_start/run_term[G*8] u64, match/next/pending_snapshot[S] u64,
+  pstate[S] u8 (state | ProbeSent 0x4 | RecentActive 0x8), infl_pos[S] u32
+  (start | count << 16), infl_buf[S*inflight_cap] u64, rq_ctx/rq_index
+  [G*readq_cap] u64, rq_meta[G*readq_cap] u32 (acks | from << 16).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+
+MAX_RUNS = 8
+MAX_READQ = 16
+
+IN_APP_RESP, IN_HEARTBEAT_RESP, IN_SNAP_STATUS, IN_UNREACHABLE = 0, 1, 2, 3
+PR_PROBE_SENT, PR_RECENT_ACTIVE = 0x04, 0x08
+META_PENDING_READINDEX = 1 << 25
+READ_ONLY_SAFE, READ_ONLY_LEASE_BASED = 0, 1
+LFLAG_ADVANCED, LFLAG_RELEASE_READS, LFLAG_STEPPED_DOWN = 0x1, 0x2, 0x4
+LSTAT_NAMES = ("applied", "stale_term", "higher_term", "non_member", "after_stepdown",
+               "bad_group", "msgs", "msgs_dropped")
+
+MSG_DTYPE = np.dtype([("index", "<u8"), ("log_term", "<u8"), ("commit", "<u8"), ("aux", "<u8"),
+                      ("group", "<u4"), ("to", "u1"), ("type", "u1"), ("reserved", "<u2")])
+assert MSG_DTYPE.itemsize == 40
+
+_P = C.c_void_p
+
+
+class LeaderGroupsC(C.Structure):
+    """struct qb_leader_groups (include/quorum_batch.h)."""
+    _fields_ = [("G", C.c_uint64), ("inflight_cap", C.c_uint32), ("readq_cap", C.c_uint32),
+                ("read_only", C.c_uint32), ("reserved", C.c_uint32)] + [
+        (n, _P) for n in ("off", "cfg", "meta", "term", "committed", "first_index", "last_index",
+                          "snap_index", "snap_term", "max_ents", "run_start", "run_term", "match",
+                          "next", "pending_snapshot", "pstate", "infl_pos", "infl_buf", "rq_ctx",
+                          "rq_index", "rq_meta")]
+
+
+class LeaderInboxC(C.Structure):
+    """struct qb_leader_inbox."""
+    _fields_ = [("M", C.c_uint64)] + [(n, _P) for n in ("group", "flags", "index", "term", "hint",
+                                                         "log_term")]
+
+
+GROUP_ARRAYS = {  # name -> numpy dtype (device storage uses the same bytes)
+    "off": np.uint32, "cfg": np.uint32, "meta": np.uint32, "term": np.uint64,
+    "committed": np.uint64, "first_index": np.uint64, "last_index": np.uint64,
+    "snap_index": np.uint64, "snap_term": np.uint64, "max_ents": np.uint64,
+    "run_start": np.uint64, "run_term": np.uint64, "match": np.uint64, "next": np.uint64,
+    "pending_snapshot": np.uint64, "pstate": np.uint8, "infl_pos": np.uint32,
+    "infl_buf": np.uint64, "rq_ctx": np.uint64, "rq_index": np.uint64, "rq_meta": np.uint32,
+}
+_TORCH = {np.uint8: torch.uint8, np.uint32: torch.int32, np.uint64: torch.int64,
+          np.uint16: torch.int16}
+_SIGNED = {np.uint8: np.uint8, np.uint32: np.int32, np.uint64: np.int64, np.uint16: np.int16}
+
+
+def _to_dev(a: np.ndarray, dt, device) -> torch.Tensor:
+    a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+    if a.size == 0:
+        a = np.zeros(1, dtype=dt)  # keep a valid device pointer
+    return torch.from_numpy(a.view(_SIGNED[dt]).copy()).to(device)
+
+
+def _to_np(t: torch.Tensor, dt, n: Optional[int] = None) -> np.ndarray:
+    a = t.detach().cpu().numpy().view(dt)
+    return a if n is None else a[:n]
+
+
+@dataclass
+class LeaderInbox:
+    """A batch of responses to leaders (SoA).  flags = slot | kind << 4 |
+    0x80 if Reject; index = Message.Index (MsgHeartbeatResp: Context)."""
+    group: torch.Tensor
+    flags: torch.Tensor
+    index: torch.Tensor
+    term: torch.Tensor
+    hint: torch.Tensor
+    log_term: torch.Tensor
+
+    _m: int = 0  # number of records (device arrays hold at least one element)
+
+    @property
+    def M(self) -> int:
+        return self._m
+
+    @classmethod
+    def from_numpy(cls, group, slot, kind, index, term, reject=None, hint=None, log_term=None,
+                   device="cuda"):
+        dev = torch.device(device)
+        M = len(group)
+        flags = (np.asarray(slot, np.uint8) & 0x0F) | ((np.asarray(kind, np.uint8) & 3) << 4)
+        if reject is not None:
+            flags = flags | (np.asarray(reject, bool).astype(np.uint8) << 7)
+        z = np.zeros(M, np.uint64)
+        ib = cls(_to_dev(np.asarray(group, np.uint32), np.uint32, dev),
+                 _to_dev(flags.astype(np.uint8), np.uint8, dev),
+                 _to_dev(index, np.uint64, dev), _to_dev(term, np.uint64, dev),
+                 _to_dev(z if hint is None else hint, np.uint64, dev),
+                 _to_dev(z if log_term is None else log_term, np.uint64, dev))
+        ib._m = M
+        return ib
+
+
+@dataclass
+class LeaderStepResult:
+    msgs: np.ndarray        # MSG_DTYPE, group order
+    msg_total: int
+    msg_off: np.ndarray     # [G+1] u32
+    stepdown_at: np.ndarray  # [G] u32 (0xFFFFFFFF = none)
+    gflags: np.ndarray      # [G] u8
+    stats: Dict[str, int]
+
+
+class LeaderGroups:
+    """Leader state of G groups resident on one device."""
+
+    def __init__(self, arrays: Dict[str, np.ndarray], inflight_cap: int, readq_cap: int = 0,
+                 read_only: int = READ_ONLY_SAFE, device="cuda"):
+        self.device = torch.device(device)
+        if not self.device.type == "cuda":
+            raise _lib.QuorumBatchError("LeaderGroups needs a HIP device; there is no CPU path")
+        self.G = len(arrays["cfg"])
+        self.S = int(arrays["off"][-1])
+        self.inflight_cap, self.readq_cap, self.read_only = inflight_cap, readq_cap, read_only
+        self.t = {k: _to_dev(arrays[k], dt, self.device) for k, dt in GROUP_ARRAYS.items()}
+        self._ws = None
+
+    def numpy(self) -> Dict[str, np.ndarray]:
+        n = {"off": self.G + 1, "cfg": self.G, "meta": self.G, "term": self.G,
+             "committed": self.G, "first_index": self.G, "last_index": self.G,
+             "snap_index": self.G, "snap_term": self.G, "max_ents": self.G,
+             "run_start": self.G * MAX_RUNS, "run_term": self.G * MAX_RUNS,
+             "match": self.S, "next": self.S, "pending_snapshot": self.S, "pstate": self.S,
+             "infl_pos": self.S, "infl_buf": self.S * self.inflight_cap,
+             "rq_ctx": self.G * self.readq_cap, "rq_index": self.G * self.readq_cap,
+             "rq_meta": self.G * self.readq_cap}
+        return {k: _to_np(self.t[k], dt, n[k]) for k, dt in GROUP_ARRAYS.items()}
+
+    def _struct(self) -> LeaderGroupsC:
+        s = LeaderGroupsC(G=self.G, inflight_cap=self.inflight_cap, readq_cap=self.readq_cap,
+                          read_only=self.read_only, reserved=0)
+        for k in GROUP_ARRAYS:
+            setattr(s, k, self.t[k].data_ptr())
+        return s
+
+    def step(self, inbox: LeaderInbox, msg_cap: Optional[int] = None,
+             stats: Optional[torch.Tensor] = None, fetch: bool = True):
+        """One batch through qb_dev_leader_step.  Returns a LeaderStepResult
+        (host copies) when fetch, else the device outputs."""
+        lib = _lib.load()
+        M = inbox.M
+        dev = self.device
+        need = lib.qb_leader_workspace_bytes(self.G, M)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=dev)
+        if msg_cap is None:
+            msg_cap = max(16, 8 * M + 4 * self.G)
+        out = self._outputs(msg_cap)
+        if stats is None:
+            stats = torch.zeros(8, dtype=torch.int64, device=dev)
+        ls = self._struct()
+        ib = LeaderInboxC(M=M, group=inbox.group.data_ptr(), flags=inbox.flags.data_ptr(),
+                          index=inbox.index.data_ptr(), term=inbox.term.data_ptr(),
+                          hint=inbox.hint.data_ptr(), log_term=inbox.log_term.data_ptr())
+        _lib.call("qb_dev_leader_step", C.byref(ls), C.byref(ib), out["msgs"].data_ptr(), msg_cap,
+                  out["total"].data_ptr(), out["off"].data_ptr(), out["stepdown"].data_ptr(),
+                  out["gflags"].data_ptr(), stats.data_ptr(), self._ws.data_ptr(),
+                  self._ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
+        if not fetch:
+            return out, stats
+        total = int(out["total"].cpu().item())
+        raw = out["msgs"].cpu().numpy().view(np.uint8)[: min(total, msg_cap) * 40]
+        st = stats.cpu().tolist()
+        return LeaderStepResult(
+            msgs=raw.view(MSG_DTYPE).copy(), msg_total=total,
+            msg_off=_to_np(out["off"], np.uint32, self.G + 1),
+            stepdown_at=_to_np(out["stepdown"], np.uint32, self.G),
+            gflags=_to_np(out["gflags"], np.uint8, self.G),
+            stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)})
+
+    def _outputs(self, msg_cap: int):
+        dev = self.device
+        key = (msg_cap,)
+        if getattr(self, "_out_key", None) != key:
+            self._out = {"msgs": torch.empty(msg_cap * 40, dtype=torch.uint8, device=dev),
+                         "total": torch.zeros(1, dtype=torch.int64, device=dev),
+                         "off": torch.zeros(self.G + 1, dtype=torch.int32, device=dev),
+                         "stepdown": torch.zeros(self.G, dtype=torch.int32, device=dev),
+                         "gflags": torch.zeros(self.G, dtype=torch.uint8, device=dev)}
+            self._out_key = key
+        return self._out

@@ -283,6 +283,148 @@ int qb_dev_csr_tally_votes(uint64_t G, const uint32_t* cfg,
                            void* stream);
 
 /* ----------------------------------------------------------------------- */
+/* Leader inbox step                              */
+/* ----------------------------------------------------------------------- */
+
+/* The full leader side of the responses in a raft leader's inbox, for G
+ * groups at once, with the reference's sequential per-message semantics:
+ *   raft.Step term filter (raft.go:847-921), stepLeader (raft.go:1099-1342):
+ *   MsgAppResp reject -> findConflictByTerm (log.go:150-171) + MaybeDecrTo
+ *     (progress.go:163-191) + BecomeProbe + sendAppend;
+ *   MsgAppResp accept -> MaybeUpdate, Probe->Replicate, Snapshot recovery,
+ *     Inflights.FreeLE, maybeCommit (raft.go:585-588) + bcastAppend
+ *     (raft.go:515-522) or the paused-peer sendAppend, the maybeSendAppend
+ *     loop (raft.go:432-492), MsgTimeoutNow to the lead transferee;
+ *   MsgHeartbeatResp -> RecentActive, ProbeSent, FreeFirstOne, sendAppend,
+ *     ReadIndex acks: readOnly.recvAck + VoteResult + advance
+ *     (read_only.go:68-121) + responseToReadIndexReq (raft.go:1737-1752);
+ *   MsgSnapStatus, MsgUnreachable (raft.go:1310-1338).
+ * Records of a group are applied in batch order; groups are independent.
+ * The leader's log is a static view (the step never appends): firstIndex,
+ * lastIndex, the terms of [firstIndex-1, lastIndex] as up to
+ * QB_LEADER_MAX_RUNS runs, the storage snapshot, and max_ents = the number
+ * of entries raftLog.entries(lo, MaxSizePerMsg) returns (entries of one size).
+ * Outbound messages are written in group order, each group's in the order
+ * the reference emits them. */
+
+#define QB_LEADER_MAX_RUNS 8
+#define QB_LEADER_MAX_READQ 16
+
+/* Inbound kinds (rec flags bits 4-5). */
+#define QB_IN_APP_RESP 0       /* pb.MsgAppResp                         */
+#define QB_IN_HEARTBEAT_RESP 1 /* pb.MsgHeartbeatResp (index = Context) */
+#define QB_IN_SNAP_STATUS 2    /* pb.MsgSnapStatus (local, Term 0)      */
+#define QB_IN_UNREACHABLE 3    /* pb.MsgUnreachable (local, Term 0)     */
+
+/* Progress state byte: StateType (tracker/state.go:26-33) | flags. */
+#define QB_PR_PROBE 0
+#define QB_PR_REPLICATE 1
+#define QB_PR_SNAPSHOT 2
+#define QB_PR_PROBE_SENT 0x04u
+#define QB_PR_RECENT_ACTIVE 0x08u
+
+/* Group meta word: leader slot (bits 0-7), lead transferee slot (8-15,
+ * 0xFF = None), term runs (16-19, 1..8), pending ReadIndex requests (20-24),
+ * bit 25: MsgReadIndex postponed until the first commit of the term
+ * (raft.pendingReadIndexMessages). */
+#define QB_META_PENDING_READINDEX (1u << 25)
+
+#define QB_READ_ONLY_SAFE 0
+#define QB_READ_ONLY_LEASE_BASED 1
+
+/* Outbound message types (raftpb MessageType, raft.pb.go:76-94) and a local
+ * ReadState (raft.readStates). */
+#define QB_MSG_APP 3
+#define QB_MSG_SNAP 7
+#define QB_MSG_TIMEOUT_NOW 14
+#define QB_MSG_READ_INDEX_RESP 16
+#define QB_READ_STATE 255
+
+/* Per-group output flags. */
+#define QB_LFLAG_ADVANCED 0x01u     /* maybeCommit returned true          */
+#define QB_LFLAG_RELEASE_READS 0x02u /* postponed MsgReadIndex to release  */
+#define QB_LFLAG_STEPPED_DOWN 0x04u  /* a higher-term response: becomeFollower */
+
+enum {
+  QB_LSTAT_APPLIED = 0,        /* reached stepLeader's handler             */
+  QB_LSTAT_STALE_TERM = 1,     /* m.Term < group term: ignored            */
+  QB_LSTAT_HIGHER_TERM = 2,    /* step-down record                         */
+  QB_LSTAT_NON_MEMBER = 3,     /* no Progress for the slot                 */
+  QB_LSTAT_AFTER_STEPDOWN = 4, /* behind the group's step-down             */
+  QB_LSTAT_BAD_GROUP = 5,      /* group index >= G                          */
+  QB_LSTAT_MSGS = 6,           /* outbound messages generated              */
+  QB_LSTAT_MSGS_DROPPED = 7,   /* messages not written (msg_cap / pool)    */
+  QB_LSTAT_COUNT = 8
+};
+
+typedef struct qb_leader_groups {
+  uint64_t G;
+  uint32_t inflight_cap; /* MaxInflightMsgs: ring size per slot, 1..4096  */
+  uint32_t readq_cap;    /* pending ReadIndex slots per group, 0..16      */
+  uint32_t read_only;    /* QB_READ_ONLY_SAFE / QB_READ_ONLY_LEASE_BASED  */
+  uint32_t reserved;
+  /* configuration, CSR as qb_dev_csr_committed_vote */
+  const uint32_t* off;   /* [G+1] */
+  const uint32_t* cfg;   /* [G] mask_in | mask_out << 16 */
+  /* per group */
+  uint32_t* meta;        /* [G] see QB_META_* (in/out)                     */
+  const uint64_t* term;  /* [G] raft.Term                                  */
+  uint64_t* committed;   /* [G] raftLog.committed (in/out)                 */
+  const uint64_t* first_index; /* [G] raftLog.firstIndex()                 */
+  const uint64_t* last_index;  /* [G] raftLog.lastIndex()                  */
+  const uint64_t* snap_index;  /* [G] storage snapshot index, 0 = unavailable */
+  const uint64_t* snap_term;   /* [G]                                      */
+  const uint64_t* max_ents;    /* [G] entries per MsgApp (>= 1)            */
+  const uint64_t* run_start;   /* [G * QB_LEADER_MAX_RUNS] ascending        */
+  const uint64_t* run_term;    /* [G * QB_LEADER_MAX_RUNS]                  */
+  /* per slot, S = off[G] (in/out) */
+  uint64_t* match;
+  uint64_t* next;
+  uint64_t* pending_snapshot;
+  uint8_t* pstate;       /* QB_PR_* */
+  uint32_t* infl_pos;    /* start | count << 16 */
+  uint64_t* infl_buf;    /* [S * inflight_cap] ring */
+  /* pending ReadIndex queue, oldest first: [G * readq_cap] (in/out) */
+  uint64_t* rq_ctx;
+  uint64_t* rq_index;
+  uint32_t* rq_meta;     /* ack slot bits (0-15) | request From slot << 16 (0xFF = local) */
+} qb_leader_groups;
+
+typedef struct qb_leader_inbox {
+  uint64_t M;
+  const uint32_t* group;
+  const uint8_t* flags;  /* slot (0-3) | kind << 4 | QB_REC_REJECT          */
+  const uint64_t* index; /* Message.Index; MsgHeartbeatResp: Context (0 = empty) */
+  const uint64_t* term;  /* Message.Term (0 = local message)                */
+  const uint64_t* hint;  /* Message.RejectHint (nullable: no rejections)    */
+  const uint64_t* log_term; /* Message.LogTerm (nullable)                   */
+} qb_leader_inbox;
+
+typedef struct qb_msg_out {
+  uint64_t index;    /* MsgApp: Index (= Next-1); MsgSnap: snapshot index; reads: read index */
+  uint64_t log_term; /* MsgApp: LogTerm; MsgSnap: snapshot term */
+  uint64_t commit;   /* MsgApp: Commit */
+  uint64_t aux;      /* MsgApp: number of entries (Index+1 ..); reads: request ctx */
+  uint32_t group;
+  uint8_t to;        /* destination slot (0xFF for a local ReadState) */
+  uint8_t type;      /* QB_MSG_* */
+  uint16_t reserved;
+} qb_msg_out;
+
+size_t qb_leader_workspace_bytes(uint64_t G, uint64_t M);
+/* msgs: device buffer of msg_cap records; msg_total (device uint64) receives
+ * the number generated (only the first msg_cap, in group order, are written);
+ * msg_off (device [G+1], nullable) the first message of each group.
+ * stepdown_at (device [G], nullable): batch index of the group's step-down
+ * record or UINT32_MAX; gflags (device [G], nullable): QB_LFLAG_*.
+ * stats: QB_LSTAT_COUNT device uint64 (accumulated). */
+int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
+                       qb_msg_out* msgs, uint64_t msg_cap, uint64_t* msg_total,
+                       uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags,
+                       uint64_t* stats, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */
 /* ----------------------------------------------------------------------- */
 

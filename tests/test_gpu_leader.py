@@ -1,0 +1,132 @@
+"""GPU parity of the leader inbox step (qb_dev_leader_step) against the
+sequential CPU oracle (oracle/leader_ref.py): the reference's own scenarios
+(tests/golden/leader_tables.json) replayed on the device, and seeded random
+batches compared field by field (state, messages, flags, counters)."""
+import copy
+
+import numpy as np
+import pytest
+
+from oracle import leader_ref as L
+from tests import leader_pack as LP
+from tests import leader_scenarios as LS
+
+pytestmark = pytest.mark.gpu
+
+TABLES = LS.load_tables()
+
+
+def _engine(groups, inflight_cap, readq_cap, read_only=0):
+    from etcd_amd.quorum.leader import LeaderGroups
+    return LeaderGroups(LP.pack(groups, inflight_cap, readq_cap), inflight_cap, readq_cap,
+                        read_only, device="cuda")
+
+
+def _inbox(recs):
+    from etcd_amd.quorum.leader import LeaderInbox
+    a = LP.records_arrays(recs)
+    if a is None:
+        return LeaderInbox.from_numpy([], [], [], [], [], device="cuda")
+    return LeaderInbox.from_numpy(a["group"], a["slot"], a["kind"], a["index"], a["term"],
+                                  a["reject"], a["hint"], a["log_term"], device="cuda")
+
+
+def _dev_msgs(res):
+    return [(int(m["group"]), int(m["type"]), int(m["to"]), int(m["index"]), int(m["log_term"]),
+             int(m["commit"]), int(m["aux"])) for m in res.msgs]
+
+
+def _orc_msgs(groups):
+    out = []
+    for gi, g in enumerate(groups):
+        out += [(gi,) + m.key() for m in g.msgs]
+    return out
+
+
+@pytest.mark.parametrize("sc", TABLES["scenarios"], ids=[s["name"] for s in TABLES["scenarios"]])
+def test_reference_scenarios_on_device(sc):
+    g = LS.build_group(sc)
+    cap = sc["infl_size"]
+    for k, op in enumerate(sc["ops"]):
+        where = f"{sc['name']} op{k}"
+        if op["op"] == "propose":  # host-side op between device batches
+            g.msgs = []
+            g.propose(op["n"])
+            LS.check_expect(where, op["expect"], [LS.msg_dict(m) for m in g.msgs], g)
+            continue
+        twin = copy.deepcopy(g)  # the oracle's run of the same record
+        twin.msgs = []
+        twin.step(LS.inbound(op), 0)
+        eng = _engine([g], cap, max(1, len(g.readq)))
+        res = eng.step(_inbox([(0, LS.inbound(op))]))
+        LP.unpack_into([g], eng.numpy(), cap, max(1, len(g.readq)))
+        msgs = [dict(zip(LS.MSG_FIELDS, m[1:])) for m in _dev_msgs(res)]
+        LS.check_expect(where, op["expect"], msgs, g)
+        assert [tuple(m.values()) for m in msgs] == [m.key() for m in twin.msgs], where
+        assert LP.state_key(g) == LP.state_key(twin), where
+
+
+def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9):
+    rng = np.random.default_rng(seed)
+    groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots)
+    for g in groups:
+        g.read_only = read_only
+    recs = LP.random_records(rng, groups, M)
+    eng = _engine(groups, inflight_cap, readq_cap, read_only)
+    res = eng.step(_inbox(recs))
+    orc = copy.deepcopy(groups)
+    for g in orc:
+        g.msgs = []
+    stats = L.run_batch(orc, recs)
+    dev = copy.deepcopy(groups)
+    LP.unpack_into(dev, eng.numpy(), inflight_cap, readq_cap)
+    for gi in range(G):
+        assert LP.state_key(dev[gi]) == LP.state_key(orc[gi]), f"seed {seed} group {gi}"
+    om = _orc_msgs(orc)
+    assert res.msg_total == len(om)
+    assert _dev_msgs(res) == om
+    want_sd = np.array([0xFFFFFFFF if g.stepped_down_at is None else g.stepped_down_at for g in orc],
+                       np.uint32)
+    assert np.array_equal(res.stepdown_at, want_sd)
+    want_fl = np.array([(1 if g.advanced else 0) | (2 if g.released_pending else 0)
+                        | (4 if g.stepped_down_at is not None else 0) for g in orc], np.uint8)
+    assert np.array_equal(res.gflags, want_fl)
+    assert res.stats["applied"] == stats["applied"]
+    assert res.stats["stale_term"] == stats["stale"]
+    assert res.stats["higher_term"] == stats["higher"]
+    assert res.stats["non_member"] == stats["nonmember"]
+    assert res.stats["after_stepdown"] == stats["after"]
+    assert res.stats["bad_group"] == stats["bad"]
+    assert res.stats["msgs"] == len(om) and res.stats["msgs_dropped"] == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_fuzz_small(seed):
+    _fuzz(seed, G=400, M=1500, inflight_cap=3, readq_cap=4)
+
+
+def test_fuzz_lease_based_and_wide():
+    _fuzz(11, G=300, M=1200, inflight_cap=5, readq_cap=2, read_only=1, max_slots=16)
+
+
+def test_fuzz_larger():
+    _fuzz(21, G=5000, M=12000, inflight_cap=8, readq_cap=4)
+
+
+def test_empty_batch_and_truncated_output():
+    rng = np.random.default_rng(5)
+    groups = LP.random_groups(rng, 50, 4, 2)
+    eng = _engine(groups, 4, 2)
+    res = eng.step(_inbox([]))
+    assert res.msg_total == 0 and res.stats["applied"] == 0
+    recs = LP.random_records(rng, groups, 400, bad_frac=0)
+    orc = copy.deepcopy(groups)
+    for g in orc:
+        g.msgs = []
+    L.run_batch(orc, recs)
+    om = _orc_msgs(orc)
+    cap = len(om) // 2
+    res = eng.step(_inbox(recs), msg_cap=cap)
+    assert res.msg_total == len(om)
+    assert _dev_msgs(res) == om[:cap]
+    assert res.stats["msgs_dropped"] == len(om) - cap
