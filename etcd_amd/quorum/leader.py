@@ -208,3 +208,62 @@ class LeaderGroups:
                          "gflags": torch.zeros(self.G, dtype=torch.uint8, device=dev)}
             self._out_key = key
         return self._out
+
+
+# ------------------------------------------------------- workload synth ---
+
+def synth_streaming(G: int, W: int = 32, D: int = 4, n: int = 5, device="cuda"):
+    """Steady-state leaders (bench/test workload of the leader step: 5 voters, leader slot
+    0, every follower Replicate with a full window of W in-flight MsgApps of D
+    entries each (MaxInflightMsgs = W), commit at the window base."""
+    dev = torch.device(device)
+    g = torch.arange(G, dtype=torch.int64, device=dev)
+    base = 1000 + (g * 37) % 1000
+    last = base + W * D
+    S = n * G
+    lg = LeaderGroups.__new__(LeaderGroups)
+    lg.device, lg.G, lg.S = dev, G, S
+    lg.inflight_cap, lg.readq_cap, lg.read_only, lg._ws = W, 0, 0, None
+    i32 = lambda x: x.to(torch.int32)
+    runs = torch.zeros(G * MAX_RUNS, dtype=torch.int64, device=dev)
+    runs_t = torch.zeros_like(runs)
+    runs[::MAX_RUNS] = base - 51
+    runs_t[::MAX_RUNS] = 7
+    slot = torch.arange(S, dtype=torch.int64, device=dev) % n
+    gs = torch.arange(S, dtype=torch.int64, device=dev) // n
+    bs, ls = base[gs], last[gs]
+    lead = slot == 0
+    j = torch.arange(W, dtype=torch.int64, device=dev)
+    infl = (bs[:, None] + (j[None, :] + 1) * D).reshape(-1)
+    lg.t = {
+        "off": i32(torch.arange(0, S + 1, n, device=dev)),
+        "cfg": torch.full((G,), (1 << n) - 1, dtype=torch.int32, device=dev),
+        "meta": torch.full((G,), 0xFF00 | (1 << 16), dtype=torch.int32, device=dev),
+        "term": torch.full((G,), 7, dtype=torch.int64, device=dev),
+        "committed": base.clone(), "first_index": base - 50, "last_index": last,
+        "snap_index": base - 51, "snap_term": torch.full((G,), 7, dtype=torch.int64, device=dev),
+        "max_ents": torch.full((G,), D, dtype=torch.int64, device=dev),
+        "run_start": runs, "run_term": runs_t,
+        "match": torch.where(lead, ls, bs), "next": ls + 1,
+        "pending_snapshot": torch.zeros(S, dtype=torch.int64, device=dev),
+        "pstate": torch.full((S,), 1 | 8, dtype=torch.uint8, device=dev),
+        "infl_pos": i32(torch.where(lead, torch.zeros_like(slot), torch.full_like(slot, W << 16))),
+        "infl_buf": infl,
+        "rq_ctx": torch.zeros(1, dtype=torch.int64, device=dev),
+        "rq_index": torch.zeros(1, dtype=torch.int64, device=dev),
+        "rq_meta": torch.zeros(1, dtype=torch.int32, device=dev),
+    }
+    return lg, base
+
+
+def streaming_inbox(G: int, base: torch.Tensor, k: int, D: int = 4, n: int = 5, device="cuda"):
+    """Step k: one MsgAppResp per group, from follower 1 + (g + k) % 4, acking
+    the next window boundary; records shuffled (arrival order)."""
+    dev = torch.device(device)
+    g = torch.randperm(G, device=dev)
+    f = 1 + (g + k) % (n - 1)
+    idx = base[g] + (k // (n - 1) + 1) * D
+    z = torch.zeros(G, dtype=torch.int64, device=dev)
+    ib = LeaderInbox(g.to(torch.int32), f.to(torch.uint8), idx, torch.full_like(idx, 7), z, z)
+    ib._m = G
+    return ib

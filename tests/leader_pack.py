@@ -175,7 +175,7 @@ def random_records(rng: np.random.Generator, groups, M: int, bad_frac: float = 0
             recs.append((G + int(rng.integers(0, 5)), L.Inbound(0, 0, 1, 1)))
             continue
         g = groups[gi]
-        slot = int(rng.integers(0, g.n_slots + (1 if rng.random() < 0.05 else 0)))
+        slot = min(15, int(rng.integers(0, g.n_slots + (1 if rng.random() < 0.05 else 0))))  # 4-bit slot field
         kind = int(rng.choice([0, 0, 0, 0, 1, 1, 2, 3]))
         r = rng.random()
         term = g.term if r < 0.85 else (g.term - 1 if r < 0.92 else (0 if r < 0.96 else g.term + 1))

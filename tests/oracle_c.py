@@ -33,6 +33,7 @@ SIG = {
     "orc_fixed_appresp_sequential": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                             _p, _p, _p, _p, _p]),
     "orc_fixed_commit_all": (None, [_u32, _u64, _p, _p, _p, _p]),
+    "orc_leader_step": (_u64, [_p, _p, _p, _u64, _p, _p, _p, _i32]),
 }
 
 _lib = None
@@ -41,8 +42,9 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        src = os.path.join(ORC_DIR, "quorum_oracle.c")
-        if not os.path.exists(ORC_PATH) or os.path.getmtime(ORC_PATH) < os.path.getmtime(src):
+        srcs = [os.path.join(ORC_DIR, f) for f in ("quorum_oracle.c", "leader_oracle.c")]
+        if not os.path.exists(ORC_PATH) or any(os.path.getmtime(ORC_PATH) < os.path.getmtime(s)
+                                                for s in srcs):
             subprocess.check_call(["make", "-s", "-C", ORC_DIR])
         lib = C.CDLL(ORC_PATH)
         for k, (r, a) in SIG.items():
@@ -168,3 +170,57 @@ def commit_all(n, match, term_start, committed):
     adv = np.empty(G, np.uint8)
     lib.orc_fixed_commit_all(n, G, ptr(match), ptr(term_start), ptr(committed), ptr(adv))
     return adv
+
+
+# ----------------------------------------------------------- leader step ---
+
+LEADER_FIELDS = ("off", "cfg", "meta", "term", "committed", "first_index", "last_index",
+                 "snap_index", "snap_term", "max_ents", "run_start", "run_term", "match", "next",
+                 "pending_snapshot", "pstate", "infl_pos", "infl_buf", "rq_ctx", "rq_index",
+                 "rq_meta")
+
+
+class _LG(C.Structure):
+    _fields_ = [("G", C.c_uint64), ("K", C.c_uint32), ("Q", C.c_uint32),
+                ("read_only", C.c_uint32), ("reserved", C.c_uint32)] + [(f, _p) for f in LEADER_FIELDS]
+
+
+class _IN(C.Structure):
+    _fields_ = [("M", C.c_uint64)] + [(f, _p) for f in ("group", "flags", "index", "term", "hint",
+                                                         "log_term")]
+
+
+LEADER_MSG_DTYPE = np.dtype([("index", "<u8"), ("log_term", "<u8"), ("commit", "<u8"),
+                             ("aux", "<u8"), ("group", "<u4"), ("to", "u1"), ("type", "u1"),
+                             ("reserved", "<u2")])
+
+
+def leader_step(arrays, inflight_cap, readq_cap, read_only, rec, threads=1, msg_cap=None):
+    """Sequential leader inbox step over SoA ``arrays`` (numpy, updated in
+    place); ``rec`` = dict(group, flags, index, term, hint, log_term).
+    Returns (msgs, total, stepdown_at, gflags, stats)."""
+    lib = load()
+    G = len(arrays["cfg"])
+    keep = {k: np.ascontiguousarray(v) if v.size else np.zeros(1, v.dtype)
+            for k, v in arrays.items()}
+    for k in arrays:
+        if arrays[k].size:
+            assert keep[k] is arrays[k] or np.shares_memory(keep[k], arrays[k]), k
+    lg = _LG(G=G, K=inflight_cap, Q=readq_cap, read_only=read_only, reserved=0)
+    for f in LEADER_FIELDS:
+        setattr(lg, f, keep[f].ctypes.data)
+    M = len(rec["group"])
+    z = np.zeros(1, np.uint64)
+    ib = _IN(M=M)
+    for f in ("group", "flags", "index", "term", "hint", "log_term"):
+        a = rec.get(f)
+        setattr(ib, f, (a if a is not None and a.size else z).ctypes.data)
+    if msg_cap is None:
+        msg_cap = 8 * M + 16
+    msgs = np.zeros(msg_cap, LEADER_MSG_DTYPE)
+    sd = np.empty(G, np.uint32)
+    gf = np.empty(G, np.uint8)
+    stats = np.zeros(8, np.uint64)
+    total = lib.orc_leader_step(C.byref(lg), C.byref(ib), msgs.ctypes.data, msg_cap,
+                                sd.ctypes.data, gf.ctypes.data, stats.ctypes.data, threads)
+    return msgs[:min(total, msg_cap)], int(total), sd, gf, stats

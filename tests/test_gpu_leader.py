@@ -130,3 +130,32 @@ def test_empty_batch_and_truncated_output():
     assert res.msg_total == len(om)
     assert _dev_msgs(res) == om[:cap]
     assert res.stats["msgs_dropped"] == len(om) - cap
+
+
+def test_streaming_workload_vs_c_oracle():
+    """The bench's streaming workload at 1M groups, six consecutive batches,
+    every state array and every message against the C oracle."""
+    import torch
+    from etcd_amd.quorum.leader import streaming_inbox, synth_streaming
+    from tests import oracle_c as oc
+    G = 1 << 20
+    lg, base = synth_streaming(G, device="cuda")
+    host = {k: v.copy() for k, v in lg.numpy().items()}
+    for k in range(6):
+        ib = streaming_inbox(G, base, k, device="cuda")
+        res = lg.step(ib, msg_cap=6 * G)
+        rec = {"group": ib.group.cpu().numpy().view(np.uint32),
+               "flags": ib.flags.cpu().numpy(), "index": ib.index.cpu().numpy().view(np.uint64),
+               "term": ib.term.cpu().numpy().view(np.uint64),
+               "hint": ib.hint.cpu().numpy().view(np.uint64),
+               "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
+        msgs, total, sd, gf, stats = oc.leader_step(host, 32, 0, 0, rec, threads=16,
+                                                    msg_cap=6 * G)
+        dev = lg.numpy()
+        for name in host:
+            assert np.array_equal(dev[name], host[name]), f"step {k}: {name}"
+        assert res.msg_total == total
+        assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8)), f"step {k}: msgs"
+        assert np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)
+        assert res.stats["applied"] == int(stats[0]) == G
+    torch.cuda.synchronize()

@@ -113,3 +113,48 @@ def test_find_conflict_by_term_matches_linear_walk():
                             break
                         i = (max(rs, first - 1) - 1) & L.M64
                 assert got == i
+
+
+def _records_soa(recs):
+    import numpy as np
+    from tests import leader_pack as LP
+    a = LP.records_arrays(recs)
+    flags = (a["slot"] & 0x0F) | ((a["kind"] & 3) << 4) | (a["reject"].astype(np.uint8) << 7)
+    return {"group": a["group"], "flags": flags.astype(np.uint8), "index": a["index"],
+            "term": a["term"], "hint": a["hint"], "log_term": a["log_term"]}
+
+
+@pytest.mark.parametrize("seed,read_only,threads", [(1, 0, 1), (2, 1, 1), (3, 0, 4)])
+def test_c_oracle_matches_python_oracle(seed, read_only, threads):
+    """The full-size checker (oracle/leader_oracle.c) against the pinned
+    Python restatement on random leader states and batches."""
+    import copy
+    import numpy as np
+    from tests import leader_pack as LP
+    from tests import oracle_c as oc
+    rng = np.random.default_rng(seed)
+    gs = LP.random_groups(rng, 600, 3, 4, max_slots=16 if read_only else 9)
+    for g in gs:
+        g.read_only = read_only
+    recs = LP.random_records(rng, gs, 2000)
+    arrays = LP.pack(gs, 3, 4)
+    msgs, total, sd, gf, stats = oc.leader_step(arrays, 3, 4, read_only, _records_soa(recs),
+                                                threads=threads)
+    orc = copy.deepcopy(gs)
+    for g in orc:
+        g.msgs = []
+    st = L.run_batch(orc, recs)
+    dev = copy.deepcopy(gs)
+    LP.unpack_into(dev, arrays, 3, 4)
+    assert [LP.state_key(g) for g in dev] == [LP.state_key(g) for g in orc]
+    want = [(gi,) + m.key() for gi, g in enumerate(orc) for m in g.msgs]
+    got = [(int(m["group"]), int(m["type"]), int(m["to"]), int(m["index"]), int(m["log_term"]),
+            int(m["commit"]), int(m["aux"])) for m in msgs]
+    assert total == len(want) and got == want
+    assert [int(x) for x in stats[:6]] == [st["applied"], st["stale"], st["higher"],
+                                           st["nonmember"], st["after"], st["bad"]]
+    want_sd = [0xFFFFFFFF if g.stepped_down_at is None else g.stepped_down_at for g in orc]
+    assert sd.tolist() == want_sd
+    want_fl = [(1 if g.advanced else 0) | (2 if g.released_pending else 0)
+               | (4 if g.stepped_down_at is not None else 0) for g in orc]
+    assert gf.tolist() == want_fl

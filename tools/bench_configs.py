@@ -152,6 +152,73 @@ def tracker_config(G, reps, seed=55):
                              "sample": f"{Gs} records on {Gs} groups, sequential C restatement"}})
 
 
+def leader_config(G, reps, warm=4):
+    """§8f rows 1-2: the leader inbox step (qb_dev_leader_step) on streaming
+    MsgAppResp batches (one per group per step), group-steps/s."""
+    from etcd_amd.quorum.leader import synth_streaming, streaming_inbox
+    lg, base = synth_streaming(G, device=dev)
+    steps = warm + reps
+    inboxes = [streaming_inbox(G, base, k, device=dev) for k in range(steps)]
+    stats = torch.zeros(8, dtype=torch.int64, device=dev)
+    outs = []
+    for k in range(warm):
+        lg.step(inboxes[k], msg_cap=6 * G, stats=stats, fetch=False)
+    torch.cuda.synchronize()
+    stats.zero_()
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    ev = HipEvents(2)
+    ev.record(ev.ev[0], sp)
+    for k in range(warm, steps):
+        lg.step(inboxes[k], msg_cap=6 * G, stats=stats, fetch=False)
+    ev.record(ev.ev[1], sp)
+    torch.cuda.synchronize()
+    t = ev.elapsed_ms(0, 1) / 1e3 / reps
+    ev.close()
+    st = stats.cpu().tolist()
+    msgs = st[6] / reps
+    # per group-step: record 21 B; group state read 84 B (off 4, cfg 4, meta 4,
+    # term/committed/first/last/snap/snap_term/max_ents 56, run 16) + commit
+    # and meta written 12 B; 5 slots x (match, next, psnap 24 + pstate 1 +
+    # infl_pos 4) read 145 B; the acking follower's freed window entry 8 B and
+    # match/next/pstate/infl_pos written 21 B; messages 40 B x 3 (stored,
+    # copied, written) per message; scans 16 B per group.
+    algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
+    # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
+    # stepLeader loop one record at a time) on a bounded sample of the same
+    # workload, 16 threads (groups partitioned) and 1 thread.
+    import time
+    from tests import oracle_c as oc
+    Gs = 1 << 20
+    lgc, basec = synth_streaming(Gs, device="cpu")
+    cpu = {}
+    for threads in (16, 1):
+        host = {k: v.copy() for k, v in lgc.numpy().items()}
+        t0 = time.perf_counter()
+        n_steps = 0
+        while True:
+            ib = streaming_inbox(Gs, basec, n_steps, device="cpu")
+            rec = {"group": ib.group.numpy().view(np.uint32), "flags": ib.flags.numpy(),
+                   "index": ib.index.numpy().view(np.uint64),
+                   "term": ib.term.numpy().view(np.uint64),
+                   "hint": ib.hint.numpy().view(np.uint64),
+                   "log_term": ib.log_term.numpy().view(np.uint64)}
+            t1 = time.perf_counter()
+            oc.leader_step(host, 32, 0, 0, rec, threads=threads, msg_cap=6 * Gs)
+            n_steps += 1
+            cpu.setdefault(threads, 0.0)
+            cpu[threads] += time.perf_counter() - t1
+            if time.perf_counter() - t0 > 6 or n_steps >= 24:
+                break
+        cpu[threads] = n_steps * Gs / cpu[threads]
+    report("leader inbox step (streaming MsgAppResp)", G, t, algo,
+           {"unit": "group-steps/s", "msgs_per_step": msgs,
+            "applied_per_step": st[0] / reps, "inflight_cap": 32, "voters": 5,
+            "cpu_baseline": {"value": cpu[16], "unit": "group-steps/s", "cores": 16,
+                             "kind": "port", "value_1thread": cpu[1],
+                             "sample": f"{Gs} groups x consecutive steps of the same workload, "
+                                       "C restatement of stepLeader (oracle/leader_oracle.c)"}})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
@@ -164,6 +231,8 @@ def main():
         csr_config("joint", 1 << 23, a.reps)
     if "5" in which:
         tracker_config(1 << 24, a.reps)
+    if "leader" in which:
+        leader_config(1 << 22, a.reps)
 
 
 if __name__ == "__main__":
