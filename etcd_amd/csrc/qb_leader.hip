@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
           continue;
         }
         const u32 slot = f & 0x0Fu;
-        if (slot >= G_.ns) {  // raft.go:1099-1104: no progress
+        if (slot >= G_.ns || (f & QB_REC_NO_PROGRESS)) {  // raft.go:1099-1104: no progress
           ++nnon;
           continue;
         }

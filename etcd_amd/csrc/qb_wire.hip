@@ -1,0 +1,348 @@
+// qb_wire.hip — wire ingest: raw raftpb.Message bytes -> leader-inbox records
+// (SURVEY.md §8f row 3), gfx950.
+//
+// Each message is validated exactly as the generated gogoproto decoder does
+// (paths relative to the reference's raft/raftpb/):
+//   Message.Unmarshal          raft.pb.go:1739-2061
+//   Entry / Snapshot / SnapshotMetadata / ConfState.Unmarshal
+//                              raft.pb.go:1360-1738, 2169-2542 (nested
+//                              messages are decoded too: a malformed nested
+//                              body fails the message, as in Go)
+//   skipRaft                   raft.pb.go:2909-2988 (unknown fields, groups)
+// and the four response types the leader step consumes (MsgAppResp,
+// MsgHeartbeatResp, MsgSnapStatus, MsgUnreachable) become SoA records; From
+// is mapped to the group's slot (the sorted voter/learner IDs of the CSR
+// config), a non-member keeps QB_REC_NO_PROGRESS (stepLeader drops it,
+// raft.go:1099-1104).
+//
+// Layout: one thread per message; a workgroup stages its 256 messages'
+// bytes (one contiguous span of the batch buffer) into LDS with 16-byte
+// loads when the span fits, so parsing reads LDS instead of issuing one
+// global byte load per varint byte; spans that do not fit parse from global.
+#include "qb_common.h"
+
+namespace qb {
+namespace wire {
+
+constexpr u32 kStage = 32 * 1024;  // LDS staging bytes per workgroup
+
+enum Kind : u32 { K_MESSAGE = 0, K_ENTRY = 1, K_SNAPSHOT = 2, K_SNAPMETA = 3, K_CONFSTATE = 4 };
+enum FieldType : u32 { T_UNKNOWN = 0, T_VARINT, T_BYTES, T_REPEATED, T_NESTED };
+
+// SCHEMAS of oracle/raftpb_ref.py (raft.proto field numbers and types).
+__device__ __forceinline__ u32 field_type(u32 kind, int fnum, u32* nested) {
+  switch (kind) {
+    case K_MESSAGE:
+      if (fnum == 7) { *nested = K_ENTRY; return T_NESTED; }
+      if (fnum == 9) { *nested = K_SNAPSHOT; return T_NESTED; }
+      if (fnum == 12) return T_BYTES;
+      return (fnum >= 1 && fnum <= 11) ? T_VARINT : T_UNKNOWN;
+    case K_ENTRY:
+      if (fnum == 4) return T_BYTES;
+      return (fnum >= 1 && fnum <= 3) ? T_VARINT : T_UNKNOWN;
+    case K_SNAPSHOT:
+      if (fnum == 1) return T_BYTES;
+      if (fnum == 2) { *nested = K_SNAPMETA; return T_NESTED; }
+      return T_UNKNOWN;
+    case K_SNAPMETA:
+      if (fnum == 1) { *nested = K_CONFSTATE; return T_NESTED; }
+      return (fnum == 2 || fnum == 3) ? T_VARINT : T_UNKNOWN;
+    default:  // K_CONFSTATE
+      if (fnum >= 1 && fnum <= 4) return T_REPEATED;
+      return fnum == 5 ? T_VARINT : T_UNKNOWN;
+  }
+}
+
+// Byte source: LDS stage or global memory, addressed by absolute offset.
+struct Src {
+  const u8* g;      // batch buffer
+  const u8* lds;    // staged span or null
+  u64 lbase, lend;  // staged range [lbase, lend)
+  __device__ __forceinline__ u8 at(u64 i) const {
+    return (lds && i >= lbase && i < lend) ? lds[i - lbase] : g[i];
+  }
+};
+
+// The generated decoders' varint loop: error at shift >= 64 or at l.
+__device__ __forceinline__ bool varint(const Src& s, u64& i, u64 l, u64& v) {
+  v = 0;
+  for (u32 shift = 0;; shift += 7) {
+    if (shift >= 64 || i >= l) return false;
+    const u8 b = s.at(i++);
+    v |= u64(b & 0x7Fu) << shift;
+    if (b < 0x80u) return true;
+  }
+}
+
+// skipRaft on [i, l): advances i past one field (with nested groups).
+__device__ bool skip_field(const Src& s, u64& i, u64 l) {
+  const u64 start = i;
+  int depth = 0;
+  while (i < l) {
+    u64 wire;
+    if (!varint(s, i, l, wire)) return false;
+    switch (wire & 7u) {
+      case 0: {
+        for (u32 shift = 0;; shift += 7) {
+          if (shift >= 64 || i >= l) return false;
+          if (s.at(i++) < 0x80u) break;
+        }
+        break;
+      }
+      case 1: i += 8; break;
+      case 2: {
+        u64 len;
+        if (!varint(s, i, l, len)) return false;
+        if (int64_t(len) < 0) return false;
+        i += len;
+        if (i < start) return false;  // wrapped: Go's int overflow -> negative
+        break;
+      }
+      case 3: ++depth; break;
+      case 4:
+        if (depth == 0) return false;
+        --depth;
+        break;
+      case 5: i += 4; break;
+      default: return false;
+    }
+    if (depth == 0) return i <= l;
+  }
+  return false;
+}
+
+struct Fields {
+  u64 type, from, term, log_term, index, reject, hint;
+  u64 ctx_pos, ctx_len;
+  bool has_ctx;
+};
+
+// Message.Unmarshal with every nested message decoded (explicit stack; the
+// deepest nesting is Message > Snapshot > SnapshotMetadata > ConfState).
+__device__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
+  struct Frame {
+    u32 kind;
+    u64 pos, end;
+  } st[4];
+  int sp = 0;
+  st[0] = Frame{K_MESSAGE, start, end};
+  f = Fields{};
+  while (sp >= 0) {
+    Frame& fr = st[sp];
+    if (fr.pos >= fr.end) {
+      --sp;
+      continue;
+    }
+    const u64 l = fr.end;
+    u64 i = fr.pos;
+    const u64 pre = i;
+    u64 wire;
+    if (!varint(s, i, l, wire)) return false;
+    const int fnum = int(u32(wire >> 3));  // int32(wire >> 3)
+    const u32 wt = u32(wire & 7u);
+    if (wt == 4) return false;  // end group for non-group
+    if (fnum <= 0) return false;  // illegal tag
+    u32 nested = 0;
+    const u32 ft = field_type(fr.kind, fnum, &nested);
+    if (ft == T_UNKNOWN) {
+      i = pre;
+      if (!skip_field(s, i, l)) return false;
+      fr.pos = i;
+      continue;
+    }
+    if (ft == T_VARINT) {
+      if (wt != 0) return false;
+      u64 v;
+      if (!varint(s, i, l, v)) return false;
+      if (fr.kind == K_MESSAGE) {
+        switch (fnum) {
+          case 1: f.type = v; break;
+          case 3: f.from = v; break;
+          case 4: f.term = v; break;
+          case 5: f.log_term = v; break;
+          case 6: f.index = v; break;
+          case 10: f.reject = v; break;
+          case 11: f.hint = v; break;
+          default: break;
+        }
+      }
+      fr.pos = i;
+      continue;
+    }
+    if (ft == T_REPEATED && wt == 0) {
+      u64 v;
+      if (!varint(s, i, l, v)) return false;
+      fr.pos = i;
+      continue;
+    }
+    if (wt != 2) return false;  // wrong wiretype
+    u64 len;
+    if (!varint(s, i, l, len)) return false;
+    if (int64_t(len) < 0) return false;
+    const u64 post = i + len;
+    if (post < i || post > l) return false;
+    if (ft == T_BYTES) {
+      if (fr.kind == K_MESSAGE && fnum == 12) {
+        f.has_ctx = true;
+        f.ctx_pos = i;
+        f.ctx_len = len;
+      }
+      fr.pos = post;
+    } else if (ft == T_REPEATED) {  // packed: each varint bounded by l, not post
+      while (i < post) {
+        u64 v;
+        if (!varint(s, i, l, v)) return false;
+      }
+      fr.pos = i;
+    } else {  // nested message on [i, post)
+      fr.pos = post;
+      if (sp + 1 >= 4) return false;  // cannot happen with this schema
+      st[++sp] = Frame{nested, i, post};
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ int kind_of_type(u64 type32) {
+  switch (u32(type32)) {
+    case 4: return QB_IN_APP_RESP;        // MsgAppResp
+    case 9: return QB_IN_HEARTBEAT_RESP;  // MsgHeartbeatResp
+    case 11: return QB_IN_SNAP_STATUS;    // MsgSnapStatus
+    case 10: return QB_IN_UNREACHABLE;    // MsgUnreachable
+    default: return -1;
+  }
+}
+
+struct Args {
+  u64 M, nbytes, G;
+  const u8* bytes;
+  const u64* moff;
+  const u32* mgroup;
+  const u32* off;
+  const u64* ids;
+  u32* rg;
+  u8* rf;
+  u64 *ri, *rt, *rh, *rl;
+  u8* status;
+  u8* mtype;
+  u64* stats;
+};
+
+__global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
+  __shared__ __attribute__((aligned(16))) u8 stage[kStage];
+  __shared__ u32 lds[4];
+  BlockTally<4> tally;
+  const u64 m0 = u64(blockIdx.x) * kBlock;
+  const u64 m = m0 + threadIdx.x;
+  const u64 mlast = (m0 + kBlock < A.M ? m0 + kBlock : A.M);
+  // Stage the block's byte span [b0, b1) when it fits (block-uniform).
+  const u64 b0 = A.moff[m0], b1 = A.moff[mlast];
+  Src s{A.bytes, nullptr, 0, 0};
+  if (b1 > b0 && b1 - b0 <= kStage - 16) {
+    const u64 a0 = b0 & ~u64(15);             // 16-byte aligned window
+    const u64 a1 = (b1 + 15) & ~u64(15);
+    const u64 n16 = (a1 - a0) / 16;
+    const uint4* gsrc = reinterpret_cast<const uint4*>(A.bytes + a0);
+    uint4* ldst = reinterpret_cast<uint4*>(stage);
+    const u64 lim = (A.nbytes + 15) / 16 - a0 / 16;  // 16-byte units readable
+    for (u64 k = threadIdx.x; k < n16; k += kBlock)
+      if (k < lim && a0 + 16 * k + 16 <= A.nbytes) ldst[k] = gsrc[k];
+      else
+        for (u32 t = 0; t < 16; ++t) {
+          const u64 p = a0 + 16 * k + t;
+          stage[16 * k + t] = p < A.nbytes ? A.bytes[p] : 0;
+        }
+    s = Src{A.bytes, stage, a0, a1 < A.nbytes ? a1 : A.nbytes};
+  }
+  __syncthreads();
+  int st_ = -1;
+  if (m < A.M) {
+    const u64 p0 = A.moff[m], p1 = A.moff[m + 1];
+    Fields f;
+    u32 group = 0xFFFFFFFFu;
+    u8 flags = 0;
+    u64 index = 0, term = 0, hint = 0, lterm = 0;
+    if (p1 < p0 || p1 > A.nbytes || !unmarshal_message(s, p0, p1, f)) {
+      st_ = QB_WIRE_UNMARSHAL;
+      if (A.mtype) A.mtype[m] = 0;
+    } else {
+      if (A.mtype) A.mtype[m] = u8(f.type);
+      const int kind = kind_of_type(f.type);
+      if (kind < 0) {
+        st_ = QB_WIRE_TYPE;
+      } else {
+        index = f.index;
+        st_ = QB_WIRE_OK;
+        if (kind == QB_IN_HEARTBEAT_RESP) {
+          index = 0;
+          if (f.has_ctx && f.ctx_len != 0) {
+            u64 v = 0;
+            if (f.ctx_len == 8)
+              for (u32 t = 0; t < 8; ++t) v = (v << 8) | s.at(f.ctx_pos + t);  // big-endian id
+            if (f.ctx_len != 8 || v == 0) st_ = QB_WIRE_CTX;
+            index = v;
+          }
+        }
+        if (st_ == QB_WIRE_OK) {
+          group = A.mgroup[m];
+          u32 slot = QB_REC_NO_PROGRESS;
+          if (group < A.G) {
+            const u32 s0 = A.off[group], s1 = A.off[group + 1];
+            for (u32 j = s0; j < s1; ++j)
+              if (A.ids[j] == f.from) {
+                slot = j - s0;
+                break;
+              }
+          }
+          flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
+          term = f.term;
+          hint = f.hint;
+          lterm = f.log_term;
+        } else {
+          index = 0;
+        }
+      }
+    }
+    A.rg[m] = group;
+    A.rf[m] = flags;
+    A.ri[m] = index;
+    A.rt[m] = term;
+    if (A.rh) A.rh[m] = hint;
+    if (A.rl) A.rl[m] = lterm;
+    A.status[m] = u8(st_);
+  }
+  tally.add(0, st_ == QB_WIRE_OK);
+  tally.add(1, st_ == QB_WIRE_UNMARSHAL);
+  tally.add(2, st_ == QB_WIRE_TYPE);
+  tally.add(3, st_ == QB_WIRE_CTX);
+  const int slot[4] = {QB_WIRE_OK, QB_WIRE_UNMARSHAL, QB_WIRE_TYPE, QB_WIRE_CTX};
+  if (A.stats) tally.flush(lds, A.stats, slot);
+}
+
+}  // namespace wire
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
+                                      const uint64_t* msg_off, const uint32_t* msg_group,
+                                      uint64_t G, const uint32_t* off, const uint64_t* ids,
+                                      uint32_t* rec_group, uint8_t* rec_flags,
+                                      uint64_t* rec_index, uint64_t* rec_term,
+                                      uint64_t* rec_hint, uint64_t* rec_log_term,
+                                      uint8_t* status, uint8_t* msg_type, uint64_t* stats,
+                                      void* stream) {
+  if (M == 0) return QB_OK;
+  QB_REQUIRE(msg_off && msg_group && rec_group && rec_flags && rec_index && rec_term && status,
+             "qb_dev_ingest_messages: msg_off, msg_group, rec_* and status are required");
+  QB_REQUIRE(nbytes == 0 || bytes, "qb_dev_ingest_messages: bytes is NULL");
+  QB_REQUIRE(G == 0 || (off && ids), "qb_dev_ingest_messages: off and ids are required");
+  wire::Args A{M, nbytes, G, bytes, reinterpret_cast<const u64*>(msg_off), msg_group, off,
+               reinterpret_cast<const u64*>(ids), rec_group, rec_flags,
+               reinterpret_cast<u64*>(rec_index), reinterpret_cast<u64*>(rec_term),
+               reinterpret_cast<u64*>(rec_hint), reinterpret_cast<u64*>(rec_log_term), status,
+               msg_type, reinterpret_cast<u64*>(stats)};
+  hipLaunchKernelGGL(wire::k_ingest, dim3(grid_for(M)), dim3(kBlock), 0, as_stream(stream), A);
+  QB_CHECK_LAUNCH("k_ingest");
+  return QB_OK;
+}

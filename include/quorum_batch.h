@@ -81,6 +81,7 @@ extern "C" {
 #define QB_MAX_SLOTS 16
 #define QB_WIDE_MAX_SLOTS 1024
 #define QB_REC_REJECT 0x80u
+#define QB_REC_NO_PROGRESS 0x40u /* leader inbox: From has no Progress (wire ingest) */
 
 /* Counters filled by qb_dev_fixed_apply_appresp (device memory, uint64 each;
  * accumulated, so zero them before a batch if per-batch numbers are wanted). */
@@ -393,7 +394,7 @@ typedef struct qb_leader_groups {
 typedef struct qb_leader_inbox {
   uint64_t M;
   const uint32_t* group;
-  const uint8_t* flags;  /* slot (0-3) | kind << 4 | QB_REC_REJECT          */
+  const uint8_t* flags;  /* slot (0-3) | kind << 4 | QB_REC_NO_PROGRESS | QB_REC_REJECT */
   const uint64_t* index; /* Message.Index; MsgHeartbeatResp: Context (0 = empty) */
   const uint64_t* term;  /* Message.Term (0 = local message)                */
   const uint64_t* hint;  /* Message.RejectHint (nullable: no rejections)    */
@@ -423,6 +424,37 @@ int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
                        uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags,
                        uint64_t* stats, void* workspace, size_t workspace_bytes,
                        void* stream);
+
+/* ----------------------------------------------------------------------- */
+/* Wire ingest                                       */
+/* ----------------------------------------------------------------------- */
+
+/* Raw protobuf-encoded raftpb.Message bytes (raft/raftpb/raft.proto:68-86)
+ * -> leader-inbox records for qb_dev_leader_step.  Message i is
+ * bytes[msg_off[i] .. msg_off[i+1]) and belongs to group msg_group[i] (the
+ * multi-raft envelope's group).  Validation is exactly Message.Unmarshal
+ * (raftpb/raft.pb.go:1739-2061, nested Entry / Snapshot / SnapshotMetadata /
+ * ConfState bodies included, unknown fields skipped as skipRaft).  From is
+ * mapped to its slot among the group's CSR slot IDs (ids[off[g] ..
+ * off[g+1]), ascending); a non-member gets QB_REC_NO_PROGRESS.  MsgAppResp /
+ * MsgHeartbeatResp / MsgSnapStatus / MsgUnreachable become records (a
+ * heartbeat response's Context must be empty or an 8-byte non-zero
+ * big-endian request id, which becomes rec_index); any other status leaves
+ * rec_group = UINT32_MAX (dropped by the step as a bad group).
+ * msg_type (nullable) receives the low byte of Message.Type;
+ * stats (nullable, 4 device uint64, accumulated) counts each status. */
+#define QB_WIRE_OK 0
+#define QB_WIRE_UNMARSHAL 1 /* Message.Unmarshal returns an error           */
+#define QB_WIRE_TYPE 2      /* not a leader-inbox response type             */
+#define QB_WIRE_CTX 3       /* Context neither empty nor an 8-byte id       */
+int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
+                           const uint64_t* msg_off, const uint32_t* msg_group,
+                           uint64_t G, const uint32_t* off, const uint64_t* ids,
+                           uint32_t* rec_group, uint8_t* rec_flags,
+                           uint64_t* rec_index, uint64_t* rec_term,
+                           uint64_t* rec_hint, uint64_t* rec_log_term,
+                           uint8_t* status, uint8_t* msg_type, uint64_t* stats,
+                           void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */

@@ -409,7 +409,7 @@ static void* worker(void* arg) {
              (L->meta[g] >> 8) & 0xFF, &j->out};
     u32 f = in->flags[i], slot = f & 0xF, kind = (f >> 4) & 3;
     int reject = (f & 0x80) != 0;
-    if (slot >= c.ns) {
+    if (slot >= c.ns || (f & 0x40)) { /* no Progress for From */
       j->stats[3]++;
       continue;
     }

@@ -1,0 +1,144 @@
+"""GPU parity of wire ingest (qb_dev_ingest_messages) against the raftpb
+restatement (oracle/raftpb_ref.py, itself checked against Google's protobuf
+runtime): valid messages of every field shape, malformed and mutated bytes
+(every Unmarshal error path), non-members, contexts; then decode + leader
+step end to end against the leader oracle."""
+import copy
+import random
+
+import numpy as np
+import pytest
+
+from oracle import leader_ref as L
+from oracle import raftpb_ref as W
+from tests import leader_pack as LP
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_u64(r):
+    return r.choice([0, 1, 5, 127, 128, 300, 1 << 32, (1 << 63) - 1, 1 << 63, (1 << 64) - 1,
+                     r.getrandbits(64), r.getrandbits(30)])
+
+
+def _random_message(r, ids):
+    t = r.choice([4, 4, 4, 9, 9, 10, 11, 3, 6, 18])
+    frm = r.choice(ids) if ids and r.random() < 0.9 else _rand_u64(r)
+    ctx = None
+    if t == 9 and r.random() < 0.7:
+        ctx = r.choice([b"", r.getrandbits(64).to_bytes(8, "big"), b"\x00" * 8, b"abc"])
+    ents = [W.marshal_entry(_rand_u64(r), _rand_u64(r), r.randint(0, 2),
+                            bytes(r.getrandbits(8) for _ in range(r.randint(0, 4))))
+            for _ in range(r.choice([0, 0, 0, 1, 2]))]
+    snap = W.EMPTY_SNAPSHOT
+    if r.random() < 0.1:
+        snap = W.marshal_snapshot(b"xy", _rand_u64(r), _rand_u64(r),
+                                  W.marshal_conf_state([1, 2, 3], [4], [5], [], True))
+    b = W.marshal_message(t, _rand_u64(r), frm, _rand_u64(r), _rand_u64(r), _rand_u64(r), ents,
+                          _rand_u64(r), snap, r.random() < 0.4, _rand_u64(r), ctx)
+    x = r.random()
+    if x < 0.05:  # unknown fields before/after
+        b = W._key(77, 0) + W.varint(9) + b + W._key(78, 2) + b"\x01z"
+    elif x < 0.10:  # truncation
+        b = b[: r.randint(0, len(b))]
+    elif x < 0.18:  # random byte mutation
+        bb = bytearray(b)
+        for _ in range(r.randint(1, 3)):
+            if bb:
+                bb[r.randrange(len(bb))] = r.getrandbits(8)
+        b = bytes(bb)
+    elif x < 0.20:  # minimal encodings (google-style: only set fields)
+        b = W._key(1, 0) + W.varint(t) + W._key(3, 0) + W.varint(frm) + W._key(6, 0) + W.varint(7)
+    return b
+
+
+def _groups_ids(r, G):
+    off = [0]
+    ids = []
+    for _ in range(G):
+        k = r.randint(1, 16)
+        s = sorted(r.sample(range(1, 10_000), k))
+        ids += s
+        off.append(off[-1] + k)
+    return np.array(off, np.uint32), np.array(ids, np.uint64)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_ingest_matches_oracle(seed):
+    import torch
+    from etcd_amd.quorum import wire
+    r = random.Random(seed)
+    G = 500
+    off, ids = _groups_ids(r, G)
+    msgs, groups = [], []
+    for _ in range(20000):
+        g = r.randrange(G + 3)  # a few envelope groups past G
+        gids = ids[off[g]:off[g + 1]].tolist() if g < G else []
+        msgs.append(_random_message(r, gids))
+        groups.append(g)
+    buf, nb, moff, mg = wire.pack_messages(msgs, groups)
+    stats = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ib, status, mtype = wire.ingest(buf, nb, moff, mg, torch.from_numpy(off.view(np.int32)).cuda(),
+                                    torch.from_numpy(ids.view(np.int64)).cuda(), stats)
+    got = list(zip(status.cpu().numpy().tolist(), ib.group.cpu().numpy().view(np.uint32).tolist(),
+                   ib.flags.cpu().numpy().tolist(),
+                   ib.index.cpu().numpy().view(np.uint64).tolist(),
+                   ib.term.cpu().numpy().view(np.uint64).tolist(),
+                   ib.hint.cpu().numpy().view(np.uint64).tolist(),
+                   ib.log_term.cpu().numpy().view(np.uint64).tolist()))
+    types = mtype.cpu().numpy().tolist()
+    counts = [0, 0, 0, 0]
+    for i, (b, g) in enumerate(zip(msgs, groups)):
+        gids = ids[off[g]:off[g + 1]].tolist() if g < G else []
+        want = W.ingest(b, g, gids)
+        counts[want[0]] += 1
+        assert got[i] == tuple(want[:7]), (i, b.hex(), got[i], want)
+        if want[0] != W.ST_UNMARSHAL:
+            assert types[i] == want[7] & 0xFF, i
+    assert stats.cpu().tolist() == counts
+    assert min(counts) > 0  # every status exercised
+
+
+def test_ingest_then_leader_step_end_to_end():
+    """Encode a random leader batch as raftpb bytes, ingest on the device, run
+    the leader step on the decoded records: identical to the oracle on the
+    original records."""
+    import torch
+    from etcd_amd.quorum import wire
+    from etcd_amd.quorum.leader import LeaderGroups
+    rng = np.random.default_rng(5)
+    groups = LP.random_groups(rng, 400, 4, 3, max_slots=9)
+    recs = LP.random_records(rng, groups, 1500, bad_frac=0)
+    node_ids = [sorted(rng.choice(np.arange(1, 1000), g.n_slots, replace=False).tolist())
+                for g in groups]
+    msgs, env = [], []
+    for gi, m in recs:
+        frm = node_ids[gi][m.slot] if m.slot < groups[gi].n_slots else 5000
+        t = {0: 4, 1: 9, 2: 11, 3: 10}[m.kind]
+        ctx = None
+        if m.kind == 1 and m.index:
+            ctx = m.index.to_bytes(8, "big")
+        idx = 0 if m.kind == 1 else m.index
+        msgs.append(W.marshal_message(t, 1, frm, m.term, m.log_term, idx, reject=m.reject,
+                                      reject_hint=m.hint, context=ctx))
+        env.append(gi)
+    off = np.zeros(len(groups) + 1, np.uint32)
+    off[1:] = np.cumsum([g.n_slots for g in groups])
+    ids = np.array([x for l in node_ids for x in l], np.uint64)
+    buf, nb, moff, mg = wire.pack_messages(msgs, env)
+    ib, status, _ = wire.ingest(buf, nb, moff, mg, torch.from_numpy(off.view(np.int32)).cuda(),
+                                torch.from_numpy(ids.view(np.int64)).cuda())
+    assert int(status.max().item()) == 0
+    eng = LeaderGroups(LP.pack(groups, 4, 3), 4, 3, 0, device="cuda")
+    res = eng.step(ib)
+    orc = copy.deepcopy(groups)
+    for g in orc:
+        g.msgs = []
+    L.run_batch(orc, recs)
+    dev = copy.deepcopy(groups)
+    LP.unpack_into(dev, eng.numpy(), 4, 3)
+    assert [LP.state_key(g) for g in dev] == [LP.state_key(g) for g in orc]
+    want = [(gi,) + m.key() for gi, g in enumerate(orc) for m in g.msgs]
+    got = [(int(m["group"]), int(m["type"]), int(m["to"]), int(m["index"]), int(m["log_term"]),
+            int(m["commit"]), int(m["aux"])) for m in res.msgs]
+    assert got == want
