@@ -51,3 +51,70 @@ def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: tor
     ib = LeaderInbox(rg, rf, ri, rt, rh, rl)
     ib._m = M
     return ib, status[:M], mtype[:M]
+
+
+# ------------------------------------------------------- workload synth ---
+
+def _vfix(v: np.ndarray, n: int) -> np.ndarray:
+    """Varints of exactly n bytes (v must need exactly n bytes)."""
+    v = v.astype(np.uint64)
+    out = np.empty((v.size, n), np.uint8)
+    for k in range(n):
+        b = ((v >> np.uint64(7 * k)) & np.uint64(0x7F)).astype(np.uint8)
+        out[:, k] = b | (0x80 if k < n - 1 else 0)
+    return out
+
+
+_EMPTY_SNAPSHOT = bytes([0x12, 0x08, 0x0A, 0x02, 0x28, 0x00, 0x10, 0x00, 0x18, 0x00])
+# Snapshot{Metadata{ConfState{AutoLeave:false}, Index:0, Term:0}} as gogoproto
+# writes it (non-nullable fields always present).
+
+
+def synth_response_stream(M: int, G: int, seed: int = 0x5EED0008, hb_frac: float = 0.1):
+    """Host bytes of M gogoproto-encoded responses to G 5-voter leaders (the
+    wire-ingest bench workload): MsgAppResp (10% rejected) and, with
+    probability hb_frac, MsgHeartbeatResp carrying an 8-byte read context.
+    Node IDs, terms and indexes are sized so every message of a kind has the
+    same layout (vectorised construction).  Returns (bytes ndarray u8,
+    msg_off u64 [M+1], msg_group u32 [M], off u32 [G+1], ids u64 [5G])."""
+    rng = np.random.default_rng(seed)
+    grp = rng.integers(0, G, M).astype(np.uint32)
+    slot = rng.integers(1, 5, M).astype(np.uint64)
+    g64 = grp.astype(np.uint64)
+    frm = np.uint64(16384) + slot * np.uint64(200000) + (g64 % np.uint64(100000))
+    to = np.uint64(16384) + (g64 % np.uint64(100000))
+    term = np.full(M, 20000, np.uint64)
+    index = np.uint64(1 << 35) + g64 * np.uint64(64) + rng.integers(0, 64, M).astype(np.uint64)
+    reject = rng.random(M) < 0.1
+    hb = rng.random(M) < hb_frac
+    ctx = (np.uint64(1) << np.uint64(56)) + rng.integers(1, 1 << 40, M).astype(np.uint64)
+
+    def col(byte):
+        return np.full((M, 1), byte, np.uint8)
+    app = np.concatenate([
+        col(0x08), col(4), col(0x10), _vfix(to, 3), col(0x18), _vfix(frm, 3), col(0x20),
+        _vfix(term, 3), col(0x28), col(0), col(0x30), _vfix(index, 6), col(0x40), col(0),
+        col(0x4A), col(len(_EMPTY_SNAPSHOT)),
+        np.tile(np.frombuffer(_EMPTY_SNAPSHOT, np.uint8), (M, 1)),
+        col(0x50), reject.astype(np.uint8)[:, None], col(0x58), col(0)], axis=1)
+    ctxb = ((ctx[:, None] >> (np.arange(7, -1, -1, dtype=np.uint64) * np.uint64(8)))
+            & np.uint64(0xFF)).astype(np.uint8)
+    hbm = np.concatenate([
+        col(0x08), col(9), col(0x10), _vfix(to, 3), col(0x18), _vfix(frm, 3), col(0x20),
+        _vfix(term, 3), col(0x28), col(0), col(0x30), col(0), col(0x40), col(0),
+        col(0x4A), col(len(_EMPTY_SNAPSHOT)),
+        np.tile(np.frombuffer(_EMPTY_SNAPSHOT, np.uint8), (M, 1)),
+        col(0x50), col(0), col(0x58), col(0), col(0x62), col(8), ctxb], axis=1)
+    la, lh = app.shape[1], hbm.shape[1]
+    lens = np.where(hb, lh, la).astype(np.uint64)
+    moff = np.zeros(M + 1, np.uint64)
+    np.cumsum(lens, out=moff[1:])
+    buf = np.empty(int(moff[-1]), np.uint8)
+    for sel, t, L_ in ((~hb, app, la), (hb, hbm, lh)):
+        pos = moff[:-1][sel].astype(np.int64)
+        buf[(pos[:, None] + np.arange(L_)).reshape(-1)] = t[sel].reshape(-1)
+    off = (np.arange(G + 1, dtype=np.uint32) * 5).astype(np.uint32)
+    gg = np.repeat(np.arange(G, dtype=np.uint64), 5)
+    ss = np.tile(np.arange(5, dtype=np.uint64), G)
+    ids = np.uint64(16384) + ss * np.uint64(200000) + (gg % np.uint64(100000))
+    return buf, moff, grp, off, ids

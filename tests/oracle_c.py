@@ -34,6 +34,7 @@ SIG = {
                                             _p, _p, _p, _p, _p]),
     "orc_fixed_commit_all": (None, [_u32, _u64, _p, _p, _p, _p]),
     "orc_leader_step": (_u64, [_p, _p, _p, _u64, _p, _p, _p, _i32]),
+    "orc_ingest": (None, [_u64, _p, _u64, _p, _p, _u64, _p, _p] + [_p] * 7 + [_i32]),
 }
 
 _lib = None
@@ -42,7 +43,7 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(ORC_DIR, f) for f in ("quorum_oracle.c", "leader_oracle.c")]
+        srcs = [os.path.join(ORC_DIR, f) for f in ("quorum_oracle.c", "leader_oracle.c", "wire_oracle.c")]
         if not os.path.exists(ORC_PATH) or any(os.path.getmtime(ORC_PATH) < os.path.getmtime(s)
                                                 for s in srcs):
             subprocess.check_call(["make", "-s", "-C", ORC_DIR])
@@ -224,3 +225,20 @@ def leader_step(arrays, inflight_cap, readq_cap, read_only, rec, threads=1, msg_
     total = lib.orc_leader_step(C.byref(lg), C.byref(ib), msgs.ctypes.data, msg_cap,
                                 sd.ctypes.data, gf.ctypes.data, stats.ctypes.data, threads)
     return msgs[:min(total, msg_cap)], int(total), sd, gf, stats
+
+
+def ingest(buf, moff, mgroup, off, ids, threads=1):
+    """Wire ingest restated (oracle/wire_oracle.c): returns dict of record
+    columns + status."""
+    lib = load()
+    M = len(mgroup)
+    out = {"group": np.empty(M, np.uint32), "flags": np.empty(M, np.uint8),
+           "index": np.empty(M, np.uint64), "term": np.empty(M, np.uint64),
+           "hint": np.empty(M, np.uint64), "log_term": np.empty(M, np.uint64),
+           "status": np.empty(M, np.uint8)}
+    b = buf if buf.size else np.zeros(1, np.uint8)
+    lib.orc_ingest(M, ptr(b), int(moff[-1]), ptr(moff), ptr(mgroup), len(off) - 1, ptr(off),
+                   ptr(ids if ids.size else np.zeros(1, np.uint64)), ptr(out["group"]),
+                   ptr(out["flags"]), ptr(out["index"]), ptr(out["term"]), ptr(out["hint"]),
+                   ptr(out["log_term"]), ptr(out["status"]), threads)
+    return out

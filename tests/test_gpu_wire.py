@@ -12,55 +12,9 @@ import pytest
 from oracle import leader_ref as L
 from oracle import raftpb_ref as W
 from tests import leader_pack as LP
+from tests.wire_gen import groups_ids as _groups_ids, random_message as _random_message
 
 pytestmark = pytest.mark.gpu
-
-
-def _rand_u64(r):
-    return r.choice([0, 1, 5, 127, 128, 300, 1 << 32, (1 << 63) - 1, 1 << 63, (1 << 64) - 1,
-                     r.getrandbits(64), r.getrandbits(30)])
-
-
-def _random_message(r, ids):
-    t = r.choice([4, 4, 4, 9, 9, 10, 11, 3, 6, 18])
-    frm = r.choice(ids) if ids and r.random() < 0.9 else _rand_u64(r)
-    ctx = None
-    if t == 9 and r.random() < 0.7:
-        ctx = r.choice([b"", r.getrandbits(64).to_bytes(8, "big"), b"\x00" * 8, b"abc"])
-    ents = [W.marshal_entry(_rand_u64(r), _rand_u64(r), r.randint(0, 2),
-                            bytes(r.getrandbits(8) for _ in range(r.randint(0, 4))))
-            for _ in range(r.choice([0, 0, 0, 1, 2]))]
-    snap = W.EMPTY_SNAPSHOT
-    if r.random() < 0.1:
-        snap = W.marshal_snapshot(b"xy", _rand_u64(r), _rand_u64(r),
-                                  W.marshal_conf_state([1, 2, 3], [4], [5], [], True))
-    b = W.marshal_message(t, _rand_u64(r), frm, _rand_u64(r), _rand_u64(r), _rand_u64(r), ents,
-                          _rand_u64(r), snap, r.random() < 0.4, _rand_u64(r), ctx)
-    x = r.random()
-    if x < 0.05:  # unknown fields before/after
-        b = W._key(77, 0) + W.varint(9) + b + W._key(78, 2) + b"\x01z"
-    elif x < 0.10:  # truncation
-        b = b[: r.randint(0, len(b))]
-    elif x < 0.18:  # random byte mutation
-        bb = bytearray(b)
-        for _ in range(r.randint(1, 3)):
-            if bb:
-                bb[r.randrange(len(bb))] = r.getrandbits(8)
-        b = bytes(bb)
-    elif x < 0.20:  # minimal encodings (google-style: only set fields)
-        b = W._key(1, 0) + W.varint(t) + W._key(3, 0) + W.varint(frm) + W._key(6, 0) + W.varint(7)
-    return b
-
-
-def _groups_ids(r, G):
-    off = [0]
-    ids = []
-    for _ in range(G):
-        k = r.randint(1, 16)
-        s = sorted(r.sample(range(1, 10_000), k))
-        ids += s
-        off.append(off[-1] + k)
-    return np.array(off, np.uint32), np.array(ids, np.uint64)
 
 
 @pytest.mark.parametrize("seed", [1, 2])
@@ -142,3 +96,26 @@ def test_ingest_then_leader_step_end_to_end():
     got = [(int(m["group"]), int(m["type"]), int(m["to"]), int(m["index"]), int(m["log_term"]),
             int(m["commit"]), int(m["aux"])) for m in res.msgs]
     assert got == want
+
+
+def test_response_stream_full_size_vs_c_oracle():
+    """The bench workload (4M gogoproto-encoded responses to 1M leaders)
+    decoded on the device and by the C restatement: every column identical."""
+    import torch
+    from etcd_amd.quorum import wire
+    from tests import oracle_c as oc
+    M, G = 1 << 22, 1 << 20
+    buf, moff, grp, off, ids = wire.synth_response_stream(M, G)
+    dev = "cuda"
+    ib, status, _ = wire.ingest(torch.from_numpy(buf).to(dev), int(moff[-1]),
+                                torch.from_numpy(moff.view(np.int64)).to(dev),
+                                torch.from_numpy(grp.view(np.int32)).to(dev),
+                                torch.from_numpy(off.view(np.int32)).to(dev),
+                                torch.from_numpy(ids.view(np.int64)).to(dev))
+    want = oc.ingest(buf, moff, grp, off, ids, threads=16)
+    assert np.array_equal(status.cpu().numpy(), want["status"])
+    assert int(want["status"].max()) == 0
+    assert np.array_equal(ib.group.cpu().numpy().view(np.uint32), want["group"])
+    assert np.array_equal(ib.flags.cpu().numpy(), want["flags"])
+    for col in ("index", "term", "hint", "log_term"):
+        assert np.array_equal(getattr(ib, col).cpu().numpy().view(np.uint64), want[col]), col

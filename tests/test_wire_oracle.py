@@ -173,3 +173,27 @@ def test_ingest_contract():
     assert W.ingest(W.marshal_message(9, 3, 9, 5, context=b"abc"), 11, ids)[0] == W.ST_CTX
     assert W.ingest(W.marshal_message(6, 3, 9, 5), 11, ids)[0] == W.ST_TYPE
     assert W.ingest(b"\x00", 11, ids)[0] == W.ST_UNMARSHAL
+
+
+def test_c_ingest_matches_python_restatement():
+    import numpy as np
+    from tests import oracle_c as oc
+    from tests.wire_gen import groups_ids, random_message
+    r = random.Random(3)
+    G = 200
+    off, ids = groups_ids(r, G)
+    msgs, groups = [], []
+    for _ in range(5000):
+        g = r.randrange(G + 2)
+        msgs.append(random_message(r, ids[off[g]:off[g + 1]].tolist() if g < G else []))
+        groups.append(g)
+    moff = np.zeros(len(msgs) + 1, np.uint64)
+    moff[1:] = np.cumsum([len(m) for m in msgs])
+    buf = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    out = oc.ingest(buf, moff, np.array(groups, np.uint32), off, ids, threads=3)
+    for i, (b, g) in enumerate(zip(msgs, groups)):
+        want = W.ingest(b, g, ids[off[g]:off[g + 1]].tolist() if g < G else [])
+        got = (int(out["status"][i]), int(out["group"][i]), int(out["flags"][i]),
+               int(out["index"][i]), int(out["term"][i]), int(out["hint"][i]),
+               int(out["log_term"][i]))
+        assert got == tuple(want[:7]), (i, b.hex())

@@ -219,6 +219,44 @@ def leader_config(G, reps, warm=4):
                                        "C restatement of stepLeader (oracle/leader_oracle.c)"}})
 
 
+def wire_config(M, reps):
+    """§8f row 3: wire ingest of M gogoproto-encoded responses (MsgAppResp +
+    10% MsgHeartbeatResp with read contexts) to M/4 5-voter leaders."""
+    from etcd_amd.quorum import wire
+    from tests import oracle_c as oc
+    G = M // 4
+    buf, moff, grp, off, ids = wire.synth_response_stream(M, G)
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_moff = torch.from_numpy(moff.view(np.int64)).to(dev)
+    d_grp = torch.from_numpy(grp.view(np.int32)).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    nb = int(moff[-1])
+    t = time_region(lambda: wire.ingest(d_buf, nb, d_moff, d_grp, d_off, d_ids), reps)
+    # bytes read: message bytes + offset 8 + envelope group 4 + the group's
+    # slot IDs 40 (5 x u64, read once per message); written: group 4, flags
+    # 1, index/term/hint/log_term 32, status 1, type 1
+    algo = nb + M * (8 + 4 + 40) + M * (4 + 1 + 32 + 1 + 1)
+    import time
+    Ms = 1 << 22
+    cpu = {}
+    for threads in (16, 1):
+        reps_c, t0 = 0, time.perf_counter()
+        while True:
+            oc.ingest(buf[: int(moff[Ms])], moff[: Ms + 1], grp[:Ms], off, ids, threads=threads)
+            reps_c += 1
+            if time.perf_counter() - t0 > 4:
+                break
+        cpu[threads] = reps_c * Ms / (time.perf_counter() - t0)
+    report("wire ingest (raftpb.Message -> leader inbox)", M, t, algo,
+           {"unit": "messages/s", "bytes_per_message": nb / M,
+            "input_GBs": nb / t / 1e9,
+            "cpu_baseline": {"value": cpu[16], "unit": "messages/s", "cores": 16, "kind": "port",
+                             "value_1thread": cpu[1],
+                             "sample": f"{Ms} messages of the same stream, C restatement of "
+                                       "gogoproto Message.Unmarshal + ingest (oracle/wire_oracle.c)"}})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
@@ -233,6 +271,8 @@ def main():
         tracker_config(1 << 24, a.reps)
     if "leader" in which:
         leader_config(1 << 22, a.reps)
+    if "wire" in which:
+        wire_config(1 << 24, a.reps)
 
 
 if __name__ == "__main__":
