@@ -69,6 +69,8 @@ SIGNATURES = {
     "qb_dev_leader_step": (_i32, [_p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_dev_ingest_messages": (_i32, [_u64, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p,
                                       _p, _p, _p, _p, _p]),
+    "qb_conf_change_workspace_bytes": (C.c_size_t, [_u64]),
+    "qb_dev_conf_change": (_i32, [_p, _p, _p, C.c_size_t, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
     "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
     "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),

@@ -457,6 +457,101 @@ int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
                            void* stream);
 
 /* ----------------------------------------------------------------------- */
+/* Configuration changes                             */
+/* ----------------------------------------------------------------------- */
+
+/* One confchange.Changer operation per group, all groups in one call:
+ * Simple / EnterJoint(autoLeave) / LeaveJoint (confchange/confchange.go:
+ * 49-146) over the group's ConfChangeSingle list (apply, makeVoter,
+ * makeLearner, remove, initProgress: confchange.go:151-281), with
+ * checkInvariants on input and output (confchange.go:283-334).
+ * A group's config is its CSR slots (ascending IDs of the ProgressMap) with
+ * cfg = Voters[0] | Voters[1] << 16 and ext = LearnersNext | AutoLeave << 16;
+ * a slot in none of the three masks is a learner.  The result is written to
+ * a second set of arrays (double-buffered): new_off [G+1] (offsets), slot
+ * IDs, masks and the Progress arrays of the leader-step layout — carried for
+ * kept slots, initialised for added ones (Next = last_index[g], Match 0,
+ * StateProbe, RecentActive; initProgress).  A group whose operation fails
+ * keeps its config and Progress; err[g] names the reference's error and
+ * err_id[g] (nullable) the offending ID where the message has one (the
+ * smallest such ID).  Restore(ConfState) (confchange/restore.go:116-155) is a
+ * sequence of such calls. */
+#define QB_CC_NONE 0                 /* copy through                      */
+#define QB_CC_SIMPLE 1
+#define QB_CC_ENTER_JOINT 2
+#define QB_CC_ENTER_JOINT_AUTOLEAVE 3
+#define QB_CC_LEAVE_JOINT 4
+
+/* raftpb.ConfChangeType (raft.pb.go) */
+#define QB_CC_ADD_NODE 0
+#define QB_CC_REMOVE_NODE 1
+#define QB_CC_UPDATE_NODE 2
+#define QB_CC_ADD_LEARNER 3
+
+enum {
+  QB_CCERR_OK = 0,
+  QB_CCERR_ALREADY_JOINT = 1,       /* "config is already joint"                        */
+  QB_CCERR_ZERO_VOTER_JOINT = 2,    /* "can't make a zero-voter config joint"           */
+  QB_CCERR_NOT_JOINT = 3,           /* "can't leave a non-joint config"                 */
+  QB_CCERR_SIMPLE_IN_JOINT = 4,     /* "can't apply simple config change in joint config" */
+  QB_CCERR_MORE_THAN_ONE = 5,       /* "more than one voter changed without entering joint config" */
+  QB_CCERR_REMOVED_ALL = 6,         /* "removed all voters"                             */
+  QB_CCERR_UNKNOWN_TYPE = 7,        /* "unexpected conf type %d"                        */
+  QB_CCERR_NO_PROGRESS = 8,         /* "no progress for %d"                             */
+  QB_CCERR_LNEXT_NOT_OUTGOING = 9,  /* "%d is in LearnersNext, but not Voters[1]"       */
+  QB_CCERR_LNEXT_IS_LEARNER = 10,   /* "%d is in LearnersNext, but is already marked as learner" */
+  QB_CCERR_LEARNER_OUTGOING = 11,   /* "%d is in Learners and Voters[1]"                */
+  QB_CCERR_LEARNER_INCOMING = 12,   /* "%d is in Learners and Voters[0]"                */
+  QB_CCERR_LEARNER_NOT_MARKED = 13, /* "%d is in Learners, but is not marked as learner" */
+  QB_CCERR_AUTOLEAVE_NOT_JOINT = 14, /* "AutoLeave must be false when not joint"        */
+  QB_CCERR_TOO_MANY_SLOTS = 15,     /* engine limit: more than QB_MAX_SLOTS members     */
+  QB_CCERR_BAD_OP = 16              /* op is not a QB_CC_* operation                     */
+};
+
+typedef struct qb_conf_change_in {
+  uint64_t G;
+  uint32_t inflight_cap;     /* ring size of infl_buf per slot */
+  uint32_t reserved;
+  const uint8_t* op;         /* [G] QB_CC_*                           */
+  const uint32_t* cc_off;    /* [G+1] ConfChangeSingle list per group */
+  const uint8_t* cc_type;    /* [cc_off[G]] QB_CC_ADD_NODE ...         */
+  const uint64_t* cc_node;   /* [cc_off[G]] NodeID (0 = ignored)       */
+  const uint64_t* last_index; /* [G] Changer.LastIndex                 */
+  const uint32_t* off;       /* [G+1] current slots                    */
+  const uint64_t* ids;       /* [off[G]] ascending per group           */
+  const uint32_t* cfg;       /* [G]                                     */
+  const uint32_t* ext;       /* [G] (nullable: no LearnersNext/AutoLeave) */
+  const uint64_t* match;     /* Progress, leader-step layout [off[G]]  */
+  const uint64_t* next;
+  const uint64_t* pending_snapshot;
+  const uint8_t* pstate;
+  const uint32_t* infl_pos;
+  const uint64_t* infl_buf;  /* [off[G] * inflight_cap] */
+} qb_conf_change_in;
+
+typedef struct qb_conf_change_out {
+  uint64_t slot_cap;         /* capacity of the per-slot output arrays */
+  uint32_t* new_off;         /* [G+1]; new_off[G] = slots needed        */
+  uint64_t* ids;
+  uint32_t* cfg;             /* [G] */
+  uint32_t* ext;             /* [G] */
+  uint64_t* match;
+  uint64_t* next;
+  uint64_t* pending_snapshot;
+  uint8_t* pstate;
+  uint32_t* infl_pos;
+  uint64_t* infl_buf;
+  uint8_t* err;              /* [G] QB_CCERR_*   */
+  uint64_t* err_id;          /* [G] (nullable)   */
+} qb_conf_change_out;
+
+size_t qb_conf_change_workspace_bytes(uint64_t G);
+/* If new_off[G] > slot_cap nothing past the capacity is written: check
+ * new_off[G] after the call. */
+int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_change_out* out,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */
 /* ----------------------------------------------------------------------- */
 

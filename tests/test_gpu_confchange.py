@@ -1,0 +1,136 @@
+"""GPU parity of batched conf changes (qb_dev_conf_change) against the
+confchange restatement: the reference's datadriven testdata replayed with
+one group per file (outputs compared as the reference's text), random
+operation sequences over many groups, and Restore(ConfState)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import confchange_ref as CC
+from tests import confchange_pack as CP
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DD = json.load(open(os.path.join(ROOT, "tests", "golden", "confchange_datadriven.json")))
+OPS = {"simple": 1, "enter-joint": 2, "leave-joint": 4}
+
+
+def _table(trackers, K=10):
+    from etcd_amd.quorum.confchange import ConfigTable
+    off, ids, cfg, ext, prog = CP.pack(trackers)
+    return ConfigTable.from_numpy(off, ids, cfg, ext, prog, K)
+
+
+def _render(t):
+    return t.config_string() + "\n" + t.progress_string()
+
+
+def test_datadriven_on_device():
+    from etcd_amd.quorum.confchange import error_text
+    names = sorted(DD)
+    table = _table([CC.Tracker.empty(10) for _ in names])
+    steps = max(len(DD[n]) for n in names)
+    for k in range(steps):
+        op, ccs, host_err = [], [], {}
+        for g, n in enumerate(names):
+            c = DD[n][k] if k < len(DD[n]) else None
+            if c is None:
+                op.append(0)
+                ccs.append([])
+                continue
+            cc = CC.parse_ccs(c["input"])
+            o = OPS[c["cmd"]]
+            if o == 2 and c.get("autoleave"):
+                o = 3
+            if o == 4 and cc:
+                host_err[g] = "this command takes no input"
+                op.append(0)
+                ccs.append([])
+                continue
+            op.append(o)
+            ccs.append(cc)
+        table, err, err_id = table.change(op, ccs, [k] * len(names))
+        state = CP.unpack(table.numpy(), 10)
+        for g, n in enumerate(names):
+            if k >= len(DD[n]):
+                continue
+            c = DD[n][k]
+            if g in host_err:
+                got = host_err[g] + "\n"
+            elif err[g]:
+                got = error_text(int(err[g]), int(err_id[g])) + "\n"
+            else:
+                got = _render(state[g])
+            assert got == c["expected"], f"{n}:{c['line']}\n{got}\nwant\n{c['expected']}"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_sequences(seed):
+    from etcd_amd.quorum.confchange import error_text
+    r = random.Random(seed)
+    G = 600
+    orc = [CC.Tracker.empty(7) for _ in range(G)]
+    # random carried Progress content, so the copy of kept slots is checked
+    table = _table(orc, K=7)
+    for step in range(12):
+        op = [CP.random_op(r, t) for t in orc]
+        ccs = [CP.random_ccs(r) for _ in orc]
+        last = [r.randint(0, 1000) for _ in orc]
+        table, err, err_id = table.change(op, ccs, last)
+        dev = CP.unpack(table.numpy(), 7)
+        for g in range(G):
+            nt, e = CP.oracle_apply(orc[g], op[g], ccs[g], last[g])
+            if e is None and sum(1 for _ in nt.prs) > 16:
+                e = "more than 16 members (engine limit)"
+                nt = orc[g]
+            got_e = error_text(int(err[g]), int(err_id[g])) if err[g] else None
+            assert got_e == e, (seed, step, g, op[g], ccs[g], got_e, e)
+            assert _render(dev[g]) == _render(nt), (seed, step, g)
+            orc[g] = nt
+        # perturb carried Progress on the device side and the oracle alike
+        a = table.numpy()
+        for g in range(G):
+            for j, s in enumerate(range(int(a["off"][g]), int(a["off"][g + 1]))):
+                i = int(a["ids"][s])
+                v = r.randint(0, 99)
+                a["match"][s] = v
+                orc[g].prs[i].match = v
+        from etcd_amd.quorum.confchange import ConfigTable
+        table = ConfigTable.from_numpy(a["off"], a["ids"], a["cfg"], a["ext"],
+                                       {k: a[k] for k in ("match", "next", "pending_snapshot",
+                                                          "pstate", "infl_pos", "infl_buf")}, 7)
+
+
+def test_restore_batch():
+    from etcd_amd.quorum.confchange import restore
+    r = random.Random(11)
+    G = 300
+    states = []
+    for _ in range(G):
+        ids = list(range(1, 1 + r.randint(1, 10)))
+        r.shuffle(ids)
+        nv = r.randint(1, len(ids))
+        voters, rest = ids[:nv], ids[nv:]
+        nl = r.randint(0, len(rest))
+        learners = rest[:nl]
+        outgoing, lnext = [], []
+        if r.random() < 0.5:
+            pool = voters + rest[nl:]
+            outgoing = r.sample(pool, r.randint(1, len(pool)))
+            cand = [i for i in outgoing if i not in voters]
+            lnext = r.sample(cand, r.randint(0, len(cand)))
+            learners = [i for i in learners if i not in outgoing]
+        states.append(dict(voters=voters, learners=learners, voters_outgoing=outgoing,
+                           learners_next=lnext, auto_leave=bool(outgoing) and r.random() < 0.5))
+    table, err, _ = restore(_table([CC.Tracker.empty(5) for _ in range(G)], K=5), states,
+                            [10] * G)
+    assert not err.any()
+    dev = CP.unpack(table.numpy(), 5)
+    for g, cs in enumerate(states):
+        want = CC.restore(CC.Tracker.empty(5), 10, cs["voters"], cs["learners"],
+                          cs["voters_outgoing"], cs["learners_next"], cs["auto_leave"])
+        assert _render(dev[g]) == _render(want), g
