@@ -99,31 +99,41 @@ class ConfigTable:
                last_index: Sequence[int]):
         """Apply op[g] with ccs[g] = [(ConfChangeType, NodeID), ...] to every
         group; returns (new ConfigTable, err u8[G], err_id u64[G])."""
-        dev = self.t["off"].device
         G = self.G
         cc_off = np.zeros(G + 1, np.uint32)
         cc_off[1:] = np.cumsum([len(c) for c in ccs])
         flat = [x for c in ccs for x in c]
-        cc_type = np.array([t for t, _ in flat], np.uint8)
-        cc_node = np.array([n for _, n in flat], np.uint64)
-        d_op = _dev(op, np.uint8, dev)
-        d_ccoff, d_cct, d_ccn = (_dev(cc_off, np.uint32, dev), _dev(cc_type, np.uint8, dev),
-                                 _dev(cc_node, np.uint64, dev))
-        d_last = _dev(last_index, np.uint64, dev)
-        cap = min(16 * G, self.S + len(flat)) + 1
+        return self.change_soa(np.asarray(op, np.uint8), cc_off,
+                               np.array([t for t, _ in flat], np.uint8),
+                               np.array([n for _, n in flat], np.uint64),
+                               np.asarray(last_index, np.uint64))
+
+    def change_soa(self, op, cc_off, cc_type, cc_node, last_index, fetch_errors=True):
+        """As ``change`` with the operation already in SoA form (numpy arrays
+        or device tensors): op[G] u8, cc_off[G+1] u32, cc_type / cc_node per
+        change, last_index[G] u64."""
+        dev = self.t["off"].device
+        G = self.G
+
+        def d(a, dt):
+            return a if isinstance(a, torch.Tensor) else _dev(a, dt, dev)
+        d_op, d_ccoff = d(op, np.uint8), d(cc_off, np.uint32)
+        d_cct, d_ccn, d_last = d(cc_type, np.uint8), d(cc_node, np.uint64), d(last_index, np.uint64)
+        n_changes = int(d_ccoff[G].item()) if isinstance(cc_off, torch.Tensor) else int(cc_off[-1])
+        cap = min(16 * G, self.S + n_changes) + 1
         K = self.inflight_cap
         o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
-             "ids": torch.zeros(cap, dtype=torch.int64, device=dev),
-             "cfg": torch.zeros(G, dtype=torch.int32, device=dev),
-             "ext": torch.zeros(G, dtype=torch.int32, device=dev),
-             "match": torch.zeros(cap, dtype=torch.int64, device=dev),
-             "next": torch.zeros(cap, dtype=torch.int64, device=dev),
-             "pending_snapshot": torch.zeros(cap, dtype=torch.int64, device=dev),
-             "pstate": torch.zeros(cap, dtype=torch.uint8, device=dev),
-             "infl_pos": torch.zeros(cap, dtype=torch.int32, device=dev),
-             "infl_buf": torch.zeros(max(1, cap * K), dtype=torch.int64, device=dev),
-             "err": torch.zeros(G, dtype=torch.uint8, device=dev),
-             "err_id": torch.zeros(G, dtype=torch.int64, device=dev)}
+             "ids": torch.empty(cap, dtype=torch.int64, device=dev),
+             "cfg": torch.empty(G, dtype=torch.int32, device=dev),
+             "ext": torch.empty(G, dtype=torch.int32, device=dev),
+             "match": torch.empty(cap, dtype=torch.int64, device=dev),
+             "next": torch.empty(cap, dtype=torch.int64, device=dev),
+             "pending_snapshot": torch.empty(cap, dtype=torch.int64, device=dev),
+             "pstate": torch.empty(cap, dtype=torch.uint8, device=dev),
+             "infl_pos": torch.empty(cap, dtype=torch.int32, device=dev),
+             "infl_buf": torch.empty(max(1, cap * K), dtype=torch.int64, device=dev),
+             "err": torch.empty(G, dtype=torch.uint8, device=dev),
+             "err_id": torch.empty(G, dtype=torch.int64, device=dev)}
         i = _In(G=G, inflight_cap=K, reserved=0)
         for k, v in (("op", d_op), ("cc_off", d_ccoff), ("cc_type", d_cct), ("cc_node", d_ccn),
                      ("last_index", d_last)):
@@ -135,9 +145,11 @@ class ConfigTable:
         for k, v in o.items():
             setattr(out, k, v.data_ptr())
         need = _lib.load().qb_conf_change_workspace_bytes(G)
-        ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        _lib.call("qb_dev_conf_change", C.byref(i), C.byref(out), ws.data_ptr(), need,
+        if getattr(self, "_ws", None) is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _lib.call("qb_dev_conf_change", C.byref(i), C.byref(out), self._ws.data_ptr(), need,
                   torch.cuda.current_stream(dev).cuda_stream)
+        self._last_out = (i, out, o)  # keep the argument blocks alive until the stream is synced
         S_new = int(o["new_off"][G].item())
         if S_new > cap:
             raise _lib.QuorumBatchError(f"conf change needs {S_new} slots, capacity {cap}")
@@ -145,6 +157,8 @@ class ConfigTable:
         for k in ("ids", "match", "next", "pending_snapshot", "pstate", "infl_pos", "infl_buf"):
             t[k] = o[k]
         nt = ConfigTable(G, S_new, K, t)
+        if not fetch_errors:
+            return nt, o["err"], o["err_id"]
         return (nt, o["err"].cpu().numpy(), o["err_id"].cpu().numpy().view(np.uint64))
 
 

@@ -257,6 +257,56 @@ def wire_config(M, reps):
                                        "gogoproto Message.Unmarshal + ingest (oracle/wire_oracle.c)"}})
 
 
+def confchange_config(G, reps):
+    """§8f row 4: one Changer.Simple(AddLearnerNode) per group over G 5-voter
+    groups (Progress carried for 5 slots, initialised for the new one),
+    groups/s; CPU beside it: the Python restatement on a small sample."""
+    import time
+    from etcd_amd.quorum.confchange import ConfigTable, ADD_LEARNER, SIMPLE
+    from oracle import confchange_ref as CC
+    K = 4
+    S = 5 * G
+    off = torch.arange(0, S + 1, 5, dtype=torch.int32, device=dev)
+    ids = (torch.arange(S, dtype=torch.int64, device=dev) % 5) + 1
+    t = {"off": off, "ids": ids,
+         "cfg": torch.full((G,), 0x1F, dtype=torch.int32, device=dev),
+         "ext": torch.zeros(G, dtype=torch.int32, device=dev),
+         "match": torch.arange(S, dtype=torch.int64, device=dev),
+         "next": torch.arange(S, dtype=torch.int64, device=dev) + 1,
+         "pending_snapshot": torch.zeros(S, dtype=torch.int64, device=dev),
+         "pstate": torch.full((S,), 1 | 8, dtype=torch.uint8, device=dev),
+         "infl_pos": torch.zeros(S, dtype=torch.int32, device=dev),
+         "infl_buf": torch.zeros(S * K, dtype=torch.int64, device=dev)}
+    table = ConfigTable(G, S, K, t)
+    op = torch.full((G,), SIMPLE, dtype=torch.uint8, device=dev)
+    cc_off = torch.arange(G + 1, dtype=torch.int32, device=dev)
+    cc_type = torch.full((G,), ADD_LEARNER, dtype=torch.uint8, device=dev)
+    cc_node = torch.full((G,), 6, dtype=torch.int64, device=dev)
+    last = torch.full((G,), 100, dtype=torch.int64, device=dev)
+    tt = time_region(lambda: table.change_soa(op, cc_off, cc_type, cc_node, last,
+                                              fetch_errors=False), reps)
+    # read: off 4, ids 40, cfg/ext 8, op 1, cc_off 4, cc 9, last 8, Progress
+    # 5 x (8+8+8+1+4+K*8); written: new_off 4, ids 48, cfg/ext 8, Progress
+    # 6 x (29 + K*8), err 1, err_id 8
+    pr = 29 + 8 * K
+    algo = G * (4 + 40 + 8 + 1 + 4 + 9 + 8 + 5 * pr + 4 + 48 + 8 + 6 * pr + 9)
+    n = 20000
+    trs = []
+    for _ in range(n):
+        tr = CC.Tracker.empty(K)
+        tr.voters_in = {1, 2, 3, 4, 5}
+        tr.prs = {i: CC.Pr(match=i, next=i + 1, state=1, recent_active=True) for i in range(1, 6)}
+        trs.append(tr)
+    t0 = time.perf_counter()
+    for tr in trs:
+        CC.Changer(tr, 100).simple([(CC.ADD_LEARNER, 6)])
+    cpu1 = n / (time.perf_counter() - t0)
+    report("conf change (Simple AddLearner, 5 -> 6 slots)", G, tt, algo,
+           {"unit": "groups/s", "cpu_baseline": {
+               "value": cpu1, "unit": "groups/s", "cores": 1, "kind": "port",
+               "sample": f"{n} groups, Python restatement of confchange.Changer (oracle)"}})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
@@ -273,6 +323,8 @@ def main():
         leader_config(1 << 22, a.reps)
     if "wire" in which:
         wire_config(1 << 24, a.reps)
+    if "confchange" in which:
+        confchange_config(1 << 23, a.reps)
 
 
 if __name__ == "__main__":
