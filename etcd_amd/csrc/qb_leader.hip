@@ -25,10 +25,13 @@
 //                    messages into an 8-slot per-group area of the workspace,
 //                    spilling into 32-message chunks from a shared pool
 //   L5 scan          exclusive scan of the message counts
-//   L6 k_ld_emit     one thread per group copies its messages to their final
-//                    place (group order, emission order within a group)
+//   L6 k_ld_emit     each workgroup copies its groups' messages, word by word,
+//                    into their final place (group order, emission order
+//                    within a group)
 // Only L4 is control-heavy; it touches a group's state only if the group has
 // records.
+#include <cstdlib>
+
 #include "qb_common.h"
 #include "qb_scan.h"
 
@@ -130,7 +133,7 @@ struct Group {
   u32 s0, ns;           // first slot, number of slots
   u32 mask_in, mask_out;
   u32 meta;
-  u64 term, committed, first, last, snap_i, snap_t, max_ents;
+  u64 term, committed;
   u32 nruns;
   u32 nmsg, stored;     // messages generated / stored (the pool can run out)
   u32 chunk;            // current overflow chunk
@@ -138,13 +141,21 @@ struct Group {
 };
 
 __device__ __forceinline__ u32 leader_slot(const Group& G_) { return G_.meta & 0xFFu; }
+// Read-only log-view fields are re-read where used (L1 hits) instead of being
+// held in registers for the whole step: this kernel is latency-bound and its
+// occupancy is set by its VGPR count.
+#define LG_FIRST(A, G_) U((A).lg.first_index)[(G_).g]
+#define LG_LAST(A, G_) U((A).lg.last_index)[(G_).g]
+#define LG_SNAP_I(A, G_) U((A).lg.snap_index)[(G_).g]
+#define LG_SNAP_T(A, G_) U((A).lg.snap_term)[(G_).g]
+#define LG_MAX_ENTS(A, G_) U((A).lg.max_ents)[(G_).g]
 __device__ __forceinline__ u32 transferee(const Group& G_) { return (G_.meta >> 8) & 0xFFu; }
 
 // raftLog.term (log.go:268-288, zeroTermOnErrCompacted): 0 outside
 // [firstIndex-1, lastIndex]; otherwise the term of the run holding i.
 __device__ u64 log_term(const Args& A, const Group& G_, u64 i) {
-  const u64 dummy = G_.first - 1;
-  if (i < dummy || i > G_.last) return 0;
+  const u64 dummy = LG_FIRST(A, G_) - 1;
+  if (i < dummy || i > LG_LAST(A, G_)) return 0;
   u64 t = 0;
   const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
   const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
@@ -157,12 +168,12 @@ __device__ u64 log_term(const Args& A, const Group& G_, u64 i) {
 // run every index has the run's term, so when that term is above `term` the
 // whole run (down to the dummy entry) is skipped.
 __device__ u64 find_conflict_by_term(const Args& A, const Group& G_, u64 index, u64 term) {
-  if (index > G_.last) return index;
-  const u64 dummy = G_.first - 1;
+  if (index > LG_LAST(A, G_)) return index;
+  const u64 dummy = LG_FIRST(A, G_) - 1;
   const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
   const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
   for (;;) {
-    if (index < dummy || index > G_.last) return index;  // term 0 <= term
+    if (index < dummy || index > LG_LAST(A, G_)) return index;  // term 0 <= term
     u64 t = 0, start = 0;
     for (u32 r = 0; r < G_.nruns; ++r)
       if (rs[r] <= index) {
@@ -315,19 +326,19 @@ __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if
   const u64 term = log_term(A, G_, nx - 1);
   u64 n = 0;
   bool compacted = false;
-  if (nx <= G_.last) {
-    if (nx < G_.first) compacted = true;
+  if (nx <= LG_LAST(A, G_)) {
+    if (nx < LG_FIRST(A, G_)) compacted = true;
     else {
-      const u64 avail = G_.last - nx + 1;
-      n = avail < G_.max_ents ? avail : G_.max_ents;
+      const u64 avail = LG_LAST(A, G_) - nx + 1;
+      n = avail < LG_MAX_ENTS(A, G_) ? avail : LG_MAX_ENTS(A, G_);
     }
   }
   if (n == 0 && !send_if_empty) return false;
   if (compacted) {
     if (!(*p.st & QB_PR_RECENT_ACTIVE)) return false;
-    if (G_.snap_i == 0) return false;  // ErrSnapshotTemporarilyUnavailable
-    emit(A, G_, QB_MSG_SNAP, to, G_.snap_i, G_.snap_t, 0, 0);
-    become_snapshot(p, G_.snap_i);
+    if (LG_SNAP_I(A, G_) == 0) return false;  // ErrSnapshotTemporarilyUnavailable
+    emit(A, G_, QB_MSG_SNAP, to, LG_SNAP_I(A, G_), LG_SNAP_T(A, G_), 0, 0);
+    become_snapshot(p, LG_SNAP_I(A, G_));
     return true;
   }
   emit(A, G_, QB_MSG_APP, to, nx - 1, term, G_.committed, n);
@@ -346,28 +357,28 @@ __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if
 
 // tracker.go:177-179 -> joint.go:49-56 -> majority.go:126-172: the q-th
 // largest match among a half's voters = the largest member value v with
-// #{members >= v} >= q.
-__device__ u64 half_ci(const u64 (&m)[QB_MAX_SLOTS], u32 mask) {
+// #{members >= v} >= q.  Runtime loops over the group's slots (its match
+// values stay in L1 after the first touch): a register-resident 16-wide
+// network cost ~60 VGPRs and halved the occupancy of this latency-bound
+// kernel.
+__device__ u64 half_ci(const u64* mp, u32 ns, u32 mask) {
   if (mask == 0) return kInf;
   const int q = __popc(mask) / 2 + 1;
   u64 best = 0;
-#pragma unroll
-  for (int i = 0; i < QB_MAX_SLOTS; ++i) {
+  for (u32 i = 0; i < ns; ++i) {
     if (!((mask >> i) & 1u)) continue;
+    const u64 vi = mp[i];
+    if (vi <= best) continue;
     int c = 0;
-#pragma unroll
-    for (int j = 0; j < QB_MAX_SLOTS; ++j) c += ((mask >> j) & 1u) && m[j] >= m[i];
-    if (c >= q && m[i] > best) best = m[i];
+    for (u32 j = 0; j < ns; ++j) c += ((mask >> j) & 1u) && mp[j] >= vi;
+    if (c >= q) best = vi;
   }
   return best;
 }
 
 __device__ bool maybe_commit(const Args& A, Group& G_) {
-  u64 m[QB_MAX_SLOTS];
   const u64* mp = U(A.lg.match) + G_.s0;
-#pragma unroll
-  for (int j = 0; j < QB_MAX_SLOTS; ++j) m[j] = u32(j) < G_.ns ? mp[j] : 0ull;
-  const u64 a = half_ci(m, G_.mask_in), b = half_ci(m, G_.mask_out);
+  const u64 a = half_ci(mp, G_.ns, G_.mask_in), b = half_ci(mp, G_.ns, G_.mask_out);
   const u64 mci = a < b ? a : b;
   if (mci > G_.committed && log_term(A, G_, mci) == G_.term) {
     G_.committed = mci;
@@ -396,7 +407,7 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, 
     const u32 start = *p.ipos & 0xFFFFu;
     infl_free_le(p, p.ibuf[start]);  // FreeFirstOne
   }
-  if (*p.match < G_.last) maybe_send_append(A, G_, slot, true);
+  if (*p.match < LG_LAST(A, G_)) maybe_send_append(A, G_, slot, true);
   if (A.lg.read_only != QB_READ_ONLY_SAFE || ctx == 0) return;
   // read_only.go:68-79 recvAck
   const u32 cap = A.lg.readq_cap;
@@ -470,7 +481,7 @@ __device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 in
   }
   while (maybe_send_append(A, G_, slot, false)) {
   }
-  if (slot == transferee(G_) && *p.match == G_.last)
+  if (slot == transferee(G_) && *p.match == LG_LAST(A, G_))
     emit(A, G_, QB_MSG_TIMEOUT_NOW, slot, 0, 0, 0, 0);
 }
 
@@ -517,7 +528,8 @@ __device__ void sort_run(u32* a, u32 n) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void k_ld_step(Args A) {
   __shared__ u32 lds[7];
   BlockTally<7> tally;
   const u64 G = A.lg.G;
@@ -539,11 +551,6 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
       G_.meta = A.lg.meta[g];
       G_.term = A.lg.term[g];
       G_.committed = A.lg.committed[g];
-      G_.first = A.lg.first_index[g];
-      G_.last = A.lg.last_index[g];
-      G_.snap_i = A.lg.snap_index[g];
-      G_.snap_t = A.lg.snap_term[g];
-      G_.max_ents = A.lg.max_ents[g];
       G_.nruns = (G_.meta >> 16) & 0xFu;
       G_.nmsg = 0;
       G_.stored = 0;
@@ -618,6 +625,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
 }
 
 // ------------------------------------------------------------------ L6 ----
+// Block-cooperative copy: the block's groups own one contiguous range of the
+// output; lanes copy it word by word (5 u64 per message), so the writes are
+// fully coalesced and the reads are runs of each group's staged messages.
 __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict__ moff,
                                                     const Msg* __restrict__ fix,
                                                     const u32* __restrict__ chead,
@@ -627,36 +637,47 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
                                                     u32* __restrict__ msg_off,
                                                     u64* __restrict__ msg_total,
                                                     u64* __restrict__ shards) {
-  __shared__ u32 lds[1];
-  BlockTally<1> tally;
-  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
-  u32 dropped = 0;
-  if (g < G) {
-    const u64 o = moff[g];
-    const u32 n = moff[g + 1] - moff[g];
-    if (msg_off) msg_off[g] = u32(o);
-    if (g == G - 1) {
-      if (msg_off) msg_off[G] = moff[G];
-      *msg_total = moff[G];
-    }
-    u32 chunk = n > kFix ? chead[g] : 0;
-    for (u32 k = 0; k < n; ++k) {
-      const Msg* src;
-      if (k < kFix) {
-        src = fix + g * kFix + k;
-      } else {
-        const u32 kk = k - kFix;
-        if (kk && kk % kChunk == 0) chunk = cnext[chunk];
-        src = chunks + u64(chunk) * kChunk + kk % kChunk;
-      }
-      if (o + k < cap) out[o + k] = *src;
-      else ++dropped;
-    }
+  __shared__ u32 lo[kBlock + 1];
+  const u64 g0 = u64(blockIdx.x) * kBlock;
+  const u32 ng = u32(G - g0 < kBlock ? G - g0 : kBlock);
+  for (u32 t = threadIdx.x; t <= ng; t += kBlock) lo[t] = moff[g0 + t];
+  __syncthreads();
+  if (threadIdx.x < ng && msg_off) msg_off[g0 + threadIdx.x] = lo[threadIdx.x];
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    if (msg_off) msg_off[G] = lo[ng];
+    *msg_total = lo[ng];
   }
-  for (int o2 = 32; o2 > 0; o2 >>= 1) dropped += __shfl_xor(dropped, o2, 64);
-  tally.t[0] = dropped;
-  const int slot[1] = {QB_LSTAT_MSGS_DROPPED};
-  tally.flush(lds, shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+  const u64 m0 = lo[0], m1 = lo[ng];
+  const u64 w1 = (m1 < cap ? m1 : (m0 < cap ? cap : m0)) * 5;
+  const u64* fw = reinterpret_cast<const u64*>(fix);
+  const u64* cw = reinterpret_cast<const u64*>(chunks);
+  u64* ow = reinterpret_cast<u64*>(out);
+  for (u64 w = m0 * 5 + threadIdx.x; w < w1; w += kBlock) {
+    const u64 idx = w / 5;
+    const u32 word = u32(w - idx * 5);
+    // the group owning message idx: last t with lo[t] <= idx (binary search)
+    u32 a = 0, b = ng;  // invariant lo[a] <= idx < lo[b]
+    while (b - a > 1) {
+      const u32 m = (a + b) >> 1;
+      if (lo[m] <= idx) a = m;
+      else b = m;
+    }
+    const u64 g = g0 + a;
+    const u32 k = u32(idx - lo[a]);
+    u64 v;
+    if (k < kFix) {
+      v = fw[(g * kFix + k) * 5 + word];
+    } else {
+      u32 c = chead[g];
+      for (u32 hop = (k - kFix) / kChunk; hop; --hop) c = cnext[c];
+      v = cw[(u64(c) * kChunk + (k - kFix) % kChunk) * 5 + word];
+    }
+    ow[w] = v;
+  }
+  if (threadIdx.x == 0 && m1 > cap) {
+    const u64 dropped = m1 - (m0 > cap ? m0 : cap);
+    atomicAdd(shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT + QB_LSTAT_MSGS_DROPPED, dropped);
+  }
 }
 
 __global__ void k_ld_fold(const u64* __restrict__ shards, u64* __restrict__ stats) {
@@ -746,7 +767,21 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   A.shards = shards;
   A.stepdown_at = stepdown_at;
   A.gflags = gflags;
-  hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  // Occupancy variant of the step kernel (min waves per SIMD; more waves
+  // trade register spills for latency hiding).  QB_LEADER_WAVES overrides
+  // the measured default (development knob).
+  static const int waves = [] {
+    const char* e = getenv("QB_LEADER_WAVES");
+    return e ? atoi(e) : 1;
+  }();
+  if (waves >= 8)
+    hipLaunchKernelGGL(ld::k_ld_step<8>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  else if (waves >= 6)
+    hipLaunchKernelGGL(ld::k_ld_step<6>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  else if (waves >= 5)
+    hipLaunchKernelGGL(ld::k_ld_step<5>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  else
+    hipLaunchKernelGGL(ld::k_ld_step<1>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
   QB_CHECK_LAUNCH("k_ld_step");
   scan::launch(mcnt, G, mbsum, st);
   QB_CHECK_LAUNCH("scan(messages)");

@@ -256,11 +256,13 @@ def synth_streaming(G: int, W: int = 32, D: int = 4, n: int = 5, device="cuda"):
     return lg, base
 
 
-def streaming_inbox(G: int, base: torch.Tensor, k: int, D: int = 4, n: int = 5, device="cuda"):
+def streaming_inbox(G: int, base: torch.Tensor, k: int, D: int = 4, n: int = 5, device="cuda",
+                    shuffle: bool = True):
     """Step k: one MsgAppResp per group, from follower 1 + (g + k) % 4, acking
-    the next window boundary; records shuffled (arrival order)."""
+    the next window boundary; records shuffled (arrival order) unless
+    ``shuffle`` is False (records already in group order)."""
     dev = torch.device(device)
-    g = torch.randperm(G, device=dev)
+    g = torch.randperm(G, device=dev) if shuffle else torch.arange(G, device=dev)
     f = 1 + (g + k) % (n - 1)
     idx = base[g] + (k // (n - 1) + 1) * D
     z = torch.zeros(G, dtype=torch.int64, device=dev)

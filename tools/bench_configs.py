@@ -152,13 +152,13 @@ def tracker_config(G, reps, seed=55):
                              "sample": f"{Gs} records on {Gs} groups, sequential C restatement"}})
 
 
-def leader_config(G, reps, warm=4):
+def leader_config(G, reps, warm=4, shuffle=True):
     """§8f rows 1-2: the leader inbox step (qb_dev_leader_step) on streaming
     MsgAppResp batches (one per group per step), group-steps/s."""
     from etcd_amd.quorum.leader import synth_streaming, streaming_inbox
     lg, base = synth_streaming(G, device=dev)
     steps = warm + reps
-    inboxes = [streaming_inbox(G, base, k, device=dev) for k in range(steps)]
+    inboxes = [streaming_inbox(G, base, k, device=dev, shuffle=shuffle) for k in range(steps)]
     stats = torch.zeros(8, dtype=torch.int64, device=dev)
     outs = []
     for k in range(warm):
@@ -183,6 +183,10 @@ def leader_config(G, reps, warm=4):
     # match/next/pstate/infl_pos written 21 B; messages 40 B x 3 (stored,
     # copied, written) per message; scans 16 B per group.
     algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
+    if not shuffle:
+        print(json.dumps({"config": "leader inbox step, records in group order (lab)",
+                          "per_launch_us": t * 1e6, "groups_per_s": G / t}), flush=True)
+        return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
     # stepLeader loop one record at a time) on a bounded sample of the same
     # workload, 16 threads (groups partitioned) and 1 thread.
@@ -321,6 +325,8 @@ def main():
         tracker_config(1 << 24, a.reps)
     if "leader" in which:
         leader_config(1 << 22, a.reps)
+    if "leader-sorted" in which:  # development: records already in group order
+        leader_config(1 << 22, a.reps, shuffle=False)
     if "wire" in which:
         wire_config(1 << 24, a.reps)
     if "confchange" in which:
