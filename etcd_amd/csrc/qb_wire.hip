@@ -24,7 +24,7 @@
 namespace qb {
 namespace wire {
 
-constexpr u32 kStage = 32 * 1024;  // LDS staging bytes per workgroup
+constexpr u32 kStage = 16 * 1024;  // LDS staging bytes per workgroup (~40 B x 256 messages fit)
 
 enum Kind : u32 { K_MESSAGE = 0, K_ENTRY = 1, K_SNAPSHOT = 2, K_SNAPMETA = 3, K_CONFSTATE = 4 };
 enum FieldType : u32 { T_UNKNOWN = 0, T_VARINT, T_BYTES, T_REPEATED, T_NESTED };
@@ -53,17 +53,20 @@ __device__ __forceinline__ u32 field_type(u32 kind, int fnum, u32* nested) {
   }
 }
 
-// Byte source: LDS stage or global memory, addressed by absolute offset.
-struct Src {
-  const u8* g;      // batch buffer
-  const u8* lds;    // staged span or null
-  u64 lbase, lend;  // staged range [lbase, lend)
-  __device__ __forceinline__ u8 at(u64 i) const {
-    return (lds && i >= lbase && i < lend) ? lds[i - lbase] : g[i];
-  }
+// Byte sources addressed by absolute offset: the workgroup's LDS stage (a
+// message whose bytes lie inside the staged span) or global memory.
+struct LdsSrc {
+  const u8* lds;
+  u64 base;
+  __device__ __forceinline__ u8 at(u64 i) const { return lds[i - base]; }
+};
+struct GlobalSrc {
+  const u8* g;
+  __device__ __forceinline__ u8 at(u64 i) const { return g[i]; }
 };
 
 // The generated decoders' varint loop: error at shift >= 64 or at l.
+template <class Src>
 __device__ __forceinline__ bool varint(const Src& s, u64& i, u64 l, u64& v) {
   v = 0;
   for (u32 shift = 0;; shift += 7) {
@@ -75,6 +78,7 @@ __device__ __forceinline__ bool varint(const Src& s, u64& i, u64 l, u64& v) {
 }
 
 // skipRaft on [i, l): advances i past one field (with nested groups).
+template <class Src>
 __device__ bool skip_field(const Src& s, u64& i, u64 l) {
   const u64 start = i;
   int depth = 0;
@@ -117,24 +121,13 @@ struct Fields {
   bool has_ctx;
 };
 
-// Message.Unmarshal with every nested message decoded (explicit stack; the
-// deepest nesting is Message > Snapshot > SnapshotMetadata > ConfState).
-__device__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
-  struct Frame {
-    u32 kind;
-    u64 pos, end;
-  } st[4];
-  int sp = 0;
-  st[0] = Frame{K_MESSAGE, start, end};
-  f = Fields{};
-  while (sp >= 0) {
-    Frame& fr = st[sp];
-    if (fr.pos >= fr.end) {
-      --sp;
-      continue;
-    }
-    const u64 l = fr.end;
-    u64 i = fr.pos;
+// The generated Unmarshal of one message kind on [i, l): nested bodies are
+// decoded by the nested kind's own instantiation (the nesting is fixed:
+// Message > Entry | Snapshot > SnapshotMetadata > ConfState), so everything
+// inlines into straight-line code with no private-memory frame stack.
+template <u32 KIND, class Src>
+__device__ __forceinline__ bool unmarshal(const Src& s, u64 i, const u64 l, Fields* f) {
+  while (i < l) {
     const u64 pre = i;
     u64 wire;
     if (!varint(s, i, l, wire)) return false;
@@ -143,36 +136,28 @@ __device__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
     if (wt == 4) return false;  // end group for non-group
     if (fnum <= 0) return false;  // illegal tag
     u32 nested = 0;
-    const u32 ft = field_type(fr.kind, fnum, &nested);
+    const u32 ft = field_type(KIND, fnum, &nested);
     if (ft == T_UNKNOWN) {
       i = pre;
       if (!skip_field(s, i, l)) return false;
-      fr.pos = i;
       continue;
     }
-    if (ft == T_VARINT) {
-      if (wt != 0) return false;
+    if (ft == T_VARINT || (ft == T_REPEATED && wt == 0)) {
+      if (wt != 0) return false;  // wrong wiretype
       u64 v;
       if (!varint(s, i, l, v)) return false;
-      if (fr.kind == K_MESSAGE) {
+      if constexpr (KIND == K_MESSAGE) {
         switch (fnum) {
-          case 1: f.type = v; break;
-          case 3: f.from = v; break;
-          case 4: f.term = v; break;
-          case 5: f.log_term = v; break;
-          case 6: f.index = v; break;
-          case 10: f.reject = v; break;
-          case 11: f.hint = v; break;
+          case 1: f->type = v; break;
+          case 3: f->from = v; break;
+          case 4: f->term = v; break;
+          case 5: f->log_term = v; break;
+          case 6: f->index = v; break;
+          case 10: f->reject = v; break;
+          case 11: f->hint = v; break;
           default: break;
         }
       }
-      fr.pos = i;
-      continue;
-    }
-    if (ft == T_REPEATED && wt == 0) {
-      u64 v;
-      if (!varint(s, i, l, v)) return false;
-      fr.pos = i;
       continue;
     }
     if (wt != 2) return false;  // wrong wiretype
@@ -182,25 +167,40 @@ __device__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
     const u64 post = i + len;
     if (post < i || post > l) return false;
     if (ft == T_BYTES) {
-      if (fr.kind == K_MESSAGE && fnum == 12) {
-        f.has_ctx = true;
-        f.ctx_pos = i;
-        f.ctx_len = len;
+      if constexpr (KIND == K_MESSAGE) {
+        if (fnum == 12) {
+          f->has_ctx = true;
+          f->ctx_pos = i;
+          f->ctx_len = len;
+        }
       }
-      fr.pos = post;
+      i = post;
     } else if (ft == T_REPEATED) {  // packed: each varint bounded by l, not post
       while (i < post) {
         u64 v;
         if (!varint(s, i, l, v)) return false;
       }
-      fr.pos = i;
     } else {  // nested message on [i, post)
-      fr.pos = post;
-      if (sp + 1 >= 4) return false;  // cannot happen with this schema
-      st[++sp] = Frame{nested, i, post};
+      bool ok = true;
+      if constexpr (KIND == K_MESSAGE) {
+        ok = nested == K_ENTRY ? unmarshal<K_ENTRY>(s, i, post, nullptr)
+                               : unmarshal<K_SNAPSHOT>(s, i, post, nullptr);
+      } else if constexpr (KIND == K_SNAPSHOT) {
+        ok = unmarshal<K_SNAPMETA>(s, i, post, nullptr);
+      } else if constexpr (KIND == K_SNAPMETA) {
+        ok = unmarshal<K_CONFSTATE>(s, i, post, nullptr);
+      }
+      if (!ok) return false;
+      i = post;
     }
   }
   return true;
+}
+
+template <class Src>
+__device__ __forceinline__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
+  f = Fields{};
+  return unmarshal<K_MESSAGE>(s, start, end, &f);
 }
 
 __device__ __forceinline__ int kind_of_type(u64 type32) {
@@ -228,6 +228,65 @@ struct Args {
   u64* stats;
 };
 
+// One message: decode, classify, map From to its slot, write the record.
+template <class Src>
+__device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u64 p0, u64 p1) {
+  Fields f;
+  int st_;
+  u32 group = 0xFFFFFFFFu;
+  u8 flags = 0;
+  u64 index = 0, term = 0, hint = 0, lterm = 0;
+  if (p1 < p0 || p1 > A.nbytes || !unmarshal_message(s, p0, p1, f)) {
+    st_ = QB_WIRE_UNMARSHAL;
+    if (A.mtype) A.mtype[m] = 0;
+  } else {
+    if (A.mtype) A.mtype[m] = u8(f.type);
+    const int kind = kind_of_type(f.type);
+    if (kind < 0) {
+      st_ = QB_WIRE_TYPE;
+    } else {
+      index = f.index;
+      st_ = QB_WIRE_OK;
+      if (kind == QB_IN_HEARTBEAT_RESP) {
+        index = 0;
+        if (f.has_ctx && f.ctx_len != 0) {
+          u64 v = 0;
+          if (f.ctx_len == 8)
+            for (u32 t = 0; t < 8; ++t) v = (v << 8) | s.at(f.ctx_pos + t);  // big-endian id
+          if (f.ctx_len != 8 || v == 0) st_ = QB_WIRE_CTX;
+          index = v;
+        }
+      }
+      if (st_ == QB_WIRE_OK) {
+        group = A.mgroup[m];
+        u32 slot = QB_REC_NO_PROGRESS;
+        if (group < A.G) {
+          const u32 s0 = A.off[group], s1 = A.off[group + 1];
+          for (u32 j = s0; j < s1; ++j)
+            if (A.ids[j] == f.from) {
+              slot = j - s0;
+              break;
+            }
+        }
+        flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
+        term = f.term;
+        hint = f.hint;
+        lterm = f.log_term;
+      } else {
+        index = 0;
+      }
+    }
+  }
+  A.rg[m] = group;
+  A.rf[m] = flags;
+  A.ri[m] = index;
+  A.rt[m] = term;
+  if (A.rh) A.rh[m] = hint;
+  if (A.rl) A.rl[m] = lterm;
+  A.status[m] = u8(st_);
+  return st_;
+}
+
 __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   __shared__ __attribute__((aligned(16))) u8 stage[kStage];
   __shared__ u32 lds[4];
@@ -237,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   const u64 mlast = (m0 + kBlock < A.M ? m0 + kBlock : A.M);
   // Stage the block's byte span [b0, b1) when it fits (block-uniform).
   const u64 b0 = A.moff[m0], b1 = A.moff[mlast];
-  Src s{A.bytes, nullptr, 0, 0};
+  u64 lbase = 0, lend = 0;  // staged span (empty: nothing staged)
   if (b1 > b0 && b1 - b0 <= kStage - 16) {
     const u64 a0 = b0 & ~u64(15);             // 16-byte aligned window
     const u64 a1 = (b1 + 15) & ~u64(15);
@@ -252,64 +311,17 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
           const u64 p = a0 + 16 * k + t;
           stage[16 * k + t] = p < A.nbytes ? A.bytes[p] : 0;
         }
-    s = Src{A.bytes, stage, a0, a1 < A.nbytes ? a1 : A.nbytes};
+    lbase = a0;
+    lend = a1 < A.nbytes ? a1 : A.nbytes;
   }
   __syncthreads();
   int st_ = -1;
   if (m < A.M) {
     const u64 p0 = A.moff[m], p1 = A.moff[m + 1];
-    Fields f;
-    u32 group = 0xFFFFFFFFu;
-    u8 flags = 0;
-    u64 index = 0, term = 0, hint = 0, lterm = 0;
-    if (p1 < p0 || p1 > A.nbytes || !unmarshal_message(s, p0, p1, f)) {
-      st_ = QB_WIRE_UNMARSHAL;
-      if (A.mtype) A.mtype[m] = 0;
-    } else {
-      if (A.mtype) A.mtype[m] = u8(f.type);
-      const int kind = kind_of_type(f.type);
-      if (kind < 0) {
-        st_ = QB_WIRE_TYPE;
-      } else {
-        index = f.index;
-        st_ = QB_WIRE_OK;
-        if (kind == QB_IN_HEARTBEAT_RESP) {
-          index = 0;
-          if (f.has_ctx && f.ctx_len != 0) {
-            u64 v = 0;
-            if (f.ctx_len == 8)
-              for (u32 t = 0; t < 8; ++t) v = (v << 8) | s.at(f.ctx_pos + t);  // big-endian id
-            if (f.ctx_len != 8 || v == 0) st_ = QB_WIRE_CTX;
-            index = v;
-          }
-        }
-        if (st_ == QB_WIRE_OK) {
-          group = A.mgroup[m];
-          u32 slot = QB_REC_NO_PROGRESS;
-          if (group < A.G) {
-            const u32 s0 = A.off[group], s1 = A.off[group + 1];
-            for (u32 j = s0; j < s1; ++j)
-              if (A.ids[j] == f.from) {
-                slot = j - s0;
-                break;
-              }
-          }
-          flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
-          term = f.term;
-          hint = f.hint;
-          lterm = f.log_term;
-        } else {
-          index = 0;
-        }
-      }
-    }
-    A.rg[m] = group;
-    A.rf[m] = flags;
-    A.ri[m] = index;
-    A.rt[m] = term;
-    if (A.rh) A.rh[m] = hint;
-    if (A.rl) A.rl[m] = lterm;
-    A.status[m] = u8(st_);
+    if (p0 >= lbase && p1 <= lend && p0 <= p1)
+      st_ = ingest_one(A, LdsSrc{stage, lbase}, m, p0, p1);
+    else
+      st_ = ingest_one(A, GlobalSrc{A.bytes}, m, p0, p1);
   }
   tally.add(0, st_ == QB_WIRE_OK);
   tally.add(1, st_ == QB_WIRE_UNMARSHAL);
