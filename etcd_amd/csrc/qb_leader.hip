@@ -220,73 +220,76 @@ __device__ void emit(const Args& A, Group& G_, u8 type, u32 to, u64 index, u64 l
 }
 
 // Progress accessors (slot j of the group).
+// A slot's Progress: the kernel arguments (uniform, scalar registers) and the
+// slot's index; addresses are formed at each use, so a live Pr costs two
+// vector registers instead of seven 64-bit pointers.
 struct Pr {
-  u64* match;
-  u64* next;
-  u64* psnap;
-  u8* st;
-  u32* ipos;
-  u64* ibuf;
-  u32 K;
+  const Args* A;
+  u64 p;
+  __device__ __forceinline__ u64& match() const { return U(A->lg.match)[p]; }
+  __device__ __forceinline__ u64& next() const { return U(A->lg.next)[p]; }
+  __device__ __forceinline__ u64& psnap() const { return U(A->lg.pending_snapshot)[p]; }
+  __device__ __forceinline__ u8& st() const { return A->lg.pstate[p]; }
+  __device__ __forceinline__ u32& ipos() const { return A->lg.infl_pos[p]; }
+  __device__ __forceinline__ u64* ibuf() const { return U(A->lg.infl_buf) + p * A->lg.inflight_cap; }
+  __device__ __forceinline__ u32 K() const { return A->lg.inflight_cap; }
 };
 __device__ __forceinline__ Pr pr_of(const Args& A, const Group& G_, u32 j) {
-  const u64 p = u64(G_.s0) + j;
-  return Pr{U(A.lg.match) + p, U(A.lg.next) + p, U(A.lg.pending_snapshot) + p, A.lg.pstate + p,
-            A.lg.infl_pos + p, U(A.lg.infl_buf) + p * A.lg.inflight_cap, A.lg.inflight_cap};
+  return Pr{&A, u64(G_.s0) + j};
 }
 __device__ __forceinline__ u32 st_state(u8 s) { return s & 3u; }
 
 // inflights.go
-__device__ __forceinline__ bool infl_full(const Pr& p) { return (*p.ipos >> 16) == p.K; }
-__device__ __forceinline__ void infl_reset(const Pr& p) { *p.ipos = 0; }
+__device__ __forceinline__ bool infl_full(const Pr& p) { return (p.ipos() >> 16) == p.K(); }
+__device__ __forceinline__ void infl_reset(const Pr& p) { p.ipos() = 0; }
 __device__ void infl_add(const Pr& p, u64 v) {
-  const u32 pos = *p.ipos;
+  const u32 pos = p.ipos();
   const u32 start = pos & 0xFFFFu, count = pos >> 16;
   u32 nxt = start + count;
-  if (nxt >= p.K) nxt -= p.K;
-  p.ibuf[nxt] = v;
-  *p.ipos = start | ((count + 1) << 16);
+  if (nxt >= p.K()) nxt -= p.K();
+  p.ibuf()[nxt] = v;
+  p.ipos() = start | ((count + 1) << 16);
 }
 __device__ void infl_free_le(const Pr& p, u64 to) {
-  const u32 pos = *p.ipos;
+  const u32 pos = p.ipos();
   const u32 start = pos & 0xFFFFu, count = pos >> 16;
-  if (count == 0 || to < p.ibuf[start]) return;
+  if (count == 0 || to < p.ibuf()[start]) return;
   u32 idx = start, i = 0;
   for (; i < count; ++i) {
-    if (to < p.ibuf[idx]) break;
-    if (++idx >= p.K) idx -= p.K;
+    if (to < p.ibuf()[idx]) break;
+    if (++idx >= p.K()) idx -= p.K();
   }
   const u32 c2 = count - i;
-  *p.ipos = c2 == 0 ? 0u : (idx | (c2 << 16));
+  p.ipos() = c2 == 0 ? 0u : (idx | (c2 << 16));
 }
 
 // progress.go
 __device__ __forceinline__ void reset_state(const Pr& p, u32 state) {
-  *p.st = u8((*p.st & QB_PR_RECENT_ACTIVE) | state);  // ProbeSent = false
-  *p.psnap = 0;
+  p.st() = u8((p.st() & QB_PR_RECENT_ACTIVE) | state);  // ProbeSent = false
+  p.psnap() = 0;
   infl_reset(p);
 }
 __device__ void become_probe(const Pr& p) {
-  const u64 m1 = *p.match + 1;
-  if (st_state(*p.st) == QB_PR_SNAPSHOT) {
-    const u64 ps1 = *p.psnap + 1;
+  const u64 m1 = p.match() + 1;
+  if (st_state(p.st()) == QB_PR_SNAPSHOT) {
+    const u64 ps1 = p.psnap() + 1;
     reset_state(p, QB_PR_PROBE);
-    *p.next = m1 > ps1 ? m1 : ps1;
+    p.next() = m1 > ps1 ? m1 : ps1;
   } else {
     reset_state(p, QB_PR_PROBE);
-    *p.next = m1;
+    p.next() = m1;
   }
 }
 __device__ __forceinline__ void become_replicate(const Pr& p) {
   reset_state(p, QB_PR_REPLICATE);
-  *p.next = *p.match + 1;
+  p.next() = p.match() + 1;
 }
 __device__ __forceinline__ void become_snapshot(const Pr& p, u64 snapi) {
   reset_state(p, QB_PR_SNAPSHOT);
-  *p.psnap = snapi;
+  p.psnap() = snapi;
 }
 __device__ __forceinline__ bool is_paused(const Pr& p) {
-  const u8 s = *p.st;
+  const u8 s = p.st();
   switch (st_state(s)) {
     case QB_PR_PROBE: return (s & QB_PR_PROBE_SENT) != 0;
     case QB_PR_REPLICATE: return infl_full(p);
@@ -295,26 +298,26 @@ __device__ __forceinline__ bool is_paused(const Pr& p) {
 }
 __device__ bool maybe_update(const Pr& p, u64 n) {
   bool updated = false;
-  if (*p.match < n) {
-    *p.match = n;
+  if (p.match() < n) {
+    p.match() = n;
     updated = true;
-    *p.st = u8(*p.st & ~QB_PR_PROBE_SENT);
+    p.st() = u8(p.st() & ~QB_PR_PROBE_SENT);
   }
   const u64 n1 = n + 1;
-  if (*p.next < n1) *p.next = n1;
+  if (p.next() < n1) p.next() = n1;
   return updated;
 }
 __device__ bool maybe_decr_to(const Pr& p, u64 rejected, u64 hint) {
-  if (st_state(*p.st) == QB_PR_REPLICATE) {
-    if (rejected <= *p.match) return false;
-    *p.next = *p.match + 1;
+  if (st_state(p.st()) == QB_PR_REPLICATE) {
+    if (rejected <= p.match()) return false;
+    p.next() = p.match() + 1;
     return true;
   }
-  if (*p.next - 1 != rejected) return false;
+  if (p.next() - 1 != rejected) return false;
   const u64 h1 = hint + 1;
   const u64 mn = rejected < h1 ? rejected : h1;
-  *p.next = mn > 1 ? mn : 1;
-  *p.st = u8(*p.st & ~QB_PR_PROBE_SENT);
+  p.next() = mn > 1 ? mn : 1;
+  p.st() = u8(p.st() & ~QB_PR_PROBE_SENT);
   return true;
 }
 
@@ -322,7 +325,7 @@ __device__ bool maybe_decr_to(const Pr& p, u64 rejected, u64 hint) {
 __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if_empty) {
   const Pr p = pr_of(A, G_, to);
   if (is_paused(p)) return false;
-  const u64 nx = *p.next;
+  const u64 nx = p.next();
   const u64 term = log_term(A, G_, nx - 1);
   u64 n = 0;
   bool compacted = false;
@@ -335,7 +338,7 @@ __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if
   }
   if (n == 0 && !send_if_empty) return false;
   if (compacted) {
-    if (!(*p.st & QB_PR_RECENT_ACTIVE)) return false;
+    if (!(p.st() & QB_PR_RECENT_ACTIVE)) return false;
     if (LG_SNAP_I(A, G_) == 0) return false;  // ErrSnapshotTemporarilyUnavailable
     emit(A, G_, QB_MSG_SNAP, to, LG_SNAP_I(A, G_), LG_SNAP_T(A, G_), 0, 0);
     become_snapshot(p, LG_SNAP_I(A, G_));
@@ -343,13 +346,13 @@ __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if
   }
   emit(A, G_, QB_MSG_APP, to, nx - 1, term, G_.committed, n);
   if (n != 0) {
-    const u32 s = st_state(*p.st);
+    const u32 s = st_state(p.st());
     if (s == QB_PR_REPLICATE) {
       const u64 last = nx + n - 1;
-      *p.next = last + 1;
+      p.next() = last + 1;
       infl_add(p, last);
     } else if (s == QB_PR_PROBE) {
-      *p.st = u8(*p.st | QB_PR_PROBE_SENT);
+      p.st() = u8(p.st() | QB_PR_PROBE_SENT);
     }
   }
   return true;
@@ -402,12 +405,12 @@ __device__ __forceinline__ u8 acks_vote(const Group& G_, u32 acks) {
 }
 
 __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 ctx) {
-  *p.st = u8((*p.st | QB_PR_RECENT_ACTIVE) & ~QB_PR_PROBE_SENT);
-  if (st_state(*p.st) == QB_PR_REPLICATE && infl_full(p)) {
-    const u32 start = *p.ipos & 0xFFFFu;
-    infl_free_le(p, p.ibuf[start]);  // FreeFirstOne
+  p.st() = u8((p.st() | QB_PR_RECENT_ACTIVE) & ~QB_PR_PROBE_SENT);
+  if (st_state(p.st()) == QB_PR_REPLICATE && infl_full(p)) {
+    const u32 start = p.ipos() & 0xFFFFu;
+    infl_free_le(p, p.ibuf()[start]);  // FreeFirstOne
   }
-  if (*p.match < LG_LAST(A, G_)) maybe_send_append(A, G_, slot, true);
+  if (p.match() < LG_LAST(A, G_)) maybe_send_append(A, G_, slot, true);
   if (A.lg.read_only != QB_READ_ONLY_SAFE || ctx == 0) return;
   // read_only.go:68-79 recvAck
   const u32 cap = A.lg.readq_cap;
@@ -447,22 +450,22 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, 
 
 __device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 index, bool reject,
                          u64 hint, u64 hint_term, u8& gfl) {
-  *p.st = u8(*p.st | QB_PR_RECENT_ACTIVE);
+  p.st() = u8(p.st() | QB_PR_RECENT_ACTIVE);
   if (reject) {
     u64 next_probe = hint;
     if (hint_term > 0) next_probe = find_conflict_by_term(A, G_, hint, hint_term);
     if (maybe_decr_to(p, index, next_probe)) {
-      if (st_state(*p.st) == QB_PR_REPLICATE) become_probe(p);
+      if (st_state(p.st()) == QB_PR_REPLICATE) become_probe(p);
       maybe_send_append(A, G_, slot, true);
     }
     return;
   }
   const bool old_paused = is_paused(p);
   if (!maybe_update(p, index)) return;
-  const u32 s = st_state(*p.st);
+  const u32 s = st_state(p.st());
   if (s == QB_PR_PROBE) {
     become_replicate(p);
-  } else if (s == QB_PR_SNAPSHOT && *p.match >= *p.psnap) {
+  } else if (s == QB_PR_SNAPSHOT && p.match() >= p.psnap()) {
     become_probe(p);
     become_replicate(p);
   } else if (s == QB_PR_REPLICATE) {
@@ -481,15 +484,15 @@ __device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 in
   }
   while (maybe_send_append(A, G_, slot, false)) {
   }
-  if (slot == transferee(G_) && *p.match == LG_LAST(A, G_))
+  if (slot == transferee(G_) && p.match() == LG_LAST(A, G_))
     emit(A, G_, QB_MSG_TIMEOUT_NOW, slot, 0, 0, 0, 0);
 }
 
 __device__ void snap_status(const Pr& p, bool reject) {
-  if (st_state(*p.st) != QB_PR_SNAPSHOT) return;
-  if (reject) *p.psnap = 0;
+  if (st_state(p.st()) != QB_PR_SNAPSHOT) return;
+  if (reject) p.psnap() = 0;
   become_probe(p);
-  *p.st = u8(*p.st | QB_PR_PROBE_SENT);
+  p.st() = u8(p.st() | QB_PR_PROBE_SENT);
 }
 
 // Sort a group's run of batch indexes ascending (runs are short: insertion
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_ld_step(Args A) {
           heartbeat_resp(A, G_, slot, p, A.in.index[i]);
         } else if (kind == QB_IN_SNAP_STATUS) {
           snap_status(p, reject);
-        } else if (st_state(*p.st) == QB_PR_REPLICATE) {  // MsgUnreachable
+        } else if (st_state(p.st()) == QB_PR_REPLICATE) {  // MsgUnreachable
           become_probe(p);
         }
       }
