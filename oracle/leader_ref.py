@@ -315,6 +315,26 @@ class LeaderGroup:
         self.advanced = False
         self.released_pending = False
 
+    def progress_string(self, slot: int) -> str:
+        """Progress.String (tracker/progress.go:214-238); a slot in neither
+        voter mask is a learner."""
+        pr = self.prs[slot]
+        out = f"{STATE_NAMES[pr.state]} match={pr.match} next={pr.next}"
+        if not (((self.mask_in | self.mask_out) >> slot) & 1):
+            out += " learner"
+        if pr.is_paused():
+            out += " paused"
+        if pr.pending_snapshot > 0:
+            out += f" pendingSnap={pr.pending_snapshot}"
+        if not pr.recent_active:
+            out += " inactive"
+        n = pr.inflights.count
+        if n > 0:
+            out += f" inflight={n}"
+            if pr.inflights.full():
+                out += "[full]"
+        return out
+
     # ----------------------------------------------------------- quorum ---
     def _voters(self, mask):
         return [s for s in range(self.n_slots) if (mask >> s) & 1]

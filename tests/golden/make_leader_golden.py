@@ -181,6 +181,96 @@ def scenarios():
     return out
 
 
+def batch(msgs, expect_msgs=None, **exp):
+    """One inbound batch (an interaction test's '> 1 receiving messages' block)
+    and the leader's outbound messages in its next Ready (exactly, in order)."""
+    e = dict(exp)
+    if expect_msgs is not None:
+        e["msgs_exact"] = expect_msgs
+    return {"op": "recv_batch", "msgs": msgs, "expect": e}
+
+
+def app(slot, index, term, reject=False, hint=0, log_term=0):
+    return {"kind": APP, "slot": slot, "term": term, "index": index, "reject": reject,
+            "hint": hint, "log_term": log_term}
+
+
+def hb(slot, term, ctx=0):
+    return {"kind": HB, "slot": slot, "term": term, "index": ctx, "reject": False, "hint": 0,
+            "log_term": 0}
+
+
+def mapp(to, index, log_term, commit, n):
+    return [MSG_APP, to, index, log_term, commit, n]
+
+
+def interaction_scenarios():
+    """Leader side of the reference's interaction tests (raft/testdata/*.txt,
+    run by raft/interaction_test.go:24-34 through rafttest's InteractionEnv):
+    every '> 1 receiving messages' block is one batch, the following
+    '> 1 handling Ready' block's Messages (or none) its expected output; the
+    'status 1' blocks are Progress.String() of every peer.  Node i is slot
+    i-1.  The env's raft.Config (rafttest/interaction_env.go:90-99) has
+    MaxSizePerMsg = MaxUint64 and MaxInflightMsgs = MaxInt32 (never full)."""
+    out = []
+    # probe_and_replicate.txt:470-767: n1 became leader at term 8 over the
+    # Figure-7 log (shifted by 10: snapshot index 10 term 1, entries 11..20 of
+    # terms 1 1 1 4 4 5 5 6 6 6, its empty entry 21 at term 8), commit 18, and
+    # probed every peer at Log:6/20 (all Probe, Next 21, ProbeSent).
+    sc = {"name": "interaction/probe_and_replicate", "cite": "raft/testdata/probe_and_replicate.txt:470-767",
+          "slots": 7, "mask_in": 0x7F, "mask_out": 0, "term": 8, "leader": 0, "transferee": 255,
+          "read_only": 0, "infl_size": 16,
+          "log": {"first": 11, "last": 21, "committed": 18,
+                  "runs": [[10, 1], [14, 4], [16, 5], [18, 6], [21, 8]],
+                  "snap_index": 10, "snap_term": 1, "max_ents": UNLIMITED},
+          "progress": [pr(21, 22, state=R)] + [pr(0, 21, probe_sent=True) for _ in range(6)],
+          "readq": [], "ops": []}
+    ops = sc["ops"]
+    for node, (hint_term, hint), (lt, idx, n) in (
+            (2, (6, 19), (6, 19, 2)), (3, (4, 14), (4, 14, 7))):
+        s_ = node - 1
+        ops.append(batch([app(s_, 20, 8, True, hint, hint_term)], [mapp(s_, idx, lt, 18, n)]))
+        ops.append(batch([app(s_, 21, 8)], [mapp(s_, 21, 8, 18, 0)]))
+        ops.append(batch([app(s_, 21, 8)], []))
+    ops.append(batch([app(3, 21, 8)], [mapp(1, 21, 8, 21, 0), mapp(2, 21, 8, 21, 0),
+                                       mapp(3, 21, 8, 21, 0)], committed=21))
+    ops.append(batch([app(3, 21, 8)], []))
+    for node, (hint_term, hint), (lt, idx, n) in (
+            (5, (6, 18), (6, 18, 3)), (6, (4, 17), (4, 15, 6)), (7, (3, 20), (1, 13, 8))):
+        s_ = node - 1
+        ops.append(batch([app(s_, 20, 8, True, hint, hint_term)], [mapp(s_, idx, lt, 21, n)]))
+        ops.append(batch([app(s_, 21, 8)], [mapp(s_, 21, 8, 21, 0)]))
+        ops.append(batch([app(s_, 21, 8)], []))
+    out.append(sc)
+
+    # snapshot_succeed_via_app_resp.txt: n1 leads at term 1 over voters 1-3
+    # with everything up to 11 replicated to n2 and compacted away
+    # (firstIndex 12, snapshot index 11 term 1); n3 never answered.
+    sc = {"name": "interaction/snapshot_succeed_via_app_resp",
+          "cite": "raft/testdata/snapshot_succeed_via_app_resp.txt:36-125",
+          "slots": 3, "mask_in": 0x7, "mask_out": 0, "term": 1, "leader": 0, "transferee": 255,
+          "read_only": 0, "infl_size": 16,
+          "log": {"first": 12, "last": 11, "committed": 11, "runs": [[11, 1]],
+                  "snap_index": 11, "snap_term": 1, "max_ents": UNLIMITED},
+          "progress": [pr(11, 12, state=R), pr(11, 12, state=R, recent_active=True),
+                       pr(0, 11, probe_sent=True)],
+          "readq": [], "ops": []}
+    sc["ops"].append(batch([], [], status=["StateReplicate match=11 next=12 inactive",
+                                           "StateReplicate match=11 next=12",
+                                           "StateProbe match=0 next=11 paused inactive"]))
+    sc["ops"].append(batch([hb(2, 1)], [[MSG_SNAP, 2, 11, 1, 0, 0]],
+                           status=["StateReplicate match=11 next=12 inactive",
+                                   "StateReplicate match=11 next=12",
+                                   "StateSnapshot match=0 next=11 paused pendingSnap=11"]))
+    sc["ops"].append(batch([app(2, 11, 1)], [mapp(2, 11, 1, 11, 0)],
+                           status=["StateReplicate match=11 next=12 inactive",
+                                   "StateReplicate match=11 next=12",
+                                   "StateReplicate match=11 next=12"]))
+    sc["ops"].append(batch([hb(1, 1), app(2, 11, 1)], []))
+    out.append(sc)
+    return out
+
+
 def progress_tables():
     return {
         # tracker/progress_test.go:40-66
@@ -226,7 +316,7 @@ def inflight_tables():
 
 
 def main():
-    doc = {"scenarios": scenarios(), "progress": progress_tables(),
+    doc = {"scenarios": scenarios() + interaction_scenarios(), "progress": progress_tables(),
            "inflights": inflight_tables()}
     with open(os.path.join(HERE, "leader_tables.json"), "w", encoding="utf-8") as f:
         json.dump(doc, f, indent=1)

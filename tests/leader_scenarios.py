@@ -37,6 +37,7 @@ def build_group(sc) -> L.LeaderGroup:
 
 
 def inbound(op) -> L.Inbound:
+    """One inbound record of a scenario ('recv' op or a 'recv_batch' entry)."""
     return L.Inbound(kind=op["kind"], slot=op["slot"], term=op["term"], index=op["index"],
                      reject=op["reject"], hint=op["hint"], log_term=op["log_term"])
 
@@ -61,6 +62,12 @@ def check_expect(where, exp, msgs, group: L.LeaderGroup):
             assert getattr(p, k) == v, f"{where}: progress[{slot}].{k}={getattr(p, k)}, want {v}"
     if "committed" in exp:
         assert group.log.committed == exp["committed"], f"{where}: committed {group.log.committed}"
+    if "msgs_exact" in exp:
+        got = [[m[k] for k in MSG_FIELDS] for m in msgs]
+        assert got == exp["msgs_exact"], f"{where}: msgs {got}, want {exp['msgs_exact']}"
+    if "status" in exp:
+        got = [group.progress_string(s) for s in range(group.n_slots)]
+        assert got == exp["status"], f"{where}: status {got}, want {exp['status']}"
     if "readq_len" in exp:
         assert len(group.readq) == exp["readq_len"], f"{where}: readq {group.readq}"
 
@@ -76,6 +83,9 @@ def run_scenario_oracle(sc):
         g.msgs = []
         if op["op"] == "recv":
             g.step(inbound(op), k)
+        elif op["op"] == "recv_batch":
+            for j, m in enumerate(op["msgs"]):
+                g.step(inbound(m), j)
         else:
             g.propose(op["n"])
         check_expect(f"{sc['name']} op{k}", op["expect"], [msg_dict(m) for m in g.msgs], g)

@@ -47,3 +47,33 @@ def test_restore_round_trip():
         assert (t.learners or set()) == set(learners)
         assert (t.learners_next or set()) == set(lnext)
         assert t.auto_leave == auto
+
+
+def _quick_inputs(r):
+    """confchange/quick_test.go:146-191 generators: setup = AddNode(1) + 1..5
+    AddNode of IDs 1..5; changes = 1..9 of any type on IDs 2..10."""
+    setup = [(CC.ADD_NODE, 1)] + [(CC.ADD_NODE, 1 + r.randrange(5))
+                                  for _ in range(1 + r.randrange(5))]
+    ccs = [(r.randrange(4), 2 + r.randrange(9)) for _ in range(1 + r.randrange(9))]
+    return setup, ccs
+
+
+def _simple_chain(t, ccs):
+    for cc in ccs:
+        t = CC.Changer(t, 10).simple([cc])
+    return t
+
+
+def test_quick_simple_equals_joint():
+    """confchange/quick_test.go:30-144: applying changes one Simple at a time
+    equals EnterJoint(ccs) + LeaveJoint (autoLeave either way)."""
+    r = random.Random(5)
+    for _ in range(2000):
+        setup, ccs = _quick_inputs(r)
+        base = _simple_chain(CC.Tracker.empty(10), setup)
+        t1 = _simple_chain(base, ccs)
+        for al in (False, True):
+            j = CC.Changer(base, 10).enter_joint(al, ccs)
+            t2 = CC.Changer(j, 10).leave_joint()
+            assert t1.config_string() == t2.config_string()
+            assert t1.progress_string() == t2.progress_string()

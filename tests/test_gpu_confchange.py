@@ -134,3 +134,31 @@ def test_restore_batch():
         want = CC.restore(CC.Tracker.empty(5), 10, cs["voters"], cs["learners"],
                           cs["voters_outgoing"], cs["learners_next"], cs["auto_leave"])
         assert _render(dev[g]) == _render(want), g
+
+
+def test_quick_simple_equals_joint_on_device():
+    """confchange/quick_test.go:30-144 batch-wide: every group's changes applied
+    as a chain of Simple calls and as EnterJoint + LeaveJoint give the same
+    config and Progress on the device (and match the oracle)."""
+    from tests.test_confchange_oracle import _quick_inputs, _simple_chain
+    r = random.Random(9)
+    G = 1500
+    inputs = [_quick_inputs(r) for _ in range(G)]
+    base = [_simple_chain(CC.Tracker.empty(10), s) for s, _ in inputs]
+    t1 = _table(base)
+    steps = max(len(c) for _, c in inputs)
+    for k in range(steps):
+        op = [1 if k < len(c) else 0 for _, c in inputs]
+        ccs = [[c[k]] if k < len(c) else [] for _, c in inputs]
+        t1, err, _ = t1.change(op, ccs, [10] * G)
+        assert not err.any()
+    for al_op in (2, 3):
+        j, err, _ = _table(base).change([al_op] * G, [c for _, c in inputs], [10] * G)
+        assert not err.any()
+        t2, err, _ = j.change([4] * G, [[] for _ in range(G)], [10] * G)
+        assert not err.any()
+        a, b = CP.unpack(t1.numpy(), 10), CP.unpack(t2.numpy(), 10)
+        for g in range(G):
+            assert _render(a[g]) == _render(b[g]), g
+    want = [_render(_simple_chain(base[g], inputs[g][1])) for g in range(G)]
+    assert [_render(x) for x in CP.unpack(t1.numpy(), 10)] == want

@@ -54,11 +54,13 @@ def test_reference_scenarios_on_device(sc):
             g.propose(op["n"])
             LS.check_expect(where, op["expect"], [LS.msg_dict(m) for m in g.msgs], g)
             continue
-        twin = copy.deepcopy(g)  # the oracle's run of the same record
+        batch = [LS.inbound(m) for m in op["msgs"]] if op["op"] == "recv_batch" else [LS.inbound(op)]
+        twin = copy.deepcopy(g)  # the oracle's run of the same records
         twin.msgs = []
-        twin.step(LS.inbound(op), 0)
+        for j, m in enumerate(batch):
+            twin.step(m, j)
         eng = _engine([g], cap, max(1, len(g.readq)))
-        res = eng.step(_inbox([(0, LS.inbound(op))]))
+        res = eng.step(_inbox([(0, m) for m in batch]))
         LP.unpack_into([g], eng.numpy(), cap, max(1, len(g.readq)))
         msgs = [dict(zip(LS.MSG_FIELDS, m[1:])) for m in _dev_msgs(res)]
         LS.check_expect(where, op["expect"], msgs, g)
