@@ -330,13 +330,22 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
   const u64 g0 = u64(blockIdx.x) * kBlock;
   const u64 g = g0 + threadIdx.x;
   const bool live = g < G;
+  // Every independent load is issued up front (cfg, votes, this group's
+  // offsets) so their latencies overlap the staging round trip instead of
+  // following it.
   const u32 c = live ? ld_nt(cfg + g) : 0u;
+  const u32 w = (VOTE && live) ? ld_nt(votes + g) : 0u;
   const u32 min_ = c & 0xFFFFu, mout = c >> 16;
 
   if constexpr (CI) {
     constexpr u32 kCap = kBlock * WMAX + 2;  // +2: 16-byte head alignment
     __shared__ __attribute__((aligned(16))) u64 lds[kCap];
     const u64 gend = (g0 + kBlock < G) ? g0 + kBlock : G;
+    u32 a = 0, b = 0;
+    if (live) {
+      a = off[g];
+      b = off[g + 1];
+    }
     const u32 base = off[g0], end = off[gend], total = off[G];
     const u32 abase = base & ~1u;
     // A table that breaks its max_slots bound must not write past the LDS run
@@ -354,7 +363,6 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
     }
     u32 lo = 0, s = 0;
     if (live) {
-      const u32 a = off[g], b = off[g + 1];
       lo = a - abase;
       s = b - a;
       s = s > WMAX ? WMAX : s;
@@ -366,7 +374,6 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
   }
   if constexpr (VOTE) {
     if (live) {
-      const u32 w = ld_nt(votes + g);
       const u32 vd = w & 0xFFFFu, gr = (w >> 16) & vd;
       const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & gr), __popc(min_ & vd));
       const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & gr), __popc(mout & vd));
