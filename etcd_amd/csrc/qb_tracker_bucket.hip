@@ -395,16 +395,31 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
     u64* __restrict__ shards) {
   constexpr u32 CH = chunk_groups(N);
+  constexpr u32 GPT = CH / kBlock;  // groups per thread in the commit phase
   __shared__ u32 tl[5];
-  BlockTally<5> tally;
+  BlockTally<7> tally;  // 5, 6: the fused pass's applied / rejected
   __shared__ u64 acc_m[N * CH];
   __shared__ u64 acc_n[NEXT ? N * CH : 1];
   __shared__ u64 gterm[CH];
   __shared__ u32 first_hi[CH];
   __shared__ u32 act[CH];
+  __shared__ u32 any_higher;
   const u32 c = blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
+  // The commit phase's loads (match rows, committed, term_start) are issued
+  // now, so their latency overlaps the record pass instead of following it.
+  u64 v[GPT][N], cm[GPT], ts[GPT];
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * kBlock;
+    const u64 g = g0 + lg;
+    const bool live = lg < ng;
+#pragma unroll
+    for (int s = 0; s < N; ++s) v[k][s] = live ? match[u64(s) * geo.G + g] : 0ull;
+    cm[k] = live ? committed[g] : 0ull;
+    ts[k] = live ? term_start[g] : 0ull;
+  }
   for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
     acc_m[k] = 0;
     if constexpr (NEXT) acc_n[k] = 0;
@@ -414,94 +429,129 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     first_hi[k] = 0xFFFFFFFFu;
     act[k] = 0;
   }
+  if (threadIdx.x == 0) any_higher = 0;
   // This chunk's records: one short run per part of its super-bucket,
   // flattened into one index space (RunTable) so every thread has a record
   // in flight at once.
   const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
   __shared__ RunTable rt;
-  // Pass 1: term filter; the first higher-term record of a group (batch
-  // order) makes the sequential leader step down (raft.go:875-879).
+  // Fused pass: the term filter and, optimistically (no step-down in the
+  // chunk, the common case), MaybeUpdate as LDS atomic max and RecentActive.
+  // A higher-term record makes the sequential leader step down and ignore
+  // everything after it (raft.go:875-879): then the updates are redone
+  // below with the step-down order known.
   for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);
     for (u32 f0 = 0; f0 < total; f0 += kBlock) {
       const u32 f = f0 + threadIdx.x;
-      bool stale = false, higher = false;
+      bool stale = false, higher = false, applied = false, rejected = false;
       if (f < total) {
         const u32 i = rt.locate(f);
         const u64 mr = recs.mr[i], term = recs.term[i];
-        const u32 lg = u32(mr) & 1023u;
+        const u32 meta = u32(mr), lg = meta & 1023u, s = (meta >> 17) & 15u;
         const u64 gt = gterm[lg];
         stale = term < gt;
         higher = term > gt;
-        if (higher) atomicMin(&first_hi[lg], u32(mr >> 32));
-      }
-      tally.add(0, stale);
-      tally.add(1, higher);
-    }
-  }
-  __syncthreads();
-  // Pass 2: MaybeUpdate (max is commutative: any order = batch order) and
-  // RecentActive, for same-term records before the group's step-down.
-  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
-    const u32 total = rt.build(cs, pb, p1, cl);
-    for (u32 f0 = 0; f0 < total; f0 += kBlock) {
-      const u32 f = f0 + threadIdx.x;
-      bool applied = false, rejected = false, after = false;
-      if (f < total) {
-        const u32 i = rt.locate(f);
-        const u64 mr = recs.mr[i];
-        const u32 meta = u32(mr), ridx = u32(mr >> 32);
-        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
-        if (recs.term[i] == gterm[lg]) {
-          if (ridx > first_hi[lg]) {
-            after = true;
+        if (higher) {
+          atomicMin(&first_hi[lg], u32(mr >> 32));
+          any_higher = 1;
+        } else if (!stale) {
+          atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+          if (meta & (1u << 21)) {
+            rejected = true;                              // raft.go:1109: not MaybeUpdate
           } else {
-            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-            if (meta & (1u << 21)) {
-              rejected = true;                              // raft.go:1109: not MaybeUpdate
-            } else {
-              applied = true;
-              const u64 idx = recs.index[i];
-              atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
-              if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
-            }
+            applied = true;
+            const u64 idx = recs.index[i];
+            atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
+            if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
           }
         }
       }
-      tally.add(2, applied);
-      tally.add(3, rejected);
-      tally.add(4, after);
+      tally.add(0, stale);
+      tally.add(1, higher);
+      tally.add(5, applied);
+      tally.add(6, rejected);
     }
   }
   __syncthreads();
+  if (any_higher) {  // block-uniform: redo the updates in step-down order
+    for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
+      acc_m[k] = 0;
+      if constexpr (NEXT) acc_n[k] = 0;
+    }
+    for (u32 k = threadIdx.x; k < CH; k += kBlock) act[k] = 0;
+    __syncthreads();
+    for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
+      const u32 total = rt.build(cs, pb, p1, cl);
+      for (u32 f0 = 0; f0 < total; f0 += kBlock) {
+        const u32 f = f0 + threadIdx.x;
+        bool applied = false, rejected = false, after = false;
+        if (f < total) {
+          const u32 i = rt.locate(f);
+          const u64 mr = recs.mr[i];
+          const u32 meta = u32(mr), ridx = u32(mr >> 32);
+          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+          if (recs.term[i] == gterm[lg]) {
+            if (ridx > first_hi[lg]) {
+              after = true;
+            } else {
+              atomicOr(&act[lg], 1u << s);
+              if (meta & (1u << 21)) {
+                rejected = true;
+              } else {
+                applied = true;
+                const u64 idx = recs.index[i];
+                atomicMax(&acc_m[s * CH + lg], idx);
+                if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);
+              }
+            }
+          }
+        }
+        tally.add(2, applied);
+        tally.add(3, rejected);
+        tally.add(4, after);
+      }
+    }
+    __syncthreads();
+  } else {
+    tally.t[2] = tally.t[5];
+    tally.t[3] = tally.t[6];
+  }
   // maybeCommit for every group of the chunk + write-back (coalesced rows).
-  for (u32 lg = threadIdx.x; lg < ng; lg += kBlock) {
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * kBlock;
+    if (lg >= ng) continue;
     const u64 g = g0 + lg;
-    u64 v[N];
 #pragma unroll
     for (int s = 0; s < N; ++s) {
-      u64* p = match + u64(s) * geo.G + g;
-      const u64 old = *p, a = acc_m[s * CH + lg];
-      v[s] = a > old ? a : old;
-      if (a > old) *p = a;
+      const u64 a = acc_m[s * CH + lg];
+      if (a > v[k][s]) {
+        v[k][s] = a;
+        match[u64(s) * geo.G + g] = a;
+      }
       if constexpr (NEXT) {
         u64* q = next + u64(s) * geo.G + g;
         const u64 nn = acc_n[s * CH + lg];
         if (nn > *q) *q = nn;
       }
     }
-    const u64 ci = select_quorum<N>(v);
-    const u64 cm = committed[g];
-    const bool adv = ci > cm && ci >= term_start[g];  // log.go:328-334
+    const u64 ci = select_quorum<N>(v[k]);
+    const bool adv = ci > cm[k] && ci >= ts[k];  // log.go:328-334
     if (adv) committed[g] = ci;
     if (advanced) advanced[g] = adv ? 1 : 0;
     stepdown_at[g] = first_hi[lg];
     if (act[lg]) active[g] = u16(active[g] | act[lg]);
   }
-  const int slot[5] = {QB_STAT_STALE_TERM, QB_STAT_HIGHER_TERM, QB_STAT_APPLIED,
-                       QB_STAT_REJECTED, QB_STAT_AFTER_STEPDOWN};
-  tally.flush(tl, shard_of(shards), slot);
+  __shared__ u32 tl7[7];
+  (void)tl;
+  const int slot[7] = {QB_STAT_STALE_TERM, QB_STAT_HIGHER_TERM, QB_STAT_APPLIED,
+                       QB_STAT_REJECTED, QB_STAT_AFTER_STEPDOWN, QB_STAT_COUNT - 1,
+                       QB_STAT_COUNT - 1};
+  tally.t[5] = 0;
+  tally.t[6] = 0;
+  tally.flush(tl7, shard_of(shards), slot);
 }
 
 template <int N>
