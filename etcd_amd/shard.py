@@ -1,14 +1,16 @@
 """Sharding of raft groups over the GPUs of one node.
 
 Groups are independent, so a shard is a contiguous range of global group
-numbers evaluated by one rank with no data exchange.  The only collective is
-assembling the node-wide result: an all-gather of the per-shard commit (u64)
-and vote (u8) vectors — RCCL (backend "nccl") on the GPU path, any
-torch.distributed backend in tests.
+numbers evaluated by one rank with no data exchange.  The two collectives are
+at the edges of the path: assembling the node-wide result (an all-gather of
+the per-shard commit u64 and vote u8 vectors) and, for record batches that
+arrive at arbitrary ranks, delivering each record to its group's shard (an
+all-to-all) — RCCL (backend "nccl") on the GPU path, any torch.distributed
+backend in tests.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -59,3 +61,41 @@ def allgather_results(commit: torch.Tensor, vote: torch.Tensor, total: int,
         parts_c.append(gc[r, : re_ - rb])
         parts_v.append(gv[r, : re_ - rb])
     return torch.cat(parts_c), torch.cat(parts_v)
+
+
+def route_records(cols: Dict[str, torch.Tensor], total: int,
+                  group: Optional[dist.ProcessGroup] = None) -> Dict[str, torch.Tensor]:
+    """Deliver every rank's records to the rank owning their group (SURVEY.md
+    §8e: message batches are bucketed by owning shard).
+
+    ``cols`` holds equal-length record columns, one of them ``"group"`` with
+    global group numbers (int32 holding uint32).  Returns this rank's records
+    with ``group`` rebased to the shard (local index), in (source rank,
+    source position) order — a fixed batch order, which is what the leader
+    step's sequential semantics need.  A group number >= total goes to the
+    last rank as an out-of-range local index (counted there as a bad group).
+    One count exchange plus one all-to-all per column: RCCL over xGMI on the
+    GPU path, any torch.distributed backend in tests."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = cols["group"].device
+    g = cols["group"].to(torch.int64) & 0xFFFFFFFF
+    bounds = torch.tensor([shard_range(total, world, r)[1] for r in range(world)],
+                          dtype=torch.int64, device=dev)
+    owner = torch.bucketize(g, bounds, right=True).clamp_(max=world - 1)
+    order = torch.argsort(owner, stable=True)
+    send_counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    out = {}
+    for name, col in cols.items():
+        send = col[order].contiguous()
+        recv = torch.empty((sum(rc),) + tuple(col.shape[1:]), dtype=col.dtype, device=dev)
+        dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
+                               group=group)
+        out[name] = recv
+    b, _ = shard_range(total, world, rank)
+    local = (out["group"].to(torch.int64) & 0xFFFFFFFF) - b
+    out["group"] = local.to(torch.int32)
+    return out

@@ -78,3 +78,56 @@ def test_sharded_eval_allgather_equals_single_process(world, total, kind):
         off, m, cfg, votes = oc.gen_csr(SEED, kind, total)
         ec, ev = oc.csr_eval(off, m, cfg, votes)
     assert np.array_equal(gc, ec) and np.array_equal(gv, ev)
+
+
+def _route_inputs(rank, M, total):
+    rng = np.random.default_rng(1000 + rank)
+    grp = rng.integers(0, total + 3, M).astype(np.uint32)  # a few past the end
+    idx = rng.integers(0, 1 << 40, M).astype(np.uint64)
+    flags = rng.integers(0, 256, M).astype(np.uint8)
+    return grp, idx, flags
+
+
+def _route_worker(rank, world, port, total, M, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.shard import route_records
+        grp, idx, flags = _route_inputs(rank, M, total)
+        out = route_records({"group": torch.from_numpy(grp.view(np.int32)),
+                             "index": torch.from_numpy(idx.view(np.int64)),
+                             "flags": torch.from_numpy(flags)}, total)
+        q.put((rank, out["group"].numpy().view(np.uint32).copy(),
+               out["index"].numpy().view(np.uint64).copy(), out["flags"].numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_route_records_by_owning_shard(world):
+    total, M = 1000, 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_route_worker, args=(r, world, port, total, M, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (g, i, f)) for r, g, i, f in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    inputs = [_route_inputs(r, M, total) for r in range(world)]
+    for r in range(world):
+        b, e = shard_range(total, world, r)
+        last = r == world - 1
+        want_g, want_i, want_f = [], [], []
+        for src in range(world):  # (source rank, source position) order
+            g, i, f = inputs[src]
+            sel = ((g >= b) & (g < e)) | ((g >= total) & last)
+            want_g.append(g[sel] - b)
+            want_i.append(i[sel])
+            want_f.append(f[sel])
+        assert np.array_equal(got[r][0], np.concatenate(want_g).astype(np.uint32))
+        assert np.array_equal(got[r][1], np.concatenate(want_i))
+        assert np.array_equal(got[r][2], np.concatenate(want_f))
