@@ -269,3 +269,51 @@ def streaming_inbox(G: int, base: torch.Tensor, k: int, D: int = 4, n: int = 5, 
     ib = LeaderInbox(g.to(torch.int32), f.to(torch.uint8), idx, torch.full_like(idx, 7), z, z)
     ib._m = G
     return ib
+
+
+def synth_readindex(G: int, Q: int = 4, n: int = 5, device="cuda"):
+    """Caught-up leaders (5 voters, every follower Replicate at the last
+    index) each holding Q pending ReadIndex requests (read_only.go:30-40: the
+    leader's own ack recorded, request contexts ctx0 + g*Q + k, half of them
+    from a follower, half local) — the ReadIndex / CheckQuorum bench workload
+    of SURVEY.md §8f row 2.  Returns (LeaderGroups, pristine read-queue
+    tensors to restore before each step)."""
+    lg, base = synth_streaming(G, W=4, D=1, n=n, device=device)
+    dev = torch.device(device)
+    S = n * G
+    last = lg.t["last_index"]
+    slot = torch.arange(S, dtype=torch.int64, device=dev) % n
+    gs = torch.arange(S, dtype=torch.int64, device=dev) // n
+    lg.t["match"] = last[gs].clone()
+    lg.t["next"] = last[gs] + 1
+    lg.t["committed"] = last.clone()
+    lg.t["infl_pos"] = torch.zeros(S, dtype=torch.int32, device=dev)
+    lg.readq_cap = Q
+    g = torch.arange(G, dtype=torch.int64, device=dev)
+    k = torch.arange(Q, dtype=torch.int64, device=dev)
+    ctx = ((1 << 40) + g[:, None] * Q + k[None, :]).reshape(-1)
+    idx = last[:, None].expand(G, Q).reshape(-1).clone()
+    frm = torch.where(k % 2 == 0, torch.full_like(k, 0xFF), 1 + (k % (n - 1)))
+    meta = (1 | (frm[None, :].expand(G, Q) << 16)).reshape(-1).to(torch.int32)  # leader acked
+    lg.t["rq_ctx"], lg.t["rq_index"], lg.t["rq_meta"] = ctx, idx, meta
+    lg.t["meta"] = torch.full((G,), 0xFF00 | (1 << 16) | (Q << 20), dtype=torch.int32, device=dev)
+    pristine = {k_: lg.t[k_].clone() for k_ in ("rq_ctx", "rq_index", "rq_meta", "meta")}
+    return lg, ctx.view(G, Q)[:, Q - 1].clone(), pristine
+
+
+def readindex_inbox(G: int, last_ctx: torch.Tensor, n: int = 5, device="cuda"):
+    """Two heartbeat responses per group (followers 1 and 2, shuffled arrival)
+    carrying the latest request context: the second one completes the quorum
+    and releases all Q requests (read_only.go:84-121)."""
+    dev = torch.device(device)
+    g = torch.randperm(2 * G, device=dev) % G
+    # follower 1 for a group's first record, follower 2 for its second
+    order = torch.argsort(g, stable=True)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(2 * G, device=dev) % 2
+    f = (1 + rank).to(torch.uint8) | (1 << 4)  # kind MsgHeartbeatResp
+    z = torch.zeros(2 * G, dtype=torch.int64, device=dev)
+    ib = LeaderInbox(g.to(torch.int32), f.to(torch.uint8), last_ctx[g],
+                     torch.full((2 * G,), 7, dtype=torch.int64, device=dev), z, z)
+    ib._m = 2 * G
+    return ib

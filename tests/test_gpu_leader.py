@@ -161,3 +161,27 @@ def test_streaming_workload_vs_c_oracle():
         assert np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)
         assert res.stats["applied"] == int(stats[0]) == G
     torch.cuda.synchronize()
+
+
+def test_readindex_workload_vs_c_oracle():
+    """The ReadIndex bench workload (§8f row 2) at 256K groups: queues,
+    released reads and every message against the C oracle."""
+    from etcd_amd.quorum.leader import readindex_inbox, synth_readindex
+    from tests import oracle_c as oc
+    G, Q = 1 << 18, 4
+    lg, last_ctx, _ = synth_readindex(G, Q, device="cuda")
+    host = {k: v.copy() for k, v in lg.numpy().items()}
+    ib = readindex_inbox(G, last_ctx, device="cuda")
+    res = lg.step(ib, msg_cap=8 * G)
+    rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
+           "index": ib.index.cpu().numpy().view(np.uint64),
+           "term": ib.term.cpu().numpy().view(np.uint64),
+           "hint": ib.hint.cpu().numpy().view(np.uint64),
+           "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
+    msgs, total, sd, gf, stats = oc.leader_step(host, lg.inflight_cap, Q, 0, rec, threads=16,
+                                                msg_cap=8 * G)
+    dev = lg.numpy()
+    for name in host:
+        assert np.array_equal(dev[name], host[name]), name
+    assert res.msg_total == total == Q * G
+    assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))

@@ -311,6 +311,66 @@ def confchange_config(G, reps):
                "sample": f"{n} groups, Python restatement of confchange.Changer (oracle)"}})
 
 
+def readindex_config(G, reps, Q=4):
+    """§8f row 2: ReadIndex acks — two heartbeat responses per leader carrying
+    the latest read context; the quorum releases all Q pending reads
+    (MsgReadIndexResp / ReadState).  The read queues are restored before each
+    step outside the timed launches (new MsgReadIndex requests are the
+    host's).  Also CheckQuorum: QuorumActive over 16M CSR groups."""
+    from etcd_amd.quorum.leader import synth_readindex, readindex_inbox
+    lg, last_ctx, pristine = synth_readindex(G, Q, device=dev)
+    inboxes = [readindex_inbox(G, last_ctx, device=dev) for _ in range(reps + 2)]
+    stats = torch.zeros(8, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    ev = HipEvents(2)
+    times = []
+    for k in range(reps + 2):
+        for name, t0 in pristine.items():
+            lg.t[name].copy_(t0)
+        if k == 2:
+            stats.zero_()
+        ev.record(ev.ev[0], sp)
+        lg.step(inboxes[k], msg_cap=8 * G, stats=stats, fetch=False)
+        ev.record(ev.ev[1], sp)
+        torch.cuda.synchronize()
+        if k >= 2:
+            times.append(ev.elapsed_ms(0, 1) / 1e3)
+    ev.close()
+    t = float(np.median(times))
+    st = stats.cpu().tolist()
+    # per group-step: 2 records 2 x 21 B, group state 84 B, 5 slots x 29 B,
+    # read queue Q x 20 B read + written, Q messages x 40 B x 3
+    algo = G * (42 + 84 + 145 + Q * 20 * 2 + Q * 40 * 3)
+    # CheckQuorum: QuorumActive over 16M groups (cfg u32 + active u16 -> u8)
+    grp = batch.CsrGroups.synth(0x5EED0003, "ragged", 1 << 24, device=dev)
+    active = torch.randint(-(1 << 15), 1 << 15, (1 << 24,), dtype=torch.int16, device=dev)
+    tq = time_region(lambda: grp.quorum_active(active), 20)
+    # CPU beside it: the C restatement on 1M groups of the same workload
+    import time
+    from tests import oracle_c as oc
+    Gs = 1 << 20
+    lgc, ctxc, _ = synth_readindex(Gs, Q, device="cpu")
+    ibc = readindex_inbox(Gs, ctxc, device="cpu")
+    recc = {"group": ibc.group.numpy().view(np.uint32), "flags": ibc.flags.numpy(),
+            "index": ibc.index.numpy().view(np.uint64), "term": ibc.term.numpy().view(np.uint64),
+            "hint": ibc.hint.numpy().view(np.uint64),
+            "log_term": ibc.log_term.numpy().view(np.uint64)}
+    cpu = {}
+    for threads in (16, 1):
+        host = {k_: v.copy() for k_, v in lgc.numpy().items()}
+        t1 = time.perf_counter()
+        oc.leader_step(host, lgc.inflight_cap, Q, 0, recc, threads=threads, msg_cap=8 * Gs)
+        cpu[threads] = Gs / (time.perf_counter() - t1)
+    report("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
+           {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps,
+            "cpu_baseline": {"value": cpu[16], "unit": "group-steps/s", "cores": 16,
+                             "kind": "port", "value_1thread": cpu[1],
+                             "sample": f"{Gs} groups, one step, C restatement (oracle)"},
+            "read_queue": Q, "check_quorum_16M_us": tq * 1e6,
+            "check_quorum_groups_per_s": (1 << 24) / tq,
+            "check_quorum_GBs": (1 << 24) * 7 / tq / 1e9})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
@@ -329,6 +389,8 @@ def main():
         leader_config(1 << 22, a.reps, shuffle=False)
     if "wire" in which:
         wire_config(1 << 24, a.reps)
+    if "readindex" in which:
+        readindex_config(1 << 22, a.reps)
     if "confchange" in which:
         confchange_config(1 << 23, a.reps)
 
