@@ -1,0 +1,142 @@
+// qb_bucket.h — device bucketing of record batches by group (shared by the
+// bucketed tracker step and the leader step): per-tile LDS counting sorts
+// into super-buckets, then into chunks of CH groups.
+#pragma once
+
+#include "qb_common.h"
+#include "qb_scan.h"
+
+namespace qb {
+namespace bk {
+
+constexpr int kTile = 4096;          // records per histogram/scatter/split tile
+constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
+using scan::kScanPer;
+constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
+
+// Bucketed record payload, structure of arrays (three u64 columns of M), so
+// every scatter store is one contiguous wave-wide write:
+//   index, term, and mr = meta | ridx << 32 with
+//   meta = lg (bits 0-9) | chunk-low (10-16) | record flags byte (17-24:
+//          slot 17-20, kind 21-22, no-progress 23, reject 24),
+//   ridx = batch index of the record (step-down ordering).
+struct Cols {
+  u64* index;
+  u64* term;
+  u64* mr;
+};
+
+__host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
+
+struct Geometry {
+  u64 G, M;
+  u32 n, CH, NC, NSB, NT;
+  u64 nbins() const { return u64(NSB) * NT; }
+};
+
+inline Geometry geometry(u32 n, u64 G, u64 M) {
+  Geometry g{};
+  g.G = G;
+  g.M = M;
+  g.n = n;
+  g.CH = chunk_groups(n);
+  g.NC = u32((G + g.CH - 1) / g.CH);
+  g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
+  g.NT = u32((M + kTile - 1) / kTile);
+  return g;
+}
+
+// Workspace carve (all offsets 256-byte aligned).
+struct Carve {
+  size_t shards, hist, bsum, parts, chunk_start, buf1, buf2, total;
+};
+// Upper bound on parts: every super-bucket contributes at most one partial.
+inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
+inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+// ncols = 3: index, term and mr move with the records; ncols = 1: only mr
+// (callers that read the payload from the original batch by ridx).
+inline Carve carve(const Geometry& g, int ncols = 3) {
+  Carve c{};
+  size_t o = 0;
+  c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
+  c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
+  c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
+  // part table: pfirst[NSB+1], part_sb[max_parts], nparts
+  c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
+  c.chunk_start = o;  o += up256(sizeof(u32) * max_parts(g) * (kChunksPerSb + 1));
+  c.buf1 = o;  o += ncols * up256(sizeof(u64) * g.M);
+  c.buf2 = o;  o += ncols * up256(sizeof(u64) * g.M);
+  c.total = o;
+  return c;
+}
+
+inline Cols cols_at(char* base, u64 M, int ncols = 3) {
+  const size_t col = up256(sizeof(u64) * M);
+  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base)};
+  return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
+              reinterpret_cast<u64*>(base + 2 * col)};
+}
+
+
+// Run table of one chunk: the chunk's run in each of up to kRuns parts,
+// with an inclusive prefix of run lengths so flattened record f maps to a
+// buffer index by binary search.
+struct RunTable {
+  static constexpr u32 kRuns = 64;
+  u32 lo[kRuns];
+  u32 pre[kRuns + 1];
+  u32 nr;
+  // Every thread calls; returns the number of records in parts [pb, min(p1, pb+kRuns)).
+  __device__ __forceinline__ u32 build(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
+    __syncthreads();  // earlier readers of the table are done
+    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
+    if (threadIdx.x < 64) {  // one wave: inclusive scan of the run lengths
+      const u32 r = threadIdx.x;
+      u32 l = 0, len = 0;
+      if (r < n) {
+        const u64 row = u64(pb + r) * (kChunksPerSb + 1) + cl;
+        l = cs[row];
+        len = cs[row + 1] - l;
+      }
+      u32 x = len;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = u32(__shfl_up(int(x), o, 64));
+        if (r >= u32(o)) x += y;
+      }
+      if (r < n) {
+        lo[r] = l;
+        pre[r + 1] = x;
+      }
+      if (r == 0) {
+        pre[0] = 0;
+        nr = n;
+      }
+    }
+    __syncthreads();
+    return pre[n];
+  }
+  __device__ __forceinline__ u32 locate(u32 f) const {
+    u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
+    while (b - a > 1) {
+      const u32 m = (a + b) >> 1;
+      if (pre[m] <= f) a = m;
+      else b = m;
+    }
+    return lo[a] + (f - pre[a]);
+  }
+};
+
+// K1-K4 of the bucketed pipeline: records (any order) -> buf2 holds each
+// chunk's records as one run per part of its super-bucket; pt / cs describe
+// the parts and the chunk runs inside them (RunTable reads them).  Records
+// with group >= G are dropped and counted into shards[QB_STAT_BAD_GROUP], and
+// with n < 16 those with slot >= n into shards[QB_STAT_NON_MEMBER].
+// rec_index == rec_term == nullptr buckets the mr column alone (carve with
+// ncols = 1).
+int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
+                   const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
+                   hipStream_t st);
+
+}  // namespace bk
+}  // namespace qb

@@ -16,9 +16,15 @@
 //   responseToReadIndexReq                raft.go:1737-1752
 //
 // Pipeline:
-//   L1 k_ld_count    per record: atomic count per group (bad groups counted)
-//   L2 scan          exclusive scan of the counts -> each group's record run
-//   L3 k_ld_scatter  per record: its batch index into its group's run
+//   L1 bucket        bk::bucket_records (qb_bucket.h) sorts the records'
+//                    batch indexes into chunks of 256 groups through LDS
+//                    counting sorts (bad groups counted)
+//   L2 k_ld_chunk_total + scan  records per chunk -> each chunk's base
+//   L3 k_ld_chunk_runs  per chunk: LDS count per group, block scan (writes
+//                    the per-group run starts), LDS-atomic scatter of the
+//                    batch indexes into the groups' runs
+//   (shards beyond the bucket geometry, > 134M groups, use per-record
+//   global atomics instead: k_ld_count / scan / k_ld_scatter)
 //   L4 k_ld_step     one thread per group: sort its run by batch index
 //                    (records arrive in any order), then the sequential
 //                    stepLeader over its Progress / log view / read queue;
@@ -32,6 +38,7 @@
 // records.
 #include <cstdlib>
 
+#include "qb_bucket.h"
 #include "qb_common.h"
 #include "qb_scan.h"
 
@@ -59,16 +66,31 @@ __host__ __device__ __forceinline__ const u64* U(const uint64_t* p) {
   return reinterpret_cast<const u64*>(p);
 }
 
+constexpr u32 kCh = bk::chunk_groups(16);  // groups per bucket chunk (256)
+static_assert(kCh == kBlock, "one thread per group of a chunk");
+
 struct Carve {
-  size_t cnt, bsum, cursor, perm, mcnt, mbsum, fix, chead, cnext, chunks, pool, shards, total;
+  size_t cnt, bsum, cursor, perm, mcnt, mbsum, fix, chead, cnext, chunks, pool, shards;
+  size_t bkt, ctot, cbsum, total;
   u64 nchunks;
+  bool bucketed;
+  bk::Geometry geo;
+  bk::Carve bcv;
 };
 inline Carve carve(u64 G, u64 M) {
   Carve c{};
   size_t o = 0;
+  c.geo = bk::geometry(16, G, M);
+  c.bucketed = c.geo.NSB <= 4096;
+  if (c.bucketed) {
+    c.bcv = bk::carve(c.geo, 1);
+    c.bkt = o;   o += up256(c.bcv.total);
+    c.ctot = o;  o += up256(sizeof(u32) * (u64(c.geo.NC) + 1));
+    c.cbsum = o; o += up256(sizeof(u32) * (scan::blocks(c.geo.NC) + 1));
+  }
   c.cnt = o;    o += up256(sizeof(u32) * (G + 1));
   c.bsum = o;   o += up256(sizeof(u32) * (scan::blocks(G) + 1));
-  c.cursor = o; o += up256(sizeof(u32) * (G + 1));
+  if (!c.bucketed) { c.cursor = o; o += up256(sizeof(u32) * (G + 1)); }
   c.perm = o;   o += up256(sizeof(u32) * (M + 1));
   c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
   c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
@@ -123,6 +145,71 @@ __global__ __launch_bounds__(kBlock) void k_ld_scatter(u64 G, u64 M, const u32* 
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < M; i += stride) {
     const u32 g = rg[i];
     if (g < G) perm[atomicAdd(cursor + g, 1u)] = u32(i);
+  }
+}
+
+// --------------------------------------------------------- L2 / L3 (bk) ----
+// Records of chunk c: the sum of its runs over the parts of its super-bucket.
+__global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
+                                                           const u32* __restrict__ pt,
+                                                           const u32* __restrict__ cs,
+                                                           u32* __restrict__ ctot) {
+  const u32 c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= geo.NC) return;
+  const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
+  u32 s = 0;
+  for (u32 p = pt[sb], p1 = pt[sb + 1]; p < p1; ++p) {
+    const u64 row = u64(p) * (bk::kChunksPerSb + 1) + cl;
+    s += cs[row + 1] - cs[row];
+  }
+  ctot[c] = s;
+}
+
+// One workgroup per chunk of kCh groups (one thread per group): count the
+// chunk's records per group in LDS, scan the counts (cnt[g] = the group's
+// run start, cnt[G] = all valid records), then place every record's batch
+// index in its group's run with an LDS cursor.  Order inside a run is
+// arbitrary; the step sorts each run.
+__global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo,
+                                                          const u64* __restrict__ mr,
+                                                          const u32* __restrict__ pt,
+                                                          const u32* __restrict__ cs,
+                                                          const u32* __restrict__ cbase,
+                                                          u32* __restrict__ cnt,
+                                                          u32* __restrict__ perm) {
+  __shared__ bk::RunTable rt;
+  __shared__ u32 cur[kCh];
+  __shared__ u32 wsum[kBlock / 64];
+  const u32 c = blockIdx.x, t = threadIdx.x;
+  const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
+  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  cur[t] = 0;
+  for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
+    const u32 total = rt.build(cs, pb, p1, cl);  // synchronises first
+    for (u32 f = t; f < total; f += kBlock) atomicAdd(&cur[u32(mr[rt.locate(f)]) & 1023u], 1u);
+  }
+  __syncthreads();
+  const u32 x = cur[t];
+  u32 inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = u32(__shfl_up(int(inc), o, 64));
+    if ((t & 63u) >= u32(o)) inc += y;
+  }
+  if ((t & 63u) == 63u) wsum[t >> 6] = inc;
+  __syncthreads();
+  for (u32 w = 0; w < (t >> 6); ++w) inc += wsum[w];
+  const u32 base = cbase[c], start = inc - x;
+  const u64 g = u64(c) * kCh + t;
+  if (g < geo.G) cnt[g] = base + start;
+  if (c + 1 == geo.NC && t == 0) cnt[geo.G] = cbase[geo.NC];
+  cur[t] = start;
+  for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
+    const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
+    for (u32 f = t; f < total; f += kBlock) {
+      const u64 v = mr[rt.locate(f)];
+      perm[base + atomicAdd(&cur[u32(v) & 1023u], 1u)] = u32(v >> 32);
+    }
   }
 }
 
@@ -683,11 +770,15 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
   }
 }
 
-__global__ void k_ld_fold(const u64* __restrict__ shards, u64* __restrict__ stats) {
+// bshards: the bucket pass's shards (bad groups), or null.
+__global__ void k_ld_fold(const u64* __restrict__ shards, const u64* __restrict__ bshards,
+                          u64* __restrict__ stats) {
   const int k = threadIdx.x;
   if (k >= QB_LSTAT_COUNT) return;
   u64 s = 0;
   for (int i = 0; i < 64; ++i) s += shards[i * QB_LSTAT_COUNT + k];
+  if (bshards && k == QB_LSTAT_BAD_GROUP)
+    for (int i = 0; i < bk::kShards; ++i) s += bshards[i * QB_STAT_COUNT + QB_STAT_BAD_GROUP];
   stats[k] += s;
 }
 
@@ -730,30 +821,54 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   char* ws = static_cast<char*>(workspace);
   u32* cnt = reinterpret_cast<u32*>(ws + c.cnt);
   u32* bsum = reinterpret_cast<u32*>(ws + c.bsum);
-  u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);
   u32* perm = reinterpret_cast<u32*>(ws + c.perm);
   u32* mcnt = reinterpret_cast<u32*>(ws + c.mcnt);
   u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
   u32* pool = reinterpret_cast<u32*>(ws + c.pool);
   u64* shards = reinterpret_cast<u64*>(ws + c.shards);
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(u32) * (G + 1), st);
-  if (e == hipSuccess) e = hipMemsetAsync(pool, 0, sizeof(u32) * 2, st);
+  hipError_t e = hipMemsetAsync(pool, 0, sizeof(u32) * 2, st);
   if (e == hipSuccess) e = hipMemsetAsync(shards, 0, sizeof(u64) * QB_LSTAT_COUNT * 64, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
-  const unsigned rgrid = M ? (grid_for(M) < 2048 ? grid_for(M) : 2048) : 1;
-  if (M) {
-    hipLaunchKernelGGL(ld::k_ld_count, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group, cnt,
-                       shards);
-    QB_CHECK_LAUNCH("k_ld_count");
-  }
-  scan::launch(cnt, G, bsum, st);
-  QB_CHECK_LAUNCH("scan(records)");
-  if (M) {
-    e = hipMemcpyAsync(cursor, cnt, sizeof(u32) * G, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(cursor)");
-    hipLaunchKernelGGL(ld::k_ld_scatter, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group,
-                       cursor, perm);
-    QB_CHECK_LAUNCH("k_ld_scatter");
+  u64* bshards = nullptr;
+  if (c.bucketed) {
+    char* bws = ws + c.bkt;
+    bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);
+    u32* ctot = reinterpret_cast<u32*>(ws + c.ctot);
+    const u32* pt = reinterpret_cast<const u32*>(bws + c.bcv.parts);
+    const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
+    e = hipMemsetAsync(bshards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bucket shards)");
+    const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags, nullptr, nullptr,
+                                      bshards, st);
+    if (rc != QB_OK) return rc;
+    hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, st, c.geo, pt, cs, ctot);
+    QB_CHECK_LAUNCH("k_ld_chunk_total");
+    scan::launch(ctot, c.geo.NC, reinterpret_cast<u32*>(ws + c.cbsum), st);
+    QB_CHECK_LAUNCH("scan(chunks)");
+    const bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 1);
+    hipLaunchKernelGGL(ld::k_ld_chunk_runs, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo,
+                       static_cast<const u64*>(b2.mr), pt, cs, ctot, cnt, perm);
+    QB_CHECK_LAUNCH("k_ld_chunk_runs");
+  } else {
+    u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);
+    e = hipMemsetAsync(cnt, 0, sizeof(u32) * (G + 1), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(counts)");
+    const unsigned rgrid = M ? (grid_for(M) < 2048 ? grid_for(M) : 2048) : 1;
+    if (M) {
+      hipLaunchKernelGGL(ld::k_ld_count, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group, cnt,
+                         shards);
+      QB_CHECK_LAUNCH("k_ld_count");
+    }
+    scan::launch(cnt, G, bsum, st);
+    QB_CHECK_LAUNCH("scan(records)");
+    if (M) {
+      e = hipMemcpyAsync(cursor, cnt, sizeof(u32) * G, hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(cursor)");
+      hipLaunchKernelGGL(ld::k_ld_scatter, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group,
+                         cursor, perm);
+      QB_CHECK_LAUNCH("k_ld_scatter");
+    }
   }
   ld::Args A{};
   A.lg = *lg;
@@ -792,7 +907,7 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
                      A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
                      msg_cap, msg_off, ld::U(msg_total), shards);
   QB_CHECK_LAUNCH("k_ld_emit");
-  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64), 0, st, shards, ld::U(stats));
+  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64), 0, st, shards, bshards, ld::U(stats));
   QB_CHECK_LAUNCH("k_ld_fold");
   return QB_OK;
 }

@@ -27,75 +27,10 @@
 //                    batch index), MaybeUpdate as LDS atomic max, RecentActive
 //                    as LDS atomic or, then maybeCommit for the chunk's groups
 //                    and a coalesced write-back of match/next/active/committed.
-#include "qb_common.h"
-#include "qb_scan.h"
+#include "qb_bucket.h"
 
 namespace qb {
 namespace bk {
-
-constexpr int kTile = 4096;          // records per histogram/scatter/split tile
-constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
-using scan::kScanPer;
-constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
-
-// Bucketed record payload, structure of arrays (three u64 columns of M), so
-// every scatter store is one contiguous wave-wide write:
-//   index, term, and mr = meta | ridx << 32 with
-//   meta = lg (bits 0-9) | chunk-low (10-16) | slot (17-20) | reject (21),
-//   ridx = batch index of the record (step-down ordering).
-struct Cols {
-  u64* index;
-  u64* term;
-  u64* mr;
-};
-
-__host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
-
-struct Geometry {
-  u64 G, M;
-  u32 n, CH, NC, NSB, NT;
-  u64 nbins() const { return u64(NSB) * NT; }
-};
-
-inline Geometry geometry(u32 n, u64 G, u64 M) {
-  Geometry g{};
-  g.G = G;
-  g.M = M;
-  g.n = n;
-  g.CH = chunk_groups(n);
-  g.NC = u32((G + g.CH - 1) / g.CH);
-  g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
-  g.NT = u32((M + kTile - 1) / kTile);
-  return g;
-}
-
-// Workspace carve (all offsets 256-byte aligned).
-struct Carve {
-  size_t shards, hist, bsum, parts, chunk_start, buf1, buf2, total;
-};
-// Upper bound on parts: every super-bucket contributes at most one partial.
-inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
-inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
-inline Carve carve(const Geometry& g) {
-  Carve c{};
-  size_t o = 0;
-  c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
-  c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
-  c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
-  // part table: pfirst[NSB+1], part_sb[max_parts], nparts
-  c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
-  c.chunk_start = o;  o += up256(sizeof(u32) * max_parts(g) * (kChunksPerSb + 1));
-  c.buf1 = o;  o += 3 * up256(sizeof(u64) * g.M);
-  c.buf2 = o;  o += 3 * up256(sizeof(u64) * g.M);
-  c.total = o;
-  return c;
-}
-
-inline Cols cols_at(char* base, u64 M) {
-  const size_t col = up256(sizeof(u64) * M);
-  return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
-              reinterpret_cast<u64*>(base + 2 * col)};
-}
 
 // Counters of block b go to shard b % kShards (QB_STAT_COUNT u64 each, one
 // cache line), folded into the caller's stats by k_stats_fold.
@@ -237,7 +172,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
   tile_perm(L, start, nrec);
   // three payload columns: index, term, mr = meta | ridx << 32
-  for (int col = 0; col < 3; ++col) {
+  for (int col = ri ? 0 : 2; col < 3; ++col) {
     for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
       const u64 i = t0 + k;
       u64 v;
@@ -249,7 +184,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
         const u32 g = rg[i], f = rf[i];
         const u32 chunk = g / geo.CH;
         const u32 meta = (g - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
-                         ((f & 0x0Fu) << 17) | (((f & QB_REC_REJECT) ? 1u : 0u) << 21);
+                         ((f & 0xFFu) << 17);
         v = u64(meta) | (u64(u32(i)) << 32);
       }
       L.stage[k] = v;
@@ -325,7 +260,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   tile_perm(L, start, nrec);
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
   __syncthreads();
-  for (int col = 0; col < 2; ++col) {
+  for (int col = in.index ? 0 : 2; col < 2; ++col) {
     const u64* src = col == 0 ? in.index : in.term;
     u64* dst = col == 0 ? out.index : out.term;
     for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) L.stage[k] = src[lo + k];
@@ -335,54 +270,6 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   }
 }
 
-// Run table of one chunk: the chunk's run in each of up to kRuns parts,
-// with an inclusive prefix of run lengths so flattened record f maps to a
-// buffer index by binary search.
-struct RunTable {
-  static constexpr u32 kRuns = 64;
-  u32 lo[kRuns];
-  u32 pre[kRuns + 1];
-  u32 nr;
-  // Every thread calls; returns the number of records in parts [pb, min(p1, pb+kRuns)).
-  __device__ __forceinline__ u32 build(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
-    __syncthreads();  // earlier readers of the table are done
-    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
-    if (threadIdx.x < 64) {  // one wave: inclusive scan of the run lengths
-      const u32 r = threadIdx.x;
-      u32 l = 0, len = 0;
-      if (r < n) {
-        const u64 row = u64(pb + r) * (kChunksPerSb + 1) + cl;
-        l = cs[row];
-        len = cs[row + 1] - l;
-      }
-      u32 x = len;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = u32(__shfl_up(int(x), o, 64));
-        if (r >= u32(o)) x += y;
-      }
-      if (r < n) {
-        lo[r] = l;
-        pre[r + 1] = x;
-      }
-      if (r == 0) {
-        pre[0] = 0;
-        nr = n;
-      }
-    }
-    __syncthreads();
-    return pre[n];
-  }
-  __device__ __forceinline__ u32 locate(u32 f) const {
-    u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
-    while (b - a > 1) {
-      const u32 m = (a + b) >> 1;
-      if (pre[m] <= f) a = m;
-      else b = m;
-    }
-    return lo[a] + (f - pre[a]);
-  }
-};
 
 // ---------------------------------------------------------------- K5 ----
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
@@ -458,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
           any_higher = 1;
         } else if (!stale) {
           atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-          if (meta & (1u << 21)) {
+          if (meta & (1u << 24)) {  // QB_REC_REJECT
             rejected = true;                              // raft.go:1109: not MaybeUpdate
           } else {
             applied = true;
@@ -497,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
               after = true;
             } else {
               atomicOr(&act[lg], 1u << s);
-              if (meta & (1u << 21)) {
+              if (meta & (1u << 24)) {  // QB_REC_REJECT
                 rejected = true;
               } else {
                 applied = true;
@@ -583,6 +470,47 @@ void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& ge
 
 using namespace qb;
 
+namespace qb {
+namespace bk {
+
+int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
+                   const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
+                   hipStream_t st) {
+  u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
+  u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
+  u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
+  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
+  const int ncols = rec_index ? 3 : 1;
+  const Cols buf1 = cols_at(ws + cv.buf1, geo.M, ncols);
+  const Cols buf2 = cols_at(ws + cv.buf2, geo.M, ncols);
+  const size_t lds_bins = sizeof(u32) * geo.NSB;
+  if (geo.M == 0) {
+    hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
+    return e == hipSuccess ? QB_OK : hip_fail(e, "hipMemsetAsync(parts)");
+  }
+  hipLaunchKernelGGL(k_bk_hist, dim3(geo.NT), dim3(kBlock), lds_bins, st, geo, rec_group,
+                     rec_flags, hist, shards);
+  QB_CHECK_LAUNCH("k_bk_hist");
+  const u64 nb = geo.nbins();
+  const u32 nblk = u32((nb + kScanPer - 1) / kScanPer);
+  hipLaunchKernelGGL(scan::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+  hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
+  hipLaunchKernelGGL(scan::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+  QB_CHECK_LAUNCH("k_scan");
+  hipLaunchKernelGGL(k_bk_scatter, dim3(geo.NT), dim3(kPartThreads), 2 * lds_bins, st, geo,
+                     rec_group, rec_flags, rec_index, rec_term, hist, buf1);
+  QB_CHECK_LAUNCH("k_bk_scatter");
+  hipLaunchKernelGGL(k_bk_parts, dim3(1), dim3(1024), 0, st, geo, hist, pt);
+  QB_CHECK_LAUNCH("k_bk_parts");
+  hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
+                     geo, hist, pt, buf1, buf2, cs);
+  QB_CHECK_LAUNCH("k_bk_split");
+  return QB_OK;
+}
+
+}  // namespace bk
+}  // namespace qb
+
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
   return bk::carve(bk::geometry(n, G, M)).total;
@@ -612,40 +540,19 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
              (unsigned long long)G);
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
-  u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
-  u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const bk::Cols buf1 = bk::cols_at(ws + cv.buf1, M);
   const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
-  const size_t lds_bins = sizeof(u32) * geo.NSB;
   hipError_t e0 = hipMemsetAsync(shards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
   if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(stat shards)");
 
-  if (M > 0) {
-    hipLaunchKernelGGL(bk::k_bk_hist, dim3(geo.NT), dim3(kBlock), lds_bins, st, geo, rec_group,
-                       rec_flags, hist, shards);
-    QB_CHECK_LAUNCH("k_bk_hist");
-    const u64 nb = geo.nbins();
-    const u32 nblk = u32((nb + bk::kScanPer - 1) / bk::kScanPer);
-    hipLaunchKernelGGL(scan::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
-    hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
-    hipLaunchKernelGGL(scan::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
-    QB_CHECK_LAUNCH("k_scan");
-    hipLaunchKernelGGL(bk::k_bk_scatter, dim3(geo.NT), dim3(bk::kPartThreads), 2 * lds_bins, st,
-                       geo, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
-                       reinterpret_cast<const u64*>(rec_term), hist, buf1);
-    QB_CHECK_LAUNCH("k_bk_scatter");
-    hipLaunchKernelGGL(bk::k_bk_parts, dim3(1), dim3(1024), 0, st, geo, hist, pt);
-    QB_CHECK_LAUNCH("k_bk_parts");
-    hipLaunchKernelGGL(bk::k_bk_split, dim3(unsigned(bk::max_parts(geo))), dim3(bk::kPartThreads),
-                       0, st, geo, hist, pt, buf1, buf2, cs);
-    QB_CHECK_LAUNCH("k_bk_split");
-  } else {
-    hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(parts)");
+  {
+    const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags,
+                                      reinterpret_cast<const u64*>(rec_index),
+                                      reinterpret_cast<const u64*>(rec_term), shards, st);
+    if (rc != QB_OK) return rc;
   }
   bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs,
                      reinterpret_cast<const u64*>(group_term),
