@@ -70,7 +70,8 @@ constexpr u32 kCh = bk::chunk_groups(16);  // groups per bucket chunk (256)
 static_assert(kCh == kBlock, "one thread per group of a chunk");
 
 struct Carve {
-  size_t cnt, bsum, cursor, perm, mcnt, mbsum, fix, chead, cnext, chunks, pool, shards;
+  size_t cnt, bsum, cursor, perm, rflags, rterm, rindex, rhint, rlt, mcnt, mbsum, fix, chead,
+      cnext, chunks, pool, shards;
   size_t bkt, ctot, cbsum, total;
   u64 nchunks;
   bool bucketed;
@@ -83,15 +84,20 @@ inline Carve carve(u64 G, u64 M) {
   c.geo = bk::geometry(16, G, M);
   c.bucketed = c.geo.NSB <= 4096;
   if (c.bucketed) {
-    c.bcv = bk::carve(c.geo, 1);
+    c.bcv = bk::carve(c.geo, 3);
     c.bkt = o;   o += up256(c.bcv.total);
     c.ctot = o;  o += up256(sizeof(u32) * (u64(c.geo.NC) + 1));
     c.cbsum = o; o += up256(sizeof(u32) * (scan::blocks(c.geo.NC) + 1));
   }
   c.cnt = o;    o += up256(sizeof(u32) * (G + 1));
   c.bsum = o;   o += up256(sizeof(u32) * (scan::blocks(G) + 1));
-  if (!c.bucketed) { c.cursor = o; o += up256(sizeof(u32) * (G + 1)); }
+  c.cursor = o; o += up256(sizeof(u32) * (G + 1));
   c.perm = o;   o += up256(sizeof(u32) * (M + 1));
+  c.rflags = o; o += up256(sizeof(u8) * (M + 1));
+  c.rterm = o;  o += up256(sizeof(u64) * (M + 1));
+  c.rindex = o; o += up256(sizeof(u64) * (M + 1));
+  c.rhint = o;  o += up256(sizeof(u64) * (M + 1));
+  c.rlt = o;    o += up256(sizeof(u64) * (M + 1));
   c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
   c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
   c.fix = o;    o += up256(sizeof(Msg) * kFix * G);
@@ -105,13 +111,24 @@ inline Carve carve(u64 G, u64 M) {
   return c;
 }
 
+// The inbox's fields gathered into group order (position k of perm), so the
+// step reads its records coalesced and one dependent hop earlier.
+struct RecCols {
+  u8* flags;
+  u64* term;
+  u64* index;
+  u64* hint;      // reject records only
+  u64* log_term;  // reject records only
+};
+
 struct Args {
   qb_leader_groups lg;
   qb_leader_inbox in;
   const u32* cnt;     // exclusive scan of per-group record counts, [G+1]
-  u32* perm;          // batch indexes grouped by group
+  u32* perm;          // batch indexes grouped by group (each run ascending)
+  RecCols rec;        // the records in perm order
   u32* mcnt;          // messages per group
-  Msg* fix;           // [G * kFix]
+  Msg* fix;           // [kFix][G]: message k of every group contiguous
   u32* chead;         // first overflow chunk per group
   u32* cnext;         // chunk links
   Msg* chunks;        // [nchunks * kChunk]
@@ -148,6 +165,109 @@ __global__ __launch_bounds__(kBlock) void k_ld_scatter(u64 G, u64 M, const u32* 
   }
 }
 
+// Sort a group's run of batch indexes ascending (runs are short: insertion
+// sort; long runs: heapsort, both in place).
+__device__ void sort_run(u32* a, u32 n) {
+  if (n <= 32) {
+    for (u32 i = 1; i < n; ++i) {
+      const u32 v = a[i];
+      u32 j = i;
+      while (j > 0 && a[j - 1] > v) {
+        a[j] = a[j - 1];
+        --j;
+      }
+      a[j] = v;
+    }
+    return;
+  }
+  auto sift = [&](u32 root, u32 end) {
+    for (;;) {
+      u32 c = 2 * root + 1;
+      if (c >= end) return;
+      if (c + 1 < end && a[c + 1] > a[c]) ++c;
+      if (a[root] >= a[c]) return;
+      const u32 t = a[root];
+      a[root] = a[c];
+      a[c] = t;
+      root = c;
+    }
+  };
+  for (u32 i = n / 2; i-- > 0;) sift(i, n);
+  for (u32 e = n - 1; e > 0; --e) {
+    const u32 t = a[0];
+    a[0] = a[e];
+    a[e] = t;
+    sift(0, e);
+  }
+}
+
+// A group's run [r0, r0 + n) of perm: batch order, then its record fields
+// gathered to the same positions.
+__device__ void gather_run(const qb_leader_inbox& in, u32* perm, u32 r0, u32 n,
+                           const RecCols& rc) {
+  if (n > 1) sort_run(perm + r0, n);
+  for (u32 k = r0; k < r0 + n; ++k) {
+    const u32 i = perm[k];
+    const u8 f = in.flags[i];
+    rc.flags[k] = f;
+    rc.term[k] = in.term[i];
+    rc.index[k] = in.index[i];
+    if (f & QB_REC_REJECT) {
+      rc.hint[k] = in.hint ? in.hint[i] : 0ull;
+      rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
+    }
+  }
+}
+
+// A run whose fields are already gathered, in arbitrary order: insertion
+// sort by batch index moving every field (runs are short); long runs are
+// sorted by index alone and gathered again.
+__device__ void order_run(const qb_leader_inbox& in, u32* perm, u32 r0, u32 n,
+                          const RecCols& rc) {
+  if (n > 32) {
+    gather_run(in, perm, r0, n, rc);
+    return;
+  }
+  for (u32 a = r0 + 1; a < r0 + n; ++a) {
+    const u32 v = perm[a];
+    const u8 f = rc.flags[a];
+    const u64 t = rc.term[a], x = rc.index[a];
+    const bool rej = (f & QB_REC_REJECT) != 0;
+    const u64 h = rej ? rc.hint[a] : 0ull, lt = rej ? rc.log_term[a] : 0ull;
+    u32 j = a;
+    while (j > r0 && perm[j - 1] > v) {
+      perm[j] = perm[j - 1];
+      const u8 fj = rc.flags[j - 1];
+      rc.flags[j] = fj;
+      rc.term[j] = rc.term[j - 1];
+      rc.index[j] = rc.index[j - 1];
+      if (fj & QB_REC_REJECT) {
+        rc.hint[j] = rc.hint[j - 1];
+        rc.log_term[j] = rc.log_term[j - 1];
+      }
+      --j;
+    }
+    perm[j] = v;
+    rc.flags[j] = f;
+    rc.term[j] = t;
+    rc.index[j] = x;
+    if (rej) {
+      rc.hint[j] = h;
+      rc.log_term[j] = lt;
+    }
+  }
+}
+
+// Fallback path (no bucket geometry): one thread per group.
+__global__ __launch_bounds__(kBlock) void k_ld_gather(u64 G, qb_leader_inbox in,
+                                                      const u32* __restrict__ cnt,
+                                                      u32* __restrict__ perm, RecCols rc) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const u32 r0 = cnt[g], r1 = cnt[g + 1];
+  if (r1 > r0) gather_run(in, perm, r0, r1 - r0, rc);
+}
+
 // --------------------------------------------------------- L2 / L3 (bk) ----
 // Records of chunk c: the sum of its runs over the parts of its super-bucket.
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
@@ -165,18 +285,30 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
   ctot[c] = s;
 }
 
+constexpr u32 kStageRecs = 1536;  // chunk records placed through LDS
+constexpr u32 kLdsSortMax = 64;   // longer runs are ordered in HBM
+struct ChunkStage {
+  u64 mr[kStageRecs];
+  u64 term[kStageRecs];
+  u64 index[kStageRecs];
+};
+__device__ __forceinline__ ChunkStage& chunk_stage() {
+  __shared__ ChunkStage s;
+  return s;
+}
+
 // One workgroup per chunk of kCh groups (one thread per group): count the
 // chunk's records per group in LDS, scan the counts (cnt[g] = the group's
 // run start, cnt[G] = all valid records), then place every record's batch
 // index in its group's run with an LDS cursor.  Order inside a run is
 // arbitrary; the step sorts each run.
-__global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo,
-                                                          const u64* __restrict__ mr,
+__global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::Cols recs,
                                                           const u32* __restrict__ pt,
                                                           const u32* __restrict__ cs,
                                                           const u32* __restrict__ cbase,
                                                           u32* __restrict__ cnt,
-                                                          u32* __restrict__ perm) {
+                                                          u32* __restrict__ perm,
+                                                          qb_leader_inbox in, RecCols rc) {
   __shared__ bk::RunTable rt;
   __shared__ u32 cur[kCh];
   __shared__ u32 wsum[kBlock / 64];
@@ -186,7 +318,8 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo,
   cur[t] = 0;
   for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);  // synchronises first
-    for (u32 f = t; f < total; f += kBlock) atomicAdd(&cur[u32(mr[rt.locate(f)]) & 1023u], 1u);
+    for (u32 f = t; f < total; f += kBlock)
+      atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
   }
   __syncthreads();
   const u32 x = cur[t];
@@ -204,13 +337,81 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo,
   if (g < geo.G) cnt[g] = base + start;
   if (c + 1 == geo.NC && t == 0) cnt[geo.G] = cbase[geo.NC];
   cur[t] = start;
+  const u32 ntot = cbase[c + 1] - base;  // workgroup-uniform
+  if (ntot <= kStageRecs) {
+    // Common case: the chunk's records are placed in LDS, each group's run
+    // is put in batch order there (runs of <= kLdsSortMax), and the chunk
+    // is written out with coalesced stores.
+    ChunkStage& cs_ = chunk_stage();
+    for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
+      const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
+      for (u32 f = t; f < total; f += kBlock) {
+        const u32 b = rt.locate(f);
+        const u64 v = recs.mr[b];
+        const u64 term = recs.term[b], index = recs.index[b];
+        const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
+        cs_.mr[e] = v;
+        cs_.term[e] = term;
+        cs_.index[e] = index;
+      }
+    }
+    __syncthreads();
+    if (x > 1 && x <= kLdsSortMax) {
+      for (u32 a = start + 1; a < start + x; ++a) {
+        const u64 v = cs_.mr[a], tv = cs_.term[a], iv = cs_.index[a];
+        u32 j = a;
+        while (j > start && (cs_.mr[j - 1] >> 32) > (v >> 32)) {
+          cs_.mr[j] = cs_.mr[j - 1];
+          cs_.term[j] = cs_.term[j - 1];
+          cs_.index[j] = cs_.index[j - 1];
+          --j;
+        }
+        cs_.mr[j] = v;
+        cs_.term[j] = tv;
+        cs_.index[j] = iv;
+      }
+    }
+    __syncthreads();
+    for (u32 e = t; e < ntot; e += kBlock) {
+      const u64 v = cs_.mr[e];
+      const u32 k = base + e, i = u32(v >> 32);
+      const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
+      perm[k] = i;
+      rc.flags[k] = fl;
+      rc.term[k] = cs_.term[e];
+      rc.index[k] = cs_.index[e];
+      if (fl & QB_REC_REJECT) {
+        rc.hint[k] = in.hint ? in.hint[i] : 0ull;
+        rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
+      }
+    }
+    __syncthreads();  // perm complete (workgroup-visible) for the long runs
+    if (x > kLdsSortMax) gather_run(in, perm, base + start, x, rc);
+    return;
+  }
   for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
     for (u32 f = t; f < total; f += kBlock) {
-      const u64 v = mr[rt.locate(f)];
-      perm[base + atomicAdd(&cur[u32(v) & 1023u], 1u)] = u32(v >> 32);
+      const u32 b = rt.locate(f);
+      const u64 v = recs.mr[b];
+      const u64 term = recs.term[b], index = recs.index[b];
+      const u32 k = base + atomicAdd(&cur[u32(v) & 1023u], 1u);
+      const u32 i = u32(v >> 32);
+      const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
+      perm[k] = i;
+      rc.flags[k] = fl;
+      rc.term[k] = term;
+      rc.index[k] = index;
+      if (fl & QB_REC_REJECT) {
+        rc.hint[k] = in.hint ? in.hint[i] : 0ull;
+        rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
+      }
     }
   }
+  // A group with several records: its run (placed in arbitrary order) is
+  // put in batch order and its fields gathered again in that order.
+  __syncthreads();  // the chunk's runs are complete (workgroup-visible)
+  if (x > 1) order_run(in, perm, base + start, x, rc);
 }
 
 // ------------------------------------------------------------------ L4 ----
@@ -218,6 +419,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo,
 struct Group {
   u64 g;
   u32 s0, ns;           // first slot, number of slots
+  u32 j0;               // first slot in the staged span
   u32 mask_in, mask_out;
   u32 meta;
   u64 term, committed;
@@ -244,10 +446,11 @@ __device__ u64 log_term(const Args& A, const Group& G_, u64 i) {
   const u64 dummy = LG_FIRST(A, G_) - 1;
   if (i < dummy || i > LG_LAST(A, G_)) return 0;
   u64 t = 0;
-  const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
-  const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
+  const u64* rs = U(A.lg.run_start) + G_.g;  // run r at rs[r * G] (run-major)
+  const u64* rt = U(A.lg.run_term) + G_.g;
+  const u64 G = A.lg.G;
   for (u32 r = 0; r < G_.nruns; ++r)
-    if (rs[r] <= i) t = rt[r];
+    if (rs[r * G] <= i) t = rt[r * G];
   return t;
 }
 
@@ -257,15 +460,16 @@ __device__ u64 log_term(const Args& A, const Group& G_, u64 i) {
 __device__ u64 find_conflict_by_term(const Args& A, const Group& G_, u64 index, u64 term) {
   if (index > LG_LAST(A, G_)) return index;
   const u64 dummy = LG_FIRST(A, G_) - 1;
-  const u64* rs = U(A.lg.run_start) + G_.g * QB_LEADER_MAX_RUNS;
-  const u64* rt = U(A.lg.run_term) + G_.g * QB_LEADER_MAX_RUNS;
+  const u64* rs = U(A.lg.run_start) + G_.g;  // run r at rs[r * G] (run-major)
+  const u64* rt = U(A.lg.run_term) + G_.g;
+  const u64 G = A.lg.G;
   for (;;) {
     if (index < dummy || index > LG_LAST(A, G_)) return index;  // term 0 <= term
     u64 t = 0, start = 0;
     for (u32 r = 0; r < G_.nruns; ++r)
-      if (rs[r] <= index) {
-        t = rt[r];
-        start = rs[r];
+      if (rs[r * G] <= index) {
+        t = rt[r * G];
+        start = rs[r * G];
       }
     if (t <= term) return index;
     const u64 lo = start > dummy ? start : dummy;
@@ -287,7 +491,7 @@ __device__ void emit(const Args& A, Group& G_, u8 type, u32 to, u64 index, u64 l
   const u32 k = G_.nmsg++;
   if (G_.dropped) return;
   if (k < kFix) {
-    A.fix[G_.g * kFix + k] = m;
+    A.fix[u64(k) * A.lg.G + G_.g] = m;
     G_.stored = k + 1;
     return;
   }
@@ -308,28 +512,65 @@ __device__ void emit(const Args& A, Group& G_, u8 type, u32 to, u64 index, u64 l
 
 // Progress accessors (slot j of the group).
 // A slot's Progress: the kernel arguments (uniform, scalar registers) and the
-// slot's index; addresses are formed at each use, so a live Pr costs two
-// vector registers instead of seven 64-bit pointers.
-struct Pr {
+// slot's index; addresses are formed at each use, so a live Pr costs a few
+// vector registers instead of seven 64-bit pointers.  With S, match / next /
+// inflight position / state byte live in the workgroup's LDS copy of its
+// slot span (k_ld_step stages it with coalesced loads and writes it back);
+// the inflight ring and pendingSnapshot stay in HBM.
+constexpr u32 kSpanCap = 1536;  // staged slots per workgroup (6 per group)
+struct SlotStage {
+  u64 match[kSpanCap];
+  u64 next[kSpanCap];
+  u32 ipos[kSpanCap];
+  u8 st[kSpanCap];
+  u8 dirty[kSpanCap];  // slot reached through pr_of: written back
+};
+__device__ __forceinline__ SlotStage& slot_stage() {
+  __shared__ SlotStage ss;
+  return ss;
+}
+
+template <bool S>
+struct PrT {
   const Args* A;
-  u64 p;
-  __device__ __forceinline__ u64& match() const { return U(A->lg.match)[p]; }
-  __device__ __forceinline__ u64& next() const { return U(A->lg.next)[p]; }
+  u64 p;  // slot index in the group arrays
+  u32 j;  // slot index in the staged span (S)
+  __device__ __forceinline__ u64& match() const {
+    if constexpr (S) return slot_stage().match[j];
+    else return U(A->lg.match)[p];
+  }
+  __device__ __forceinline__ u64& next() const {
+    if constexpr (S) return slot_stage().next[j];
+    else return U(A->lg.next)[p];
+  }
+  __device__ __forceinline__ u8& st() const {
+    if constexpr (S) return slot_stage().st[j];
+    else return A->lg.pstate[p];
+  }
+  __device__ __forceinline__ u32& ipos() const {
+    if constexpr (S) return slot_stage().ipos[j];
+    else return A->lg.infl_pos[p];
+  }
   __device__ __forceinline__ u64& psnap() const { return U(A->lg.pending_snapshot)[p]; }
-  __device__ __forceinline__ u8& st() const { return A->lg.pstate[p]; }
-  __device__ __forceinline__ u32& ipos() const { return A->lg.infl_pos[p]; }
   __device__ __forceinline__ u64* ibuf() const { return U(A->lg.infl_buf) + p * A->lg.inflight_cap; }
   __device__ __forceinline__ u32 K() const { return A->lg.inflight_cap; }
 };
-__device__ __forceinline__ Pr pr_of(const Args& A, const Group& G_, u32 j) {
-  return Pr{&A, u64(G_.s0) + j};
+// Every Progress write goes through a PrT from here, so marking the slot
+// dirty here covers them all (maybe_commit only reads match).
+template <bool S>
+__device__ __forceinline__ PrT<S> pr_of(const Args& A, const Group& G_, u32 j) {
+  if constexpr (S) slot_stage().dirty[G_.j0 + j] = 1;
+  return PrT<S>{&A, u64(G_.s0) + j, G_.j0 + j};
 }
 __device__ __forceinline__ u32 st_state(u8 s) { return s & 3u; }
 
 // inflights.go
-__device__ __forceinline__ bool infl_full(const Pr& p) { return (p.ipos() >> 16) == p.K(); }
-__device__ __forceinline__ void infl_reset(const Pr& p) { p.ipos() = 0; }
-__device__ void infl_add(const Pr& p, u64 v) {
+template <class P>
+__device__ __forceinline__ bool infl_full(const P& p) { return (p.ipos() >> 16) == p.K(); }
+template <class P>
+__device__ __forceinline__ void infl_reset(const P& p) { p.ipos() = 0; }
+template <class P>
+__device__ void infl_add(const P& p, u64 v) {
   const u32 pos = p.ipos();
   const u32 start = pos & 0xFFFFu, count = pos >> 16;
   u32 nxt = start + count;
@@ -337,7 +578,8 @@ __device__ void infl_add(const Pr& p, u64 v) {
   p.ibuf()[nxt] = v;
   p.ipos() = start | ((count + 1) << 16);
 }
-__device__ void infl_free_le(const Pr& p, u64 to) {
+template <class P>
+__device__ void infl_free_le(const P& p, u64 to) {
   const u32 pos = p.ipos();
   const u32 start = pos & 0xFFFFu, count = pos >> 16;
   if (count == 0 || to < p.ibuf()[start]) return;
@@ -351,12 +593,14 @@ __device__ void infl_free_le(const Pr& p, u64 to) {
 }
 
 // progress.go
-__device__ __forceinline__ void reset_state(const Pr& p, u32 state) {
+template <class P>
+__device__ __forceinline__ void reset_state(const P& p, u32 state) {
   p.st() = u8((p.st() & QB_PR_RECENT_ACTIVE) | state);  // ProbeSent = false
   p.psnap() = 0;
   infl_reset(p);
 }
-__device__ void become_probe(const Pr& p) {
+template <class P>
+__device__ void become_probe(const P& p) {
   const u64 m1 = p.match() + 1;
   if (st_state(p.st()) == QB_PR_SNAPSHOT) {
     const u64 ps1 = p.psnap() + 1;
@@ -367,15 +611,18 @@ __device__ void become_probe(const Pr& p) {
     p.next() = m1;
   }
 }
-__device__ __forceinline__ void become_replicate(const Pr& p) {
+template <class P>
+__device__ __forceinline__ void become_replicate(const P& p) {
   reset_state(p, QB_PR_REPLICATE);
   p.next() = p.match() + 1;
 }
-__device__ __forceinline__ void become_snapshot(const Pr& p, u64 snapi) {
+template <class P>
+__device__ __forceinline__ void become_snapshot(const P& p, u64 snapi) {
   reset_state(p, QB_PR_SNAPSHOT);
   p.psnap() = snapi;
 }
-__device__ __forceinline__ bool is_paused(const Pr& p) {
+template <class P>
+__device__ __forceinline__ bool is_paused(const P& p) {
   const u8 s = p.st();
   switch (st_state(s)) {
     case QB_PR_PROBE: return (s & QB_PR_PROBE_SENT) != 0;
@@ -383,7 +630,8 @@ __device__ __forceinline__ bool is_paused(const Pr& p) {
     default: return true;
   }
 }
-__device__ bool maybe_update(const Pr& p, u64 n) {
+template <class P>
+__device__ bool maybe_update(const P& p, u64 n) {
   bool updated = false;
   if (p.match() < n) {
     p.match() = n;
@@ -394,7 +642,8 @@ __device__ bool maybe_update(const Pr& p, u64 n) {
   if (p.next() < n1) p.next() = n1;
   return updated;
 }
-__device__ bool maybe_decr_to(const Pr& p, u64 rejected, u64 hint) {
+template <class P>
+__device__ bool maybe_decr_to(const P& p, u64 rejected, u64 hint) {
   if (st_state(p.st()) == QB_PR_REPLICATE) {
     if (rejected <= p.match()) return false;
     p.next() = p.match() + 1;
@@ -409,8 +658,9 @@ __device__ bool maybe_decr_to(const Pr& p, u64 rejected, u64 hint) {
 }
 
 // raft.go:432-492
+template <bool S>
 __device__ bool maybe_send_append(const Args& A, Group& G_, u32 to, bool send_if_empty) {
-  const Pr p = pr_of(A, G_, to);
+  const PrT<S> p = pr_of<S>(A, G_, to);
   if (is_paused(p)) return false;
   const u64 nx = p.next();
   const u64 term = log_term(A, G_, nx - 1);
@@ -466,8 +716,9 @@ __device__ u64 half_ci(const u64* mp, u32 ns, u32 mask) {
   return best;
 }
 
+template <bool S>
 __device__ bool maybe_commit(const Args& A, Group& G_) {
-  const u64* mp = U(A.lg.match) + G_.s0;
+  const u64* mp = S ? slot_stage().match + G_.j0 : U(A.lg.match) + G_.s0;
   const u64 a = half_ci(mp, G_.ns, G_.mask_in), b = half_ci(mp, G_.ns, G_.mask_out);
   const u64 mci = a < b ? a : b;
   if (mci > G_.committed && log_term(A, G_, mci) == G_.term) {
@@ -477,9 +728,10 @@ __device__ bool maybe_commit(const Args& A, Group& G_) {
   return false;
 }
 
+template <bool S>
 __device__ void bcast_append(const Args& A, Group& G_) {
   for (u32 s = 0; s < G_.ns; ++s)
-    if (s != leader_slot(G_)) maybe_send_append(A, G_, s, true);
+    if (s != leader_slot(G_)) maybe_send_append<S>(A, G_, s, true);
 }
 
 // joint.go:61-75 over majority.go:178-210 with votes = acks (all true).
@@ -491,13 +743,14 @@ __device__ __forceinline__ u8 acks_vote(const Group& G_, u32 acks) {
   return joint_vote(r1, r2);
 }
 
-__device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 ctx) {
+template <bool S>
+__device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const PrT<S>& p, u64 ctx) {
   p.st() = u8((p.st() | QB_PR_RECENT_ACTIVE) & ~QB_PR_PROBE_SENT);
   if (st_state(p.st()) == QB_PR_REPLICATE && infl_full(p)) {
     const u32 start = p.ipos() & 0xFFFFu;
     infl_free_le(p, p.ibuf()[start]);  // FreeFirstOne
   }
-  if (p.match() < LG_LAST(A, G_)) maybe_send_append(A, G_, slot, true);
+  if (p.match() < LG_LAST(A, G_)) maybe_send_append<S>(A, G_, slot, true);
   if (A.lg.read_only != QB_READ_ONLY_SAFE || ctx == 0) return;
   // read_only.go:68-79 recvAck
   const u32 cap = A.lg.readq_cap;
@@ -535,7 +788,8 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const Pr& p, 
   G_.meta = (G_.meta & ~(0x1Fu << 20)) | (rest << 20);
 }
 
-__device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 index, bool reject,
+template <bool S>
+__device__ void app_resp(const Args& A, Group& G_, u32 slot, const PrT<S>& p, u64 index, bool reject,
                          u64 hint, u64 hint_term, u8& gfl) {
   p.st() = u8(p.st() | QB_PR_RECENT_ACTIVE);
   if (reject) {
@@ -543,7 +797,7 @@ __device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 in
     if (hint_term > 0) next_probe = find_conflict_by_term(A, G_, hint, hint_term);
     if (maybe_decr_to(p, index, next_probe)) {
       if (st_state(p.st()) == QB_PR_REPLICATE) become_probe(p);
-      maybe_send_append(A, G_, slot, true);
+      maybe_send_append<S>(A, G_, slot, true);
     }
     return;
   }
@@ -558,156 +812,173 @@ __device__ void app_resp(const Args& A, Group& G_, u32 slot, const Pr& p, u64 in
   } else if (s == QB_PR_REPLICATE) {
     infl_free_le(p, index);
   }
-  if (maybe_commit(A, G_)) {
+  if (maybe_commit<S>(A, G_)) {
     gfl |= QB_LFLAG_ADVANCED;
     if (G_.meta & QB_META_PENDING_READINDEX) {
       // releasePendingReadIndexMessages (raft.go:1813-1825) is the host's.
       G_.meta &= ~QB_META_PENDING_READINDEX;
       gfl |= QB_LFLAG_RELEASE_READS;
     }
-    bcast_append(A, G_);
+    bcast_append<S>(A, G_);
   } else if (old_paused) {
-    maybe_send_append(A, G_, slot, true);
+    maybe_send_append<S>(A, G_, slot, true);
   }
-  while (maybe_send_append(A, G_, slot, false)) {
+  while (maybe_send_append<S>(A, G_, slot, false)) {
   }
   if (slot == transferee(G_) && p.match() == LG_LAST(A, G_))
     emit(A, G_, QB_MSG_TIMEOUT_NOW, slot, 0, 0, 0, 0);
 }
 
-__device__ void snap_status(const Pr& p, bool reject) {
+template <class P>
+__device__ void snap_status(const P& p, bool reject) {
   if (st_state(p.st()) != QB_PR_SNAPSHOT) return;
   if (reject) p.psnap() = 0;
   become_probe(p);
   p.st() = u8(p.st() | QB_PR_PROBE_SENT);
 }
 
-// Sort a group's run of batch indexes ascending (runs are short: insertion
-// sort; long runs: heapsort, both in place).
-__device__ void sort_run(u32* a, u32 n) {
-  if (n <= 32) {
-    for (u32 i = 1; i < n; ++i) {
-      const u32 v = a[i];
-      u32 j = i;
-      while (j > 0 && a[j - 1] > v) {
-        a[j] = a[j - 1];
-        --j;
-      }
-      a[j] = v;
+struct StepCounts {
+  u32 applied = 0, stale = 0, higher = 0, non = 0, after = 0, msgs = 0, stored = 0;
+};
+
+// One group's records [r0, r1) of the gathered columns, in batch order (raft.go:847-921 term
+// filter, then stepLeader per record).
+template <bool S>
+__device__ void step_group(const Args& A, u64 g, u32 r0, u32 r1, u32 s0, u32 s1, u32 sb,
+                           u32& stepdown, u8& gfl, StepCounts& n) {
+  Group G_;
+  G_.g = g;
+  G_.s0 = s0;
+  G_.ns = s1 - s0;
+  G_.j0 = s0 - sb;
+  const u32 c = A.lg.cfg[g];
+  G_.mask_in = c & 0xFFFFu;
+  G_.mask_out = c >> 16;
+  G_.meta = A.lg.meta[g];
+  G_.term = A.lg.term[g];
+  G_.committed = A.lg.committed[g];
+  G_.nruns = (G_.meta >> 16) & 0xFu;
+  G_.nmsg = 0;
+  G_.stored = 0;
+  G_.chunk = 0;
+  G_.dropped = false;
+  for (u32 k = r0; k < r1; ++k) {
+    if (stepdown != kNone) {
+      ++n.after;
+      continue;
     }
-    return;
-  }
-  auto sift = [&](u32 root, u32 end) {
-    for (;;) {
-      u32 c = 2 * root + 1;
-      if (c >= end) return;
-      if (c + 1 < end && a[c + 1] > a[c]) ++c;
-      if (a[root] >= a[c]) return;
-      const u32 t = a[root];
-      a[root] = a[c];
-      a[c] = t;
-      root = c;
+    const u64 t = A.rec.term[k];
+    const u32 f = A.rec.flags[k];
+    if (t != 0 && t > G_.term) {  // raft.go:852-880: becomeFollower
+      stepdown = A.perm[k];
+      ++n.higher;
+      continue;
     }
-  };
-  for (u32 i = n / 2; i-- > 0;) sift(i, n);
-  for (u32 e = n - 1; e > 0; --e) {
-    const u32 t = a[0];
-    a[0] = a[e];
-    a[e] = t;
-    sift(0, e);
+    if (t != 0 && t < G_.term) {  // raft.go:883-921: ignored
+      ++n.stale;
+      continue;
+    }
+    const u32 slot = f & 0x0Fu;
+    if (slot >= G_.ns || (f & QB_REC_NO_PROGRESS)) {  // raft.go:1099-1104: no progress
+      ++n.non;
+      continue;
+    }
+    ++n.applied;
+    const PrT<S> p = pr_of<S>(A, G_, slot);
+    const u32 kind = (f >> 4) & 3u;
+    const bool reject = (f & QB_REC_REJECT) != 0;
+    if (kind == QB_IN_APP_RESP) {
+      const u64 hint = reject ? A.rec.hint[k] : 0;
+      const u64 ht = reject ? A.rec.log_term[k] : 0;
+      app_resp<S>(A, G_, slot, p, A.rec.index[k], reject, hint, ht, gfl);
+    } else if (kind == QB_IN_HEARTBEAT_RESP) {
+      heartbeat_resp<S>(A, G_, slot, p, A.rec.index[k]);
+    } else if (kind == QB_IN_SNAP_STATUS) {
+      snap_status(p, reject);
+    } else if (st_state(p.st()) == QB_PR_REPLICATE) {  // MsgUnreachable
+      become_probe(p);
+    }
   }
+  if (stepdown != kNone) gfl |= QB_LFLAG_STEPPED_DOWN;
+  A.lg.committed[g] = G_.committed;
+  A.lg.meta[g] = G_.meta;
+  n.msgs = G_.nmsg;
+  n.stored = G_.stored;
 }
 
-template <int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void k_ld_step(Args A) {
+// One thread per group.  The workgroup's groups own one contiguous slot span
+// [off[g0], off[g0 + 256]); when it fits kSpanCap, its match / next /
+// inflight positions / state bytes are staged in LDS with coalesced loads,
+// stepped there, and written back coalesced (the step's Progress reads and
+// read-modify-writes then cost LDS latency, not HBM round trips).  A larger
+// span runs on the HBM arrays directly.
+__global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
   __shared__ u32 lds[7];
   BlockTally<7> tally;
   const u64 G = A.lg.G;
-  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
-  u32 napplied = 0, nstale = 0, nhigher = 0, nnon = 0, nafter = 0;
-  u32 nmsg = 0, nstored = 0;
-  if (g < G) {
-    const u32 r0 = A.cnt[g], r1 = A.cnt[g + 1];
+  const u64 g0 = u64(blockIdx.x) * kBlock;
+  const u64 g = g0 + threadIdx.x;
+  const u64 gend = g0 + kBlock < G ? g0 + kBlock : G;
+  const bool live = g < G;
+  const u32 r0 = live ? A.cnt[g] : 0u, r1 = live ? A.cnt[g + 1] : 0u;
+  const u32 s0 = live ? A.lg.off[g] : 0u, s1 = live ? A.lg.off[g + 1] : 0u;
+  const u32 sb = A.lg.off[g0], span = A.lg.off[gend] - sb;
+  const bool staged = span <= kSpanCap;  // workgroup-uniform
+  const bool busy = __syncthreads_or(r1 > r0);
+  if (!busy) {
+    // No records for any group of the workgroup: only the outputs.
+    if (live) {
+      A.mcnt[g] = 0;
+      if (A.stepdown_at) A.stepdown_at[g] = kNone;
+      if (A.gflags) A.gflags[g] = 0;
+    }
+    return;
+  }
+  SlotStage& ss = slot_stage();
+  if (staged) {
+    for (u32 j = threadIdx.x; j < span; j += kBlock) {
+      ss.match[j] = U(A.lg.match)[sb + j];
+      ss.next[j] = U(A.lg.next)[sb + j];
+      ss.ipos[j] = A.lg.infl_pos[sb + j];
+      ss.st[j] = A.lg.pstate[sb + j];
+      ss.dirty[j] = 0;
+    }
+    __syncthreads();
+  }
+  StepCounts n;
+  if (live) {
     u32 stepdown = kNone;
     u8 gfl = 0;
     if (r1 > r0) {
-      Group G_;
-      G_.g = g;
-      G_.s0 = A.lg.off[g];
-      G_.ns = A.lg.off[g + 1] - G_.s0;
-      const u32 c = A.lg.cfg[g];
-      G_.mask_in = c & 0xFFFFu;
-      G_.mask_out = c >> 16;
-      G_.meta = A.lg.meta[g];
-      G_.term = A.lg.term[g];
-      G_.committed = A.lg.committed[g];
-      G_.nruns = (G_.meta >> 16) & 0xFu;
-      G_.nmsg = 0;
-      G_.stored = 0;
-      G_.chunk = 0;
-      G_.dropped = false;
-      u32* run = A.perm + r0;
-      sort_run(run, r1 - r0);
-      for (u32 k = r0; k < r1; ++k) {
-        const u32 i = A.perm[k];
-        if (stepdown != kNone) {
-          ++nafter;
-          continue;
-        }
-        const u64 t = A.in.term[i];
-        const u32 f = A.in.flags[i];
-        if (t != 0 && t > G_.term) {  // raft.go:852-880: becomeFollower
-          stepdown = i;
-          ++nhigher;
-          continue;
-        }
-        if (t != 0 && t < G_.term) {  // raft.go:883-921: ignored
-          ++nstale;
-          continue;
-        }
-        const u32 slot = f & 0x0Fu;
-        if (slot >= G_.ns || (f & QB_REC_NO_PROGRESS)) {  // raft.go:1099-1104: no progress
-          ++nnon;
-          continue;
-        }
-        ++napplied;
-        const Pr p = pr_of(A, G_, slot);
-        const u32 kind = (f >> 4) & 3u;
-        const bool reject = (f & QB_REC_REJECT) != 0;
-        if (kind == QB_IN_APP_RESP) {
-          const u64 hint = reject && A.in.hint ? A.in.hint[i] : 0;
-          const u64 ht = reject && A.in.log_term ? A.in.log_term[i] : 0;
-          app_resp(A, G_, slot, p, A.in.index[i], reject, hint, ht, gfl);
-        } else if (kind == QB_IN_HEARTBEAT_RESP) {
-          heartbeat_resp(A, G_, slot, p, A.in.index[i]);
-        } else if (kind == QB_IN_SNAP_STATUS) {
-          snap_status(p, reject);
-        } else if (st_state(p.st()) == QB_PR_REPLICATE) {  // MsgUnreachable
-          become_probe(p);
-        }
-      }
-      if (stepdown != kNone) gfl |= QB_LFLAG_STEPPED_DOWN;
-      A.lg.committed[g] = G_.committed;
-      A.lg.meta[g] = G_.meta;
-      nmsg = G_.nmsg;
-      nstored = G_.stored;
+      if (staged) step_group<true>(A, g, r0, r1, s0, s1, sb, stepdown, gfl, n);
+      else step_group<false>(A, g, r0, r1, s0, s1, sb, stepdown, gfl, n);
     }
-    A.mcnt[g] = nstored;
+    A.mcnt[g] = n.stored;
     if (A.stepdown_at) A.stepdown_at[g] = stepdown;
     if (A.gflags) A.gflags[g] = gfl;
+  }
+  if (staged) {
+    __syncthreads();
+    for (u32 j = threadIdx.x; j < span; j += kBlock) {
+      if (!ss.dirty[j]) continue;
+      U(A.lg.match)[sb + j] = ss.match[j];
+      U(A.lg.next)[sb + j] = ss.next[j];
+      A.lg.infl_pos[sb + j] = ss.ipos[j];
+      A.lg.pstate[sb + j] = ss.st[j];
+    }
   }
   // Per-wave sums of per-thread counts, then one flush per block.
   auto wsum = [](u32 v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
   };
-  tally.t[0] += wsum(napplied);
-  tally.t[1] += wsum(nstale);
-  tally.t[2] += wsum(nhigher);
-  tally.t[3] += wsum(nnon);
-  tally.t[4] += wsum(nafter);
-  tally.t[5] += wsum(nmsg);
-  tally.t[6] += wsum(nmsg - nstored);
+  tally.t[0] += wsum(n.applied);
+  tally.t[1] += wsum(n.stale);
+  tally.t[2] += wsum(n.higher);
+  tally.t[3] += wsum(n.non);
+  tally.t[4] += wsum(n.after);
+  tally.t[5] += wsum(n.msgs);
+  tally.t[6] += wsum(n.msgs - n.stored);
   const int slot[7] = {QB_LSTAT_APPLIED, QB_LSTAT_STALE_TERM, QB_LSTAT_HIGHER_TERM,
                        QB_LSTAT_NON_MEMBER, QB_LSTAT_AFTER_STEPDOWN, QB_LSTAT_MSGS,
                        QB_LSTAT_MSGS_DROPPED};
@@ -756,7 +1027,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
     const u32 k = u32(idx - lo[a]);
     u64 v;
     if (k < kFix) {
-      v = fw[(g * kFix + k) * 5 + word];
+      v = fw[(u64(k) * G + g) * 5 + word];
     } else {
       u32 c = chead[g];
       for (u32 hop = (k - kFix) / kChunk; hop; --hop) c = cnext[c];
@@ -771,15 +1042,19 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
 }
 
 // bshards: the bucket pass's shards (bad groups), or null.
+// One wave per counter: lanes sum strided shards, then a shuffle reduction.
 __global__ void k_ld_fold(const u64* __restrict__ shards, const u64* __restrict__ bshards,
                           u64* __restrict__ stats) {
-  const int k = threadIdx.x;
+  const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (k >= QB_LSTAT_COUNT) return;
-  u64 s = 0;
-  for (int i = 0; i < 64; ++i) s += shards[i * QB_LSTAT_COUNT + k];
+  u64 s = shards[lane * QB_LSTAT_COUNT + k];
   if (bshards && k == QB_LSTAT_BAD_GROUP)
-    for (int i = 0; i < bk::kShards; ++i) s += bshards[i * QB_STAT_COUNT + QB_STAT_BAD_GROUP];
-  stats[k] += s;
+    for (int i = lane; i < bk::kShards; i += 64) s += bshards[i * QB_STAT_COUNT + QB_STAT_BAD_GROUP];
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 y = u64(__shfl_xor(static_cast<unsigned long long>(s), o, 64));
+    s += y;
+  }
+  if (lane == 0) stats[k] += s;
 }
 
 }  // namespace ld
@@ -822,6 +1097,9 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   u32* cnt = reinterpret_cast<u32*>(ws + c.cnt);
   u32* bsum = reinterpret_cast<u32*>(ws + c.bsum);
   u32* perm = reinterpret_cast<u32*>(ws + c.perm);
+  const ld::RecCols rcols{reinterpret_cast<u8*>(ws + c.rflags), reinterpret_cast<u64*>(ws + c.rterm),
+                       reinterpret_cast<u64*>(ws + c.rindex), reinterpret_cast<u64*>(ws + c.rhint),
+                       reinterpret_cast<u64*>(ws + c.rlt)};
   u32* mcnt = reinterpret_cast<u32*>(ws + c.mcnt);
   u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
   u32* pool = reinterpret_cast<u32*>(ws + c.pool);
@@ -830,7 +1108,11 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   if (e == hipSuccess) e = hipMemsetAsync(shards, 0, sizeof(u64) * QB_LSTAT_COUNT * 64, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
   u64* bshards = nullptr;
-  if (c.bucketed) {
+  // QB_LEADER_GROUPING=atomic selects the per-record-atomic grouping even
+  // when the bucket geometry fits (test knob: both paths are checked).
+  const char* grouping = getenv("QB_LEADER_GROUPING");
+  const bool force_atomic = grouping && grouping[0] == 'a';
+  if (c.bucketed && !force_atomic) {
     char* bws = ws + c.bkt;
     bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);
     u32* ctot = reinterpret_cast<u32*>(ws + c.ctot);
@@ -838,17 +1120,17 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
     const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
     e = hipMemsetAsync(bshards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bucket shards)");
-    const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags, nullptr, nullptr,
-                                      bshards, st);
+    const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags,
+                                      ld::U(in->index), ld::U(in->term), bshards, st);
     if (rc != QB_OK) return rc;
     hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
                        dim3(kBlock), 0, st, c.geo, pt, cs, ctot);
     QB_CHECK_LAUNCH("k_ld_chunk_total");
     scan::launch(ctot, c.geo.NC, reinterpret_cast<u32*>(ws + c.cbsum), st);
     QB_CHECK_LAUNCH("scan(chunks)");
-    const bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 1);
+    const bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 3);
     hipLaunchKernelGGL(ld::k_ld_chunk_runs, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo,
-                       static_cast<const u64*>(b2.mr), pt, cs, ctot, cnt, perm);
+                       b2, pt, cs, ctot, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");
   } else {
     u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);
@@ -868,6 +1150,9 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
       hipLaunchKernelGGL(ld::k_ld_scatter, dim3(rgrid), dim3(kBlock), 0, st, G, M, in->group,
                          cursor, perm);
       QB_CHECK_LAUNCH("k_ld_scatter");
+      hipLaunchKernelGGL(ld::k_ld_gather, dim3(grid_for(G)), dim3(kBlock), 0, st, G, *in, cnt,
+                         perm, rcols);
+      QB_CHECK_LAUNCH("k_ld_gather");
     }
   }
   ld::Args A{};
@@ -875,6 +1160,7 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   A.in = *in;
   A.cnt = cnt;
   A.perm = perm;
+  A.rec = rcols;
   A.mcnt = mcnt;
   A.fix = reinterpret_cast<ld::Msg*>(ws + c.fix);
   A.chead = reinterpret_cast<u32*>(ws + c.chead);
@@ -885,21 +1171,7 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   A.shards = shards;
   A.stepdown_at = stepdown_at;
   A.gflags = gflags;
-  // Occupancy variant of the step kernel (min waves per SIMD; more waves
-  // trade register spills for latency hiding).  QB_LEADER_WAVES overrides
-  // the measured default (development knob).
-  static const int waves = [] {
-    const char* e = getenv("QB_LEADER_WAVES");
-    return e ? atoi(e) : 1;
-  }();
-  if (waves >= 8)
-    hipLaunchKernelGGL(ld::k_ld_step<8>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
-  else if (waves >= 6)
-    hipLaunchKernelGGL(ld::k_ld_step<6>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
-  else if (waves >= 5)
-    hipLaunchKernelGGL(ld::k_ld_step<5>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
-  else
-    hipLaunchKernelGGL(ld::k_ld_step<1>, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
+  hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
   QB_CHECK_LAUNCH("k_ld_step");
   scan::launch(mcnt, G, mbsum, st);
   QB_CHECK_LAUNCH("scan(messages)");
@@ -907,7 +1179,7 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
                      A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
                      msg_cap, msg_off, ld::U(msg_total), shards);
   QB_CHECK_LAUNCH("k_ld_emit");
-  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64), 0, st, shards, bshards, ld::U(stats));
+  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64 * QB_LSTAT_COUNT), 0, st, shards, bshards, ld::U(stats));
   QB_CHECK_LAUNCH("k_ld_fold");
   return QB_OK;
 }

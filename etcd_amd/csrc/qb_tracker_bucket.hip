@@ -142,7 +142,12 @@ __device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec
 
 // ---------------------------------------------------------------- K3 ----
 // Level 1: one block per tile of the original records; bins = super-buckets;
-// each bin's run goes to gstart[bin] (from the level-1 scan).
+// each bin's run goes to gstart[bin] (from the level-1 scan).  Every global
+// load of the tile (group, flags and both payload columns) is issued before
+// the first LDS step, so the loads overlap each other and the ranking; the
+// payload then goes register -> LDS -> permuted LDS read -> coalesced store.
+constexpr int kPer = kTile / kPartThreads;  // records per thread
+
 __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
@@ -151,19 +156,32 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   u32* start = dyn;               // NSB: count, then local exclusive start
   u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
   __shared__ TileLds L;
+  const u64 t0 = u64(blockIdx.x) * kTile;
+  const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
+  u32 g[kPer], f[kPer];
+  u64 vi[kPer], vt[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const u32 k = threadIdx.x + j * kPartThreads;
+    const bool in = k < nrec;
+    g[j] = in ? rg[t0 + k] : 0xFFFFFFFFu;
+    f[j] = in ? rf[t0 + k] : 0u;
+    vi[j] = (in && ri) ? ri[t0 + k] : 0ull;
+    vt[j] = (in && ri) ? rt[t0 + k] : 0ull;
+  }
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     start[b] = 0;
     gstart[b] = offsets[u64(b) * geo.NT + blockIdx.x];
   }
   __syncthreads();
-  const u64 t0 = u64(blockIdx.x) * kTile;
-  const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
   const u32 sbgroups = geo.CH * kChunksPerSb;
-  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
-    const u32 g = rg[t0 + k];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const u32 k = threadIdx.x + j * kPartThreads;
+    if (k >= nrec) continue;
     u16 b = kNoBin;
-    if (g < geo.G && (rf[t0 + k] & 0x0Fu) < geo.n) {
-      b = u16(g / sbgroups);
+    if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
+      b = u16(g[j] / sbgroups);
       L.rank[k] = u16(atomicAdd(&start[b], 1u));
     }
     L.bin[k] = b;
@@ -173,19 +191,20 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   tile_perm(L, start, nrec);
   // three payload columns: index, term, mr = meta | ridx << 32
   for (int col = ri ? 0 : 2; col < 3; ++col) {
-    for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
-      const u64 i = t0 + k;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = threadIdx.x + j * kPartThreads;
+      if (k >= nrec) continue;
       u64 v;
       if (col == 0) {
-        v = ri[i];
+        v = vi[j];
       } else if (col == 1) {
-        v = rt[i];
+        v = vt[j];
       } else {
-        const u32 g = rg[i], f = rf[i];
-        const u32 chunk = g / geo.CH;
-        const u32 meta = (g - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
-                         ((f & 0xFFu) << 17);
-        v = u64(meta) | (u64(u32(i)) << 32);
+        const u32 chunk = g[j] / geo.CH;
+        const u32 meta = (g[j] - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
+                         ((f[j] & 0xFFu) << 17);
+        v = u64(meta) | (u64(u32(t0 + k)) << 32);
       }
       L.stage[k] = v;
     }
@@ -243,6 +262,16 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
   const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
   const u32 nrec = hi - lo;
+  // The payload columns are loaded now, with mr, and held in registers.
+  u64 vi[kPer], vt[kPer];
+  if (in.index) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = threadIdx.x + j * kPartThreads;
+      vi[j] = k < nrec ? in.index[lo + k] : 0ull;
+      vt[j] = k < nrec ? in.term[lo + k] : 0ull;
+    }
+  }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
   for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
@@ -261,9 +290,12 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
   __syncthreads();
   for (int col = in.index ? 0 : 2; col < 2; ++col) {
-    const u64* src = col == 0 ? in.index : in.term;
     u64* dst = col == 0 ? out.index : out.term;
-    for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) L.stage[k] = src[lo + k];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = threadIdx.x + j * kPartThreads;
+      if (k < nrec) L.stage[k] = col == 0 ? vi[j] : vt[j];
+    }
     __syncthreads();
     for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) dst[lo + e] = L.stage[L.perm[e]];
     __syncthreads();

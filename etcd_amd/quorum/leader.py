@@ -10,7 +10,7 @@ Array names and meanings (all numpy dtypes little-endian):
   off[G+1] u32, cfg[G] u32 (mask_in | mask_out << 16), meta[G] u32 (leader
   slot | transferee << 8 | runs << 16 | readq length << 20 | pending-read bit
   25), term/committed/first_index/last_index/snap_index/snap_term/max_ents[G]
-  u64, run_start/run_term[G*8] u64, match/next/pending_snapshot[S] u64,
+  u64, run_start/run_term[8*G] u64 (run-major: run r of group g at r*G+g), match/next/pending_snapshot[S] u64,
   pstate[S] u8 (state | ProbeSent 0x4 | RecentActive 0x8), infl_pos[S] u32
   (start | count << 16), infl_buf[S*inflight_cap] u64, rq_ctx/rq_index
   [G*readq_cap] u64, rq_meta[G*readq_cap] u32 (acks | from << 16).
@@ -227,8 +227,8 @@ def synth_streaming(G: int, W: int = 32, D: int = 4, n: int = 5, device="cuda"):
     i32 = lambda x: x.to(torch.int32)
     runs = torch.zeros(G * MAX_RUNS, dtype=torch.int64, device=dev)
     runs_t = torch.zeros_like(runs)
-    runs[::MAX_RUNS] = base - 51
-    runs_t[::MAX_RUNS] = 7
+    runs[:G] = base - 51  # run 0 of every group (run-major)
+    runs_t[:G] = 7
     slot = torch.arange(S, dtype=torch.int64, device=dev) % n
     gs = torch.arange(S, dtype=torch.int64, device=dev) // n
     bs, ls = base[gs], last[gs]

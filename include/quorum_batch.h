@@ -376,8 +376,9 @@ typedef struct qb_leader_groups {
   const uint64_t* snap_index;  /* [G] storage snapshot index, 0 = unavailable */
   const uint64_t* snap_term;   /* [G]                                      */
   const uint64_t* max_ents;    /* [G] entries per MsgApp (>= 1)            */
-  const uint64_t* run_start;   /* [G * QB_LEADER_MAX_RUNS] ascending        */
-  const uint64_t* run_term;    /* [G * QB_LEADER_MAX_RUNS]                  */
+  const uint64_t* run_start;   /* [QB_LEADER_MAX_RUNS * G] run-major: run r of
+                                  group g at r * G + g; ascending in r        */
+  const uint64_t* run_term;    /* [QB_LEADER_MAX_RUNS * G] same layout      */
   /* per slot, S = off[G] (in/out) */
   uint64_t* match;
   uint64_t* next;

@@ -31,7 +31,6 @@ typedef uint32_t u32;
 typedef uint16_t u16;
 typedef uint8_t u8;
 
-#define RUNS 8
 #define NOSLOT 0xFFu
 #define P_PROBE 0
 #define P_REPL 1
@@ -102,7 +101,7 @@ static u64 term_of(const ctx* c, u64 i) {
   u32 nr = (L->meta[c->g] >> 16) & 0xF;
   u64 t = 0;
   for (u32 r = 0; r < nr; ++r)
-    if (L->run_s[c->g * RUNS + r] <= i) t = L->run_t[c->g * RUNS + r];
+    if (L->run_s[r * L->G + c->g] <= i) t = L->run_t[r * L->G + c->g];  /* run-major */
   return t;
 }
 

@@ -42,8 +42,8 @@ def pack(groups, inflight_cap: int, readq_cap: int):
         a["snap_term"][i] = g.log.snap_term
         a["max_ents"][i] = g.log.max_ents
         for r, (st, t) in enumerate(g.log.runs):
-            a["run_start"][i * MAX_RUNS + r] = st
-            a["run_term"][i * MAX_RUNS + r] = t
+            a["run_start"][r * G + i] = st  # run-major
+            a["run_term"][r * G + i] = t
         for j, p in enumerate(g.prs):
             s = int(off[i]) + j
             a["match"][s] = p.match
@@ -166,11 +166,16 @@ def random_groups(rng: np.random.Generator, G: int, inflight_cap: int, readq_cap
     return groups
 
 
-def random_records(rng: np.random.Generator, groups, M: int, bad_frac: float = 0.01):
+def random_records(rng: np.random.Generator, groups, M: int, bad_frac: float = 0.01,
+                   hot_groups: int = 0, hot_frac: float = 0.0):
+    """M random inbox records; with hot_groups, a hot_frac share of them goes
+    to the first hot_groups groups (long per-group runs, crowded chunks)."""
     G = len(groups)
     recs = []
     for _ in range(M):
         gi = int(rng.integers(0, G))
+        if hot_groups and rng.random() < hot_frac:
+            gi = int(rng.integers(0, hot_groups))
         if rng.random() < bad_frac:
             recs.append((G + int(rng.integers(0, 5)), L.Inbound(0, 0, 1, 1)))
             continue

@@ -68,12 +68,13 @@ def test_reference_scenarios_on_device(sc):
         assert LP.state_key(g) == LP.state_key(twin), where
 
 
-def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9):
+def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_groups=0,
+          hot_frac=0.0):
     rng = np.random.default_rng(seed)
     groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots)
     for g in groups:
         g.read_only = read_only
-    recs = LP.random_records(rng, groups, M)
+    recs = LP.random_records(rng, groups, M, hot_groups=hot_groups, hot_frac=hot_frac)
     eng = _engine(groups, inflight_cap, readq_cap, read_only)
     res = eng.step(_inbox(recs))
     orc = copy.deepcopy(groups)
@@ -113,6 +114,24 @@ def test_fuzz_lease_based_and_wide():
 
 def test_fuzz_larger():
     _fuzz(21, G=5000, M=12000, inflight_cap=8, readq_cap=4)
+
+
+def test_fuzz_long_runs():
+    """Groups with ~100 records in one batch (runs ordered outside LDS),
+    chunks still placed through LDS."""
+    _fuzz(41, G=600, M=2000, inflight_cap=6, readq_cap=3, hot_groups=2, hot_frac=0.1)
+
+
+def test_fuzz_crowded_chunk():
+    """A chunk with more records than the LDS placement holds (> 1536)."""
+    _fuzz(42, G=300, M=5000, inflight_cap=6, readq_cap=3, hot_groups=3, hot_frac=0.5)
+
+
+def test_fuzz_atomic_grouping(monkeypatch):
+    """The grouping used beyond the bucket geometry (> 134M groups per
+    shard): per-record global atomics, then the same gather and step."""
+    monkeypatch.setenv("QB_LEADER_GROUPING", "atomic")
+    _fuzz(31, G=3000, M=9000, inflight_cap=6, readq_cap=3, max_slots=16)
 
 
 def test_empty_batch_and_truncated_output():
