@@ -31,9 +31,8 @@
 //                    messages into an 8-slot per-group area of the workspace,
 //                    spilling into 32-message chunks from a shared pool
 //   L5 scan          exclusive scan of the message counts
-//   L6 k_ld_emit     each workgroup copies its groups' messages, word by word,
-//                    into their final place (group order, emission order
-//                    within a group)
+//   L6 k_ld_emit     each group's messages copied to their final place
+//                    (group order, emission order within a group)
 // Only L4 is control-heavy; it touches a group's state only if the group has
 // records.
 #include <cstdlib>
@@ -47,6 +46,7 @@ namespace ld {
 
 constexpr u32 kFix = 8;         // messages per group kept in the fixed area
 constexpr u32 kChunk = 32;      // messages per overflow chunk
+constexpr u32 kEmitStage = 1024;  // messages per workgroup staged by k_ld_emit
 constexpr u32 kNone = 0xFFFFFFFFu;
 constexpr u8 kNoSlot = 0xFF;
 
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
   ctot[c] = s;
 }
 
-constexpr u32 kStageRecs = 1536;  // chunk records placed through LDS
+constexpr u32 kStageRecs = 1024;  // chunk records placed through LDS
 constexpr u32 kLdsSortMax = 64;   // longer runs are ordered in HBM
 struct ChunkStage {
   u64 mr[kStageRecs];
@@ -986,9 +986,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
 }
 
 // ------------------------------------------------------------------ L6 ----
-// Block-cooperative copy: the block's groups own one contiguous range of the
-// output; lanes copy it word by word (5 u64 per message), so the writes are
-// fully coalesced and the reads are runs of each group's staged messages.
+// Each group's staged messages to their final place (msg_off = the scan of
+// the counts), the workgroup's output range written with coalesced word
+// stores.  Messages past msg_cap are counted as dropped.
 __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict__ moff,
                                                     const Msg* __restrict__ fix,
                                                     const u32* __restrict__ chead,
@@ -1009,31 +1009,52 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
     *msg_total = lo[ng];
   }
   const u64 m0 = lo[0], m1 = lo[ng];
-  const u64 w1 = (m1 < cap ? m1 : (m0 < cap ? cap : m0)) * 5;
   const u64* fw = reinterpret_cast<const u64*>(fix);
   const u64* cw = reinterpret_cast<const u64*>(chunks);
   u64* ow = reinterpret_cast<u64*>(out);
-  for (u64 w = m0 * 5 + threadIdx.x; w < w1; w += kBlock) {
-    const u64 idx = w / 5;
-    const u32 word = u32(w - idx * 5);
-    // the group owning message idx: last t with lo[t] <= idx (binary search)
-    u32 a = 0, b = ng;  // invariant lo[a] <= idx < lo[b]
-    while (b - a > 1) {
-      const u32 m = (a + b) >> 1;
-      if (lo[m] <= idx) a = m;
-      else b = m;
+  const u32 t = threadIdx.x;
+  const u32 n = t < ng ? lo[t + 1] - lo[t] : 0u;
+  const u64 w1 = (m1 < cap ? m1 : (m0 < cap ? cap : m0)) * 5;  // end of the words kept
+  if (m1 - m0 <= kEmitStage && !__syncthreads_or(n > kFix)) {
+    // The workgroup's messages (all in the fixed area) are gathered into LDS
+    // row by row of the k-major area (coalesced reads), then stored as one
+    // contiguous run of words (coalesced writes).
+    __shared__ u64 words[kEmitStage * 5];
+    const u32 mo = lo[t < ng ? t : 0] - u32(m0);
+    for (u32 k = 0; k < kFix; ++k) {
+      if (!__syncthreads_or(k < n)) break;
+      if (k < n) {
+        const u64* src = fw + (u64(k) * G + g0 + t) * 5;
+#pragma unroll
+        for (int w = 0; w < 5; ++w) words[(mo + k) * 5 + w] = src[w];
+      }
     }
-    const u64 g = g0 + a;
-    const u32 k = u32(idx - lo[a]);
-    u64 v;
-    if (k < kFix) {
-      v = fw[(u64(k) * G + g) * 5 + word];
-    } else {
-      u32 c = chead[g];
-      for (u32 hop = (k - kFix) / kChunk; hop; --hop) c = cnext[c];
-      v = cw[(u64(c) * kChunk + (k - kFix) % kChunk) * 5 + word];
+    __syncthreads();
+    for (u64 w = m0 * 5 + t; w < w1; w += kBlock) ow[w] = words[w - m0 * 5];
+  } else {
+    // Word by word over the workgroup's output range (any message count).
+    for (u64 w = m0 * 5 + t; w < w1; w += kBlock) {
+      const u64 idx = w / 5;
+      const u32 word = u32(w - idx * 5);
+      // the group owning message idx: last a with lo[a] <= idx (binary search)
+      u32 a = 0, b = ng;  // invariant lo[a] <= idx < lo[b]
+      while (b - a > 1) {
+        const u32 m = (a + b) >> 1;
+        if (lo[m] <= idx) a = m;
+        else b = m;
+      }
+      const u64 g = g0 + a;
+      const u32 k = u32(idx - lo[a]);
+      u64 v;
+      if (k < kFix) {
+        v = fw[(u64(k) * G + g) * 5 + word];
+      } else {
+        u32 c = chead[g];
+        for (u32 hop = (k - kFix) / kChunk; hop; --hop) c = cnext[c];
+        v = cw[(u64(c) * kChunk + (k - kFix) % kChunk) * 5 + word];
+      }
+      ow[w] = v;
     }
-    ow[w] = v;
   }
   if (threadIdx.x == 0 && m1 > cap) {
     const u64 dropped = m1 - (m0 > cap ? m0 : cap);
