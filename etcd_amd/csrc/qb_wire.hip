@@ -67,6 +67,39 @@ struct GlobalSrc {
 
 // The generated decoders' varint loop: error at shift >= 64 or at l.
 template <class Src>
+__device__ __forceinline__ bool varint(const Src& s, u64& i, u64 l, u64& v);
+
+// Straight-line varint for the fast prefix: from the LDS stage, the 8 bytes
+// at i come from two aligned 8-byte LDS reads, the terminator is the lowest
+// byte with its high bit clear and the 7-bit groups are compacted with
+// shifts and masks (no per-byte loop, no divergence); a varint longer than 8
+// bytes takes the byte loop.  Bytes at or past l never decide the result: a
+// terminator found there is the same EOF error the byte loop reports.
+template <class Src>
+__device__ __forceinline__ bool varint_fast(const Src& s, u64& i, u64 l, u64& v) {
+  return varint(s, i, l, v);
+}
+template <>
+__device__ __forceinline__ bool varint_fast<LdsSrc>(const LdsSrc& s, u64& i, u64 l, u64& v) {
+  const u64 off = i - s.base;
+  const u64* w = reinterpret_cast<const u64*>(s.lds) + (off >> 3);
+  const u32 sh = u32(off & 7u) * 8u;
+  const u64 lo = w[0], hi = w[1];
+  const u64 x = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+  const u64 stop = ~x & 0x8080808080808080ull;
+  if (stop == 0) return varint(s, i, l, v);
+  const u32 n = (u32(__builtin_ctzll(stop)) >> 3) + 1u;  // bytes in the varint
+  if (i + n > l) return false;
+  const u64 xm = n == 8 ? x : x & ((1ull << (8u * n)) - 1u);
+  v = (xm & 0x7Full) | ((xm >> 1) & (0x7Full << 7)) | ((xm >> 2) & (0x7Full << 14)) |
+      ((xm >> 3) & (0x7Full << 21)) | ((xm >> 4) & (0x7Full << 28)) |
+      ((xm >> 5) & (0x7Full << 35)) | ((xm >> 6) & (0x7Full << 42)) |
+      ((xm >> 7) & (0x7Full << 49));
+  i += n;
+  return true;
+}
+
+template <class Src>
 __device__ __forceinline__ bool varint(const Src& s, u64& i, u64 l, u64& v) {
   v = 0;
   for (u32 shift = 0;; shift += 7) {
@@ -197,10 +230,52 @@ __device__ __forceinline__ bool unmarshal(const Src& s, u64 i, const u64 l, Fiel
   return true;
 }
 
+// gogoproto's Marshal writes a Message's fields in field-number order, every
+// non-nullable one always (raft.pb.go MarshalToSizedBuffer): type, to, from,
+// term, logTerm, index, [entries], commit, snapshot, reject, rejectHint,
+// [context].  fast_prefix consumes the longest prefix of the message that
+// follows that order with one-byte keys, in straight-line code (no per-field
+// dispatch, so the lanes of a wave stay converged), and the generic loop
+// continues from there.  Unmarshal is a left fold over the fields, so the
+// result is the generic decoder's on any input: a field is consumed here
+// only when its key byte is the expected one-byte key, and it is then
+// decoded exactly as the generic loop decodes it.  The snapshot is consumed
+// only in its common empty form (12 00: an empty SnapshotMetadata).
+template <class Src>
+__device__ __forceinline__ bool fast_prefix(const Src& s, u64& i, const u64 l, Fields& f) {
+#define QB_FAST_VARINT(KEY, DST)                     \
+  {                                                  \
+    if (i >= l || s.at(i) != (KEY)) return true;     \
+    u64 i2 = i + 1, v;                               \
+    if (!varint_fast(s, i2, l, v)) return false;     \
+    DST = v;                                         \
+    i = i2;                                          \
+  }
+  u64 ignored;
+  QB_FAST_VARINT(0x08, f.type)
+  QB_FAST_VARINT(0x10, ignored)
+  QB_FAST_VARINT(0x18, f.from)
+  QB_FAST_VARINT(0x20, f.term)
+  QB_FAST_VARINT(0x28, f.log_term)
+  QB_FAST_VARINT(0x30, f.index)
+  QB_FAST_VARINT(0x40, ignored)
+  if (i + 4 > l || s.at(i) != 0x4A || s.at(i + 1) != 0x02 || s.at(i + 2) != 0x12 ||
+      s.at(i + 3) != 0x00)
+    return true;
+  i += 4;
+  QB_FAST_VARINT(0x50, f.reject)
+  QB_FAST_VARINT(0x58, f.hint)
+#undef QB_FAST_VARINT
+  (void)ignored;
+  return true;
+}
+
 template <class Src>
 __device__ __forceinline__ bool unmarshal_message(const Src& s, u64 start, u64 end, Fields& f) {
   f = Fields{};
-  return unmarshal<K_MESSAGE>(s, start, end, &f);
+  u64 i = start;
+  if (!fast_prefix(s, i, end, f)) return false;
+  return unmarshal<K_MESSAGE>(s, i, end, &f);
 }
 
 __device__ __forceinline__ int kind_of_type(u64 type32) {
@@ -231,6 +306,14 @@ struct Args {
 // One message: decode, classify, map From to its slot, write the record.
 template <class Src>
 __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u64 p0, u64 p1) {
+  // The group's slot range is loaded first: its latency (a random row of
+  // off) overlaps the parse instead of following it.
+  const u32 mg = A.mgroup[m];
+  u32 s0 = 0, s1 = 0;
+  if (mg < A.G) {
+    s0 = A.off[mg];
+    s1 = A.off[mg + 1];
+  }
   Fields f;
   int st_;
   u32 group = 0xFFFFFFFFu;
@@ -258,15 +341,21 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
         }
       }
       if (st_ == QB_WIRE_OK) {
-        group = A.mgroup[m];
+        group = mg;
         u32 slot = QB_REC_NO_PROGRESS;
         if (group < A.G) {
-          const u32 s0 = A.off[group], s1 = A.off[group + 1];
-          for (u32 j = s0; j < s1; ++j)
-            if (A.ids[j] == f.from) {
-              slot = j - s0;
-              break;
-            }
+          // The first kIdBatch IDs are loaded together (one round trip),
+          // wider configs continue one by one.
+          constexpr u32 kIdBatch = 8;
+          const u32 n = s1 - s0;
+          u64 id[kIdBatch];
+#pragma unroll
+          for (u32 k = 0; k < kIdBatch; ++k) id[k] = k < n ? A.ids[s0 + k] : 0ull;
+#pragma unroll
+          for (u32 k = kIdBatch; k-- > 0;)
+            if (k < n && id[k] == f.from) slot = k;
+          for (u32 j = s0 + kIdBatch; j < s1 && slot == QB_REC_NO_PROGRESS; ++j)
+            if (A.ids[j] == f.from) slot = j - s0;
         }
         flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
         term = f.term;
@@ -288,7 +377,7 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
 }
 
 __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
-  __shared__ __attribute__((aligned(16))) u8 stage[kStage];
+  __shared__ __attribute__((aligned(16))) u8 stage[kStage + 16];  // + window over-read
   __shared__ u32 lds[4];
   BlockTally<4> tally;
   const u64 m0 = u64(blockIdx.x) * kBlock;

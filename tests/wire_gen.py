@@ -38,6 +38,12 @@ def random_message(r, ids):
         b = bytes(bb)
     elif x < 0.20:  # minimal encodings (google-style: only set fields)
         b = W._key(1, 0) + W.varint(t) + W._key(3, 0) + W.varint(frm) + W._key(6, 0) + W.varint(7)
+    elif x < 0.26:  # fields repeated after the canonical run (the last one wins)
+        extra = r.choice([(1, r.choice([4, 9, 11, 3])), (3, frm), (4, rand_u64(r)), (6, rand_u64(r)),
+                          (10, r.randint(0, 1)), (11, rand_u64(r))])
+        b = b + W._key(extra[0], 0) + W.varint(extra[1])
+    elif x < 0.30:  # canonical run broken midway (a field moved to the front)
+        b = W._key(6, 0) + W.varint(rand_u64(r)) + b
     return b
 
 
