@@ -31,9 +31,15 @@ namespace cc {
 constexpr int kBlk = 128;
 constexpr int kTab = 24;  // working table: 16 old slots + up to 8 new IDs
 
+// A thread's working table, column-major in the workgroup's LDS block
+// (entry k of thread t at [k][t]): the lanes of a wave touch consecutive
+// words, so table accesses are free of bank conflicts (a per-thread row of
+// 24 u64 put every 4th lane on the same bank).
 struct Tab {
-  u64 id[kTab];
+  u64* col;  // &lds[0][threadIdx.x]
+  __device__ __forceinline__ u64& id(int k) const { return col[k * kBlk]; }
 };
+__device__ __forceinline__ Tab tab_of(u64 (*lds)[kBlk]) { return Tab{&lds[0][threadIdx.x]}; }
 
 struct Args {
   u64 G;
@@ -75,7 +81,7 @@ struct Roles {
 
 __device__ __forceinline__ int find(const Tab& t, int n, u64 id) {
   for (int k = 0; k < n; ++k)
-    if (t.id[k] == id) return k;
+    if (t.id(k) == id) return k;
   return -1;
 }
 
@@ -86,7 +92,7 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
   auto first = [&](u32 m) {
     u64 best = ~0ull;
     for (int k = 0; k < r.n; ++k)
-      if ((m >> k) & 1u && t.id[k] < best) best = t.id[k];
+      if ((m >> k) & 1u && t.id(k) < best) best = t.id(k);
     return best;
   };
   const u32 members = r.in | r.out | r.lrn | r.lnext;
@@ -103,13 +109,13 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
 // Replays group g's operation.  On success fills the table/roles of the new
 // config and returns 0; otherwise an error code (the table then holds the
 // old config).  Roles.fresh marks entries whose Progress is (re)created.
-__device__ int replay(const Args& A, u64 g, Tab& t, Roles& r, bool& autoleave, u64* bad,
+__device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autoleave, u64* bad,
                       int* n_old) {
   const u32 s0 = A.off[g], s1 = A.off[g + 1];
   const u32 ns = s1 - s0;
   const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
   r = Roles{};
-  for (u32 j = 0; j < ns; ++j) t.id[j] = A.ids[s0 + j];
+  for (u32 j = 0; j < ns; ++j) t.id(j) = A.ids[s0 + j];
   r.n = int(ns);
   *n_old = int(ns);
   r.in = c & 0xFFFFu;
@@ -157,7 +163,7 @@ __device__ int replay(const Args& A, u64 g, Tab& t, Roles& r, bool& autoleave, u
         if (x < 0) {
           if (r.n >= kTab) return QB_CCERR_TOO_MANY_SLOTS;
           x = r.n++;
-          t.id[x] = id;
+          t.id(x) = id;
         }
         const u32 b = 1u << x;
         r.prs |= b;
@@ -216,10 +222,10 @@ __device__ int replay(const Args& A, u64 g, Tab& t, Roles& r, bool& autoleave, u
 }
 
 __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
-  __shared__ Tab tabs[kBlk];
+  __shared__ u64 tabs[kTab][kBlk];
   const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
   if (g >= A.G) return;
-  Tab& t = tabs[threadIdx.x];
+  Tab t = tab_of(tabs);
   Roles r;
   bool al;
   u64 bad = 0;
@@ -230,63 +236,125 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
   if (A.err_id) A.err_id[g] = rc ? bad : 0;
 }
 
+// Carried Progress and inflight rings are copied by the whole workgroup
+// after the per-group pass: each thread lists its new slots' (destination,
+// source) pairs in LDS, then lanes copy rows (and consecutive words of the
+// rings) with loads batched ahead of stores.  The per-group pass itself
+// only stores, so its stores never stall a later load (gfx9 counts loads
+// and stores on one vector memory counter).
+constexpr u32 kNoSrc = 0xFFFFFFFFu;
+constexpr u32 kRows = kBlk * QB_MAX_SLOTS;
+
 __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
-  __shared__ Tab tabs[kBlk];
+  __shared__ u64 tabs[kTab][kBlk];
+  __shared__ u32 row_dst[kRows], row_src[kRows];
+  __shared__ u32 nrows;
+  if (threadIdx.x == 0) nrows = 0;
+  __syncthreads();
   const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
-  if (g >= A.G) return;
-  Tab& t = tabs[threadIdx.x];
-  Roles r;
-  bool al;
-  u64 bad = 0;
-  int n_old;
-  int rc = replay(A, g, t, r, al, &bad, &n_old);
-  const u32 s0 = A.off[g];
-  const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
-  if (d1 > A.S_cap) return;  // caller's capacity exceeded (reported by the host call)
-  if (rc) {  // the old config is kept
-    r = Roles{};
-    r.n = n_old;
-    r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
-    const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
-    r.in = c & 0xFFFFu;
-    r.out = c >> 16;
-    r.lnext = e & 0xFFFFu;
-    al = (e >> 16) & 1u;
-  }
-  // surviving entries in ascending ID order (selection over <= 24 entries)
-  u32 left = r.prs, ncfg_in = 0, ncfg_out = 0, nlnext = 0;
-  const u64 last = A.last_index[g];
-  for (u32 j = 0; left; ++j) {
-    int best = -1;
-    for (int k = 0; k < r.n; ++k)
-      if (((left >> k) & 1u) && (best < 0 || t.id[k] < t.id[best])) best = k;
-    left &= ~(1u << best);
-    const u32 b = 1u << best;
-    if (r.in & b) ncfg_in |= 1u << j;
-    if (r.out & b) ncfg_out |= 1u << j;
-    if (r.lnext & b) nlnext |= 1u << j;
-    const u64 d = d0 + j;
-    A.n_ids[d] = t.id[best];
-    if (best < n_old && !(r.fresh & b)) {  // carried Progress (checkAndCopy's shallow copy)
-      const u64 o = u64(s0) + best;
-      A.n_match[d] = A.match[o];
-      A.n_next[d] = A.next[o];
-      A.n_psnap[d] = A.psnap[o];
-      A.n_pstate[d] = A.pstate[o];
-      A.n_infl_pos[d] = A.infl_pos[o];
-      for (u32 q = 0; q < A.K; ++q) A.n_infl_buf[d * A.K + q] = A.infl_buf[o * A.K + q];
-    } else {  // initProgress (confchange.go:258-281)
-      A.n_match[d] = 0;
-      A.n_next[d] = last;
-      A.n_psnap[d] = 0;
-      A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
-      A.n_infl_pos[d] = 0;
-      for (u32 q = 0; q < A.K; ++q) A.n_infl_buf[d * A.K + q] = 0;
+  if (g < A.G) {
+    Tab t = tab_of(tabs);
+    Roles r;
+    bool al;
+    u64 bad = 0;
+    int n_old;
+    int rc = replay(A, g, t, r, al, &bad, &n_old);
+    const u32 s0 = A.off[g];
+    const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
+    if (d1 <= A.S_cap) {  // else the caller's capacity is exceeded (reported by the host call)
+      if (rc) {  // the old config is kept
+        r = Roles{};
+        r.n = n_old;
+        r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
+        const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
+        r.in = c & 0xFFFFu;
+        r.out = c >> 16;
+        r.lnext = e & 0xFFFFu;
+        al = (e >> 16) & 1u;
+      }
+      // surviving entries in ascending ID order (selection over <= 24 entries)
+      u32 left = r.prs, ncfg_in = 0, ncfg_out = 0, nlnext = 0;
+      const u64 last = A.last_index[g];
+      const u32 nnew = u32(__popc(r.prs));
+      const u32 row0 = atomicAdd(&nrows, nnew);
+      for (u32 j = 0; left; ++j) {
+        int best = -1;
+        for (int k = 0; k < r.n; ++k)
+          if (((left >> k) & 1u) && (best < 0 || t.id(k) < t.id(best))) best = k;
+        left &= ~(1u << best);
+        const u32 b = 1u << best;
+        if (r.in & b) ncfg_in |= 1u << j;
+        if (r.out & b) ncfg_out |= 1u << j;
+        if (r.lnext & b) nlnext |= 1u << j;
+        const u64 d = d0 + j;
+        A.n_ids[d] = t.id(best);
+        u32 src = kNoSrc;
+        if (best < n_old && !(r.fresh & b)) {  // carried Progress (checkAndCopy's shallow copy)
+          src = s0 + u32(best);                // copied by the workgroup below
+        } else {  // initProgress (confchange.go:258-281)
+          A.n_match[d] = 0;
+          A.n_next[d] = last;
+          A.n_psnap[d] = 0;
+          A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
+          A.n_infl_pos[d] = 0;
+        }
+        row_dst[row0 + j] = u32(d);
+        row_src[row0 + j] = src;
+      }
+      A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
+      A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
     }
   }
-  A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
-  A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
-  (void)d1;
+  __syncthreads();
+  // Carried Progress: four rows per lane in flight (all loads, then all
+  // stores), so loads do not queue behind earlier stores on the shared
+  // vector memory counter.
+  const u32 nr = nrows;
+  for (u32 e0 = threadIdx.x; e0 < nr; e0 += 4 * kBlk) {
+    u64 m[4], nx[4], ps[4];
+    u32 ip[4];
+    u8 st[4];
+    u32 dst[4];
+    bool on[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32 e = e0 + u32(q) * kBlk;
+      const u32 src = e < nr ? row_src[e] : kNoSrc;
+      on[q] = src != kNoSrc;
+      dst[q] = e < nr ? row_dst[e] : 0u;
+      m[q] = on[q] ? A.match[src] : 0ull;
+      nx[q] = on[q] ? A.next[src] : 0ull;
+      ps[q] = on[q] ? A.psnap[src] : 0ull;
+      ip[q] = on[q] ? A.infl_pos[src] : 0u;
+      st[q] = on[q] ? A.pstate[src] : u8(0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!on[q]) continue;
+      A.n_match[dst[q]] = m[q];
+      A.n_next[dst[q]] = nx[q];
+      A.n_psnap[dst[q]] = ps[q];
+      A.n_infl_pos[dst[q]] = ip[q];
+      A.n_pstate[dst[q]] = st[q];
+    }
+  }
+  if (A.K == 0) return;  // uniform
+  const u32 K = A.K, words = nr * K;
+  constexpr int kB = 8;  // words per lane in flight
+  for (u32 w0 = threadIdx.x; w0 < words; w0 += kB * kBlk) {
+    u64 v[kB], at[kB];
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      const u32 w = w0 + u32(q) * kBlk;
+      const u32 e = w < words ? w / K : 0u, k = w - e * K;
+      const u32 src = w < words ? row_src[e] : kNoSrc;
+      at[q] = w < words ? u64(row_dst[e]) * K + k : ~0ull;
+      v[q] = src == kNoSrc ? 0ull : A.infl_buf[u64(src) * K + k];
+    }
+#pragma unroll
+    for (int q = 0; q < kB; ++q)
+      if (at[q] != ~0ull) A.n_infl_buf[at[q]] = v[q];
+  }
 }
 
 }  // namespace cc
