@@ -256,7 +256,7 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": f"k_fixed<{n},4,true,true>",
+                "kernel": f"k_fixed<{n},2,true,true>",
                 "bytes_per_group": bpg,
                 "avg_kernel_us": avg_kernel_s * 1e6,
                 "timing": (f"HIP events around the timed region on the launch streams; per-launch "

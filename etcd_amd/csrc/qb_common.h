@@ -134,6 +134,32 @@ struct BlockTally {
   }
 };
 
+// ------------------------------------------------------------- LDS-DMA ---
+// global_load_lds_dwordx4: each lane's 16 bytes land at the wave-uniform LDS
+// base (M0) + lane * 16, with no VGPR destination.  A staging loop of plain
+// loads (load -> wait -> ds_write per iteration) pays one HBM round trip per
+// iteration; the DMA form issues every piece of a run back to back and the
+// block's next __syncthreads() (which waits vmcnt(0)) retires them all.
+using lds_void_t = __attribute__((address_space(3))) void;
+using gbl_cvoid_t = const __attribute__((address_space(1))) void;
+
+// Stage n 16-byte pieces src[0..n) into lds[0..n).  Every thread of the
+// block calls it; the caller's __syncthreads() makes the run visible.
+// BLOCK * MAXIT must cover n.  Nontemporal (the run is read once).
+template <int BLOCK, int MAXIT>
+__device__ __forceinline__ void stage16_lds(void* lds, const void* src, u32 n) {
+  const u32 wave_base = threadIdx.x & ~63u;
+#pragma unroll
+  for (int k = 0; k < MAXIT; ++k) {
+    const u32 i = u32(k) * BLOCK + threadIdx.x;
+    if (i < n) {
+      char* dst = static_cast<char*>(lds) + 16u * (u32(k) * BLOCK + wave_base);
+      __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)(static_cast<const char*>(src) + 16ull * i),
+                                       (lds_void_t*)dst, 16, 0, 2);
+    }
+  }
+}
+
 inline unsigned grid_for(u64 threads, unsigned block = kBlock) {
   return unsigned((threads + block - 1) / block);
 }

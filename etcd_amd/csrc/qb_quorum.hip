@@ -214,85 +214,20 @@ extern "C" int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_
 // -------------------------------------------------------------------- CSR ---
 //
 // A workgroup owns kBlock consecutive groups.  Their slots are one contiguous
-// run of match[] (group-major CSR), so the run is staged into LDS with
-// coalesced 16-byte nontemporal loads and each thread then reads its own
-// slots from LDS.  Non-member slots (learners, the other half) are fed as 0:
-// zeros sort to the bottom and leave the q-th largest unchanged for q <= n,
-// exactly the fill-with-zero of majority.go:149-161.
+// run of match[] (group-major CSR), staged into LDS by LDS-DMA
+// (global_load_lds_dwordx4, every piece issued before the one wait at the
+// barrier: a load -> wait -> ds_write loop paid one HBM round trip per
+// iteration, 276 -> 203 us at 16M ragged groups).  Each thread then gathers
+// the members of each half of its config from LDS (non-members: learners,
+// the other half) and selects that half's q-th largest (half_ci).
 //
-// Occupancy is what sets this kernel's speed: the table's
-// max_slots bound (WMAX) caps both the LDS run buffer (kBlock * WMAX u64) and
-// the widest compare-exchange network compiled in, which sets the VGPR count.
-// Within that bound the network width W in {4, 8, 12, 16} is chosen per wave
-// from the wave's widest group (uniform branch).  Majority-only waves run one
-// masked sort; a wave with a joint group runs one sort of all slots carrying
-// 2-bit membership tags and reads both halves' q-th largest from it.
+// The table's max_slots bound (WMAX) caps the LDS run buffer (kBlock * WMAX
+// u64) and the widest network compiled in; within it the network width is
+// the wave's largest member count (uniform branch).  Compacting the members
+// first makes a 5+5 joint config two 5-wide sorts instead of one tagged
+// 10-wide sort (8M joint groups 134 -> 106 us), DESIGN.md §3.2.
 
 namespace qb {
-
-template <int W>
-__device__ __forceinline__ u64 csr_select(const u64* src, u32 s, u32 mask) {
-  u64 v[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) v[j] = (u32(j) < s && ((mask >> j) & 1u)) ? src[j] : 0ull;
-  sort_net<W>(v);
-  const int n = __popc(mask);
-  if (n == 0) return kInf;  // majority.go:128-133
-  const int want = W - (n / 2 + 1);  // srt[n - (n/2+1)] shifted by W - n zeros
-  u64 r = 0;
-#pragma unroll
-  for (int j = 0; j < W; ++j) r = (j == want) ? v[j] : r;
-  return r;
-}
-
-__device__ __forceinline__ void cmpx_tag(u64& a, u64& b, u32& ta, u32& tb) {
-  const bool sw = b < a;
-  const u64 lo = sw ? b : a, hi = sw ? a : b;
-  const u32 tl = sw ? tb : ta, th = sw ? ta : tb;
-  a = lo;
-  b = hi;
-  ta = tl;
-  tb = th;
-}
-
-template <class Net, int... K>
-__device__ __forceinline__ void run_net_tag(u64* v, u32* t, std::integer_sequence<int, K...>) {
-  ((cmpx_tag(v[Net::A[K]], v[Net::B[K]], t[Net::A[K]], t[Net::B[K]])), ...);
-}
-
-// JointConfig.CommittedIndex (joint.go:49-56): one ascending sort of all
-// slots, tag bit 0 = incoming member, bit 1 = outgoing member; walking down
-// from the largest, the q-th member of a half is that half's CommittedIndex.
-// An empty half is ∞ and drops out of the min.
-template <int W>
-__device__ __forceinline__ u64 csr_joint(const u64* src, u32 s, u32 min_, u32 mout) {
-  u64 v[W];
-  u32 t[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) {
-    const bool live = u32(j) < s;
-    v[j] = live ? src[j] : 0ull;
-    t[j] = live ? (((min_ >> j) & 1u) | (((mout >> j) & 1u) << 1)) : 0u;
-  }
-  run_net_tag<SortNet<W>>(v, t, std::make_integer_sequence<int, SortNet<W>::K>{});
-  const int qi = __popc(min_) / 2 + 1, qo = __popc(mout) / 2 + 1;
-  int ci = 0, co = 0;
-  u64 ri = kInf, ro = kInf;
-#pragma unroll
-  for (int j = W - 1; j >= 0; --j) {
-    ci += int(t[j] & 1u);
-    co += int(t[j] >> 1);
-    ri = (ci == qi && (t[j] & 1u)) ? v[j] : ri;
-    ro = (co == qo && (t[j] >> 1)) ? v[j] : ro;
-  }
-  return ro < ri ? ro : ri;
-}
-
-template <int W>
-__device__ __forceinline__ u64 csr_ci(const u64* src, u32 s, u32 min_, u32 mout) {
-  if (__ballot(mout != 0) == 0) return csr_select<W>(src, s, min_);
-  return csr_joint<W>(src, s, min_, mout);
-}
 
 __device__ __forceinline__ u32 wave_max(u32 x) {
 #pragma unroll
@@ -303,21 +238,56 @@ __device__ __forceinline__ u32 wave_max(u32 x) {
   return __builtin_amdgcn_readfirstlane(x);  // wave-uniform, scalar branch
 }
 
-// Network width = the wave's widest group (exact, 4..WMAX): e.g. W = 11 for
-// a ragged wave with an 11-slot group (38 compare-exchanges vs 42 at 12).
-template <int W, int WMAX>
-__device__ __forceinline__ u64 csr_ci_width(u32 wmax, const u64* src, u32 s, u32 min_, u32 mout) {
-  if constexpr (W >= WMAX) {
-    return csr_ci<WMAX>(src, s, min_, mout);
+// MajorityConfig.CommittedIndex of one half (majority.go:126-172): the
+// members of `mask`, in slot order, compacted into M registers (M = the
+// wave's largest member count) and zero-padded — zeros sort below every value
+// and leave the q-th largest unchanged for q <= n, the fill-with-zero of
+// majority.go:149-161 — then sorted; the answer is ascending index
+// M - (n/2+1), picked by a conditional-move chain (no dynamic register
+// indexing, no scratch).  n = 0 is ∞ (majority.go:128-133).
+template <int M>
+__device__ __forceinline__ u64 half_ci(const u64* src, u32 mask) {
+  const int n = __popc(mask);
+  u64 v[M];
+  u32 m = mask;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const u32 j = m ? u32(__builtin_ctz(m)) : 0u;
+    v[k] = m ? src[j] : 0ull;
+    m &= m - 1u;
+  }
+  if constexpr (M >= 2) sort_net<M>(v);
+  const int want = M - (n / 2 + 1);
+  u64 r = 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) r = (j == want) ? v[j] : r;
+  return n == 0 ? kInf : r;
+}
+
+template <int M, int MAX>
+__device__ __forceinline__ u64 half_ci_width(u32 mw, const u64* src, u32 mask) {
+  if constexpr (M >= MAX) {
+    return half_ci<MAX>(src, mask);
   } else {
-    if (wmax <= u32(W)) return csr_ci<W>(src, s, min_, mout);
-    return csr_ci_width<W + 1, WMAX>(wmax, src, s, min_, mout);
+    if (mw <= u32(M)) return half_ci<M>(src, mask);
+    return half_ci_width<M + 1, MAX>(mw, src, mask);
   }
 }
 
+// JointConfig.CommittedIndex (joint.go:49-56) = min of the halves; an empty
+// outgoing half is ∞, so a plain majority config (mask_out = 0) is the
+// incoming half alone and a wave with no joint group skips the second half.
 template <int WMAX>
-__device__ __forceinline__ u64 csr_ci_dispatch(const u64* src, u32 s, u32 min_, u32 mout) {
-  return csr_ci_width<(WMAX < 4 ? WMAX : 4), WMAX>(wave_max(s), src, s, min_, mout);
+__device__ __forceinline__ u64 csr_ci(const u64* src, u32 s, u32 min_, u32 mout) {
+  const u32 live = s >= 32 ? ~0u : ((1u << s) - 1u);
+  min_ &= live;
+  mout &= live;
+  u64 c = half_ci_width<1, WMAX>(wave_max(u32(__popc(min_))), src, min_);
+  if (__ballot(mout != 0) != 0) {
+    const u64 c2 = half_ci_width<1, WMAX>(wave_max(u32(__popc(mout))), src, mout);
+    c = c2 < c ? c2 : c;
+  }
+  return c;
 }
 
 template <int WMAX, bool CI, bool VOTE>
@@ -352,15 +322,12 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
     // buffer (results for such a table are unspecified, never out of bounds).
     const u32 span = end - abase < kCap ? end - abase : kCap;
     const u32 npair = (span + 1u) >> 1;
-    using V = u32 __attribute__((ext_vector_type(4)));
-    for (u32 i = threadIdx.x; i < npair; i += kBlock) {
-      const u32 idx = abase + 2u * i;
-      if (idx + 1u < total) {
-        reinterpret_cast<V*>(lds)[i] = ld_nt(reinterpret_cast<const V*>(match + idx));
-      } else {
-        lds[2u * i] = match[idx];
-      }
-    }
+    // Pairs wholly inside match[0, total) go by LDS-DMA, all issued before
+    // any wait; only the array's last element can be an unpaired tail.
+    const u32 nfull = (abase + 2u * npair <= total) ? npair : npair - 1u;
+    constexpr int kIt = int((kCap / 2 + kBlock - 1) / kBlock);
+    stage16_lds<kBlock, kIt>(lds, match + abase, nfull);
+    if (threadIdx.x == 0 && nfull < npair) lds[2u * nfull] = match[abase + 2u * nfull];
     u32 lo = 0, s = 0;
     if (live) {
       lo = a - abase;
@@ -369,7 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_csr(u64 G, const u32* __restrict__ o
       lo = lo + s <= kCap ? lo : 0;
     }
     __syncthreads();
-    const u64 ci = csr_ci_dispatch<WMAX>(lds + lo, s, min_, mout);
+    const u64 ci = csr_ci<WMAX>(lds + lo, s, min_, mout);
     if (live) st_nt(commit + g, ci);
   }
   if constexpr (VOTE) {

@@ -58,13 +58,25 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
   __syncthreads();
   const u64 t0 = u64(blockIdx.x) * kTile;
   const u32 sbgroups = geo.CH * kChunksPerSb;
-  for (int k = 0; k < kTile / kBlock; ++k) {
+  // The tile's group / flag loads are all issued before the first LDS
+  // atomic (a load -> use loop waited one HBM round trip per iteration).
+  constexpr int kHistPer = kTile / kBlock;
+  u32 gg[kHistPer];
+  u8 ff[kHistPer];
+#pragma unroll
+  for (int k = 0; k < kHistPer; ++k) {
+    const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
+    gg[k] = i < geo.M ? rg[i] : 0xFFFFFFFFu;
+    ff[k] = i < geo.M ? rf[i] : u8(0);
+  }
+#pragma unroll
+  for (int k = 0; k < kHistPer; ++k) {
     const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
     bool bad = false, nonmember = false;
     if (i < geo.M) {
-      const u32 g = rg[i];
+      const u32 g = gg[k];
       bad = g >= geo.G;
-      nonmember = !bad && (rf[i] & 0x0Fu) >= geo.n;
+      nonmember = !bad && (ff[k] & 0x0Fu) >= geo.n;
       if (!bad && !nonmember) atomicAdd(&lh[g / sbgroups], 1u);
     }
     tally.add(0, bad);
@@ -272,14 +284,22 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
       vt[j] = k < nrec ? in.term[lo + k] : 0ull;
     }
   }
+  u64 vm[kPer];  // loaded together: one round trip, not one per record
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const u32 k = threadIdx.x + j * kPartThreads;
+    vm[j] = k < nrec ? in.mr[lo + k] : 0ull;
+  }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
-  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
-    const u64 mr = in.mr[lo + k];
-    const u16 b = u16((u32(mr) >> 10) & 127u);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const u32 k = threadIdx.x + j * kPartThreads;
+    if (k >= nrec) continue;
+    const u16 b = u16((u32(vm[j]) >> 10) & 127u);
     L.bin[k] = b;
     L.rank[k] = u16(atomicAdd(&start[b], 1u));
-    L.stage[k] = mr;
+    L.stage[k] = vm[j];
   }
   __syncthreads();
   tile_scan_bins(start, kChunksPerSb, L.wsum);
@@ -360,37 +380,57 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   // A higher-term record makes the sequential leader step down and ignore
   // everything after it (raft.go:875-879): then the updates are redone
   // below with the step-down order known.
+  // kRecPer records per thread are in flight at once: all three columns of
+  // each are loaded before the first is classified (one HBM round trip per
+  // kBlock * kRecPer records instead of two per kBlock).
+  constexpr int kRecPer = 4;
   for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);
-    for (u32 f0 = 0; f0 < total; f0 += kBlock) {
-      const u32 f = f0 + threadIdx.x;
-      bool stale = false, higher = false, applied = false, rejected = false;
-      if (f < total) {
-        const u32 i = rt.locate(f);
-        const u64 mr = recs.mr[i], term = recs.term[i];
-        const u32 meta = u32(mr), lg = meta & 1023u, s = (meta >> 17) & 15u;
-        const u64 gt = gterm[lg];
-        stale = term < gt;
-        higher = term > gt;
-        if (higher) {
-          atomicMin(&first_hi[lg], u32(mr >> 32));
-          any_higher = 1;
-        } else if (!stale) {
-          atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-          if (meta & (1u << 24)) {  // QB_REC_REJECT
-            rejected = true;                              // raft.go:1109: not MaybeUpdate
-          } else {
-            applied = true;
-            const u64 idx = recs.index[i];
-            atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
-            if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
-          }
+    for (u32 f0 = 0; f0 < total; f0 += kBlock * kRecPer) {
+      u64 rmr[kRecPer], rtm[kRecPer], rix[kRecPer];
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) {
+        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        rmr[r] = 0;
+        rtm[r] = 0;
+        rix[r] = 0;
+        if (f < total) {
+          const u32 i = rt.locate(f);
+          rmr[r] = recs.mr[i];
+          rtm[r] = recs.term[i];
+          rix[r] = recs.index[i];
         }
       }
-      tally.add(0, stale);
-      tally.add(1, higher);
-      tally.add(5, applied);
-      tally.add(6, rejected);
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) {
+        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        bool stale = false, higher = false, applied = false, rejected = false;
+        if (f < total) {
+          const u64 mr = rmr[r], term = rtm[r];
+          const u32 meta = u32(mr), lg = meta & 1023u, s = (meta >> 17) & 15u;
+          const u64 gt = gterm[lg];
+          stale = term < gt;
+          higher = term > gt;
+          if (higher) {
+            atomicMin(&first_hi[lg], u32(mr >> 32));
+            any_higher = 1;
+          } else if (!stale) {
+            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+            if (meta & (1u << 24)) {  // QB_REC_REJECT
+              rejected = true;                              // raft.go:1109: not MaybeUpdate
+            } else {
+              applied = true;
+              const u64 idx = rix[r];
+              atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
+              if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
+            }
+          }
+        }
+        tally.add(0, stale);
+        tally.add(1, higher);
+        tally.add(5, applied);
+        tally.add(6, rejected);
+      }
     }
   }
   __syncthreads();

@@ -96,9 +96,60 @@ __device__ __forceinline__ u64 ci32(const u64* src, u32 s, u32 mi, u32 mo) {
   return c2 < c ? c2 : c;
 }
 
+// ---- members of each half compacted (slot order) into M registers ----
+__device__ __forceinline__ u32 wmax_u32(u32 x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const u32 y = u32(__shfl_xor(int(x), o, 64));
+    x = y > x ? y : x;
+  }
+  return __builtin_amdgcn_readfirstlane(x);
+}
+template <int M>
+__device__ __forceinline__ u64 half_ci(const u64* src, u32 mask) {
+  const int n = __popc(mask);
+  u64 v[M];
+  u32 m = mask;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const u32 j = m ? u32(__builtin_ctz(m)) : 0u;
+    v[k] = m ? src[j] : 0ull;
+    m &= m - 1u;
+  }
+  if constexpr (M >= 2) sort_net<M>(v);
+  const int want = M - (n / 2 + 1);
+  u64 r = 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) r = (j == want) ? v[j] : r;
+  return n == 0 ? kInf : r;
+}
+template <int M, int MAX>
+__device__ __forceinline__ u64 half_ci_w(u32 mw, const u64* src, u32 mask) {
+  if constexpr (M >= MAX) {
+    return half_ci<MAX>(src, mask);
+  } else {
+    if (mw <= u32(M)) return half_ci<M>(src, mask);
+    return half_ci_w<M + 1, MAX>(mw, src, mask);
+  }
+}
+template <int MAX>
+__device__ __forceinline__ u64 ci_compact(const u64* src, u32 s, u32 mi, u32 mo) {
+  const u32 live = s >= 32 ? ~0u : ((1u << s) - 1u);
+  mi &= live;
+  mo &= live;
+  u64 c = half_ci_w<1, MAX>(wmax_u32(u32(__popc(mi))), src, mi);
+  if (__ballot(mo != 0) != 0) {
+    const u64 c2 = half_ci_w<1, MAX>(wmax_u32(u32(__popc(mo))), src, mo);
+    c = c2 < c ? c2 : c;
+  }
+  return c;
+}
+
 template <int MODE>  // 0 = 64-bit network, 1 = 32-bit offsets, 2 = memory floor
 __device__ __forceinline__ u64 eval(const u64* src, u32 s, u32 mi, u32 mo) {
-  if constexpr (MODE == 2) {
+  if constexpr (MODE == 3) {
+    return ci_compact<12>(src, s, mi, mo);
+  } else if constexpr (MODE == 2) {
     u64 x = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) x ^= (u32(j) < s) ? src[j] : 0ull;
@@ -124,7 +175,7 @@ __device__ __forceinline__ u8 vote_of(u32 mi, u32 mo, u32 w) {
 }
 
 // LDS-staged (product structure).  SMAX = max slots per group provisioned.
-template <int BLOCK, int SMAX, int MODE, bool NT>
+template <int BLOCK, int SMAX, int MODE, bool NT, bool DMA = false>
 __global__ __launch_bounds__(BLOCK) void k_lds(u64 G, const u32* __restrict__ off,
                                                const u64* __restrict__ match,
                                                const u32* __restrict__ cfg,
@@ -141,6 +192,11 @@ __global__ __launch_bounds__(BLOCK) void k_lds(u64 G, const u32* __restrict__ of
   const u32 abase = base & ~1u;
   const u32 npair = (end - abase + 1u) >> 1;
   using V = u32 __attribute__((ext_vector_type(4)));
+  if constexpr (DMA) {
+    const u32 nfull = (abase + 2u * npair <= total) ? npair : npair - 1u;
+    stage16_lds<BLOCK, (BLOCK * SMAX / 2 + BLOCK) / BLOCK>(lds, match + abase, nfull);
+    if (threadIdx.x == 0 && nfull < npair) lds[2u * nfull] = match[abase + 2u * nfull];
+  } else {
   for (u32 i = threadIdx.x; i < npair; i += BLOCK) {
     const u32 idx = abase + 2u * i;
     if (idx + 1u < total)
@@ -148,6 +204,7 @@ __global__ __launch_bounds__(BLOCK) void k_lds(u64 G, const u32* __restrict__ of
           NT ? ldn(reinterpret_cast<const V*>(match + idx)) : *reinterpret_cast<const V*>(match + idx);
     else
       lds[2u * i] = match[idx];
+  }
   }
   u32 lo = 0, s = 0;
   if (live) {
@@ -295,10 +352,10 @@ void L_cap(u64 G, const u32* off, const u64* m, const u32* cfg, const u32* vt, u
 using Launch = void (*)(u64, const u32*, const u64*, const u32*, const u32*, u64*, u8*,
                         hipStream_t);
 
-template <int BLOCK, int SMAX, int MODE, bool NT>
+template <int BLOCK, int SMAX, int MODE, bool NT, bool DMA = false>
 void L_lds(u64 G, const u32* off, const u64* m, const u32* cfg, const u32* vt, u64* c, u8* v,
            hipStream_t st) {
-  hipLaunchKernelGGL((k_lds<BLOCK, SMAX, MODE, NT>), dim3(unsigned((G + BLOCK - 1) / BLOCK)),
+  hipLaunchKernelGGL((k_lds<BLOCK, SMAX, MODE, NT, DMA>), dim3(unsigned((G + BLOCK - 1) / BLOCK)),
                      dim3(BLOCK), 0, st, G, off, m, cfg, vt, c, v);
 }
 template <int BLOCK, int MODE>
@@ -313,16 +370,13 @@ struct Variant {
   Launch fn;
 };
 const Variant kV[] = {
-    {"lds256_s12_net64", L_lds<256, 12, 0, false>},
-    {"lds128_s12_floor", L_lds<128, 12, 2, false>},
-    {"cap256_12_2sort", L_cap<256, 12, 0>},
-    {"cap256_10_2sort", L_cap<256, 10, 0>},
-    {"cap256_9_2sort", L_cap<256, 9, 0>},
-    {"cap128_12_2sort", L_cap<128, 12, 0>},
-    {"cap128_10_2sort", L_cap<128, 10, 0>},
-    {"cap256_10_tag", L_cap<256, 10, 1>},
-    {"cap128_10_tag", L_cap<128, 10, 1>},
-    {"cap256_12_tag", L_cap<256, 12, 1>},
+    {"lds256_s12_net64", L_lds<256, 12, 0, true>},
+    {"lds256_s12_floor", L_lds<256, 12, 2, true>},
+    {"dma256_s12_floor", L_lds<256, 12, 2, true, true>},
+    {"dma256_s12_net64", L_lds<256, 12, 0, true, true>},
+    {"dma128_s12_floor", L_lds<128, 12, 2, true, true>},
+    {"dma512_s12_floor", L_lds<512, 12, 2, true, true>},
+    {"dma256_s12_compact", L_lds<256, 12, 3, true, true>},
 };
 
 }  // namespace
