@@ -12,7 +12,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libquorumbatch.so")
+# QB_LIB_PATH overrides the in-tree build (A/B timing of two builds; tools/lab).
+LIB_PATH = os.environ.get("QB_LIB_PATH") or os.path.join(_HERE, "libquorumbatch.so")
 
 QB_OK = 0
 QB_EINVAL = -1

@@ -390,16 +390,23 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     const u64 a0 = b0 & ~u64(15);             // 16-byte aligned window
     const u64 a1 = (b1 + 15) & ~u64(15);
     const u64 n16 = (a1 - a0) / 16;
-    const uint4* gsrc = reinterpret_cast<const uint4*>(A.bytes + a0);
-    uint4* ldst = reinterpret_cast<uint4*>(stage);
-    const u64 lim = (A.nbytes + 15) / 16 - a0 / 16;  // 16-byte units readable
-    for (u64 k = threadIdx.x; k < n16; k += kBlock)
-      if (k < lim && a0 + 16 * k + 16 <= A.nbytes) ldst[k] = gsrc[k];
-      else
-        for (u32 t = 0; t < 16; ++t) {
-          const u64 p = a0 + 16 * k + t;
-          stage[16 * k + t] = p < A.nbytes ? A.bytes[p] : 0;
-        }
+    // Pieces wholly inside the byte buffer go by LDS-DMA, all issued before
+    // the barrier's one wait; only the buffer's last piece can be partial.
+    // (A byte buffer that is not 16-byte aligned stages with plain loads.)
+    const u64 whole = (A.nbytes - a0) / 16;
+    u32 nfull = u32(n16 < whole ? n16 : whole);
+    if ((reinterpret_cast<uintptr_t>(A.bytes) & 15u) == 0) {
+      constexpr int kIt = int((kStage + 16) / 16 / kBlock) + 1;
+      stage16_lds<kBlock, kIt>(stage, A.bytes + a0, nfull);
+    } else {
+      const uint4* gsrc = reinterpret_cast<const uint4*>(A.bytes + a0);
+      for (u64 k = threadIdx.x; k < nfull; k += kBlock) reinterpret_cast<uint4*>(stage)[k] = gsrc[k];
+    }
+    for (u64 k = nfull + threadIdx.x; k < n16; k += kBlock)
+      for (u32 t = 0; t < 16; ++t) {
+        const u64 p = a0 + 16 * k + t;
+        stage[16 * k + t] = p < A.nbytes ? A.bytes[p] : 0;
+      }
     lbase = a0;
     lend = a1 < A.nbytes ? a1 : A.nbytes;
   }

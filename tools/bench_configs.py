@@ -28,6 +28,9 @@ from etcd_amd.quorum import batch  # noqa: E402
 dev = torch.device("cuda", 0)
 
 
+GPU_ONLY = False
+
+
 def time_region(fn, reps, warm_s=0.3, regions=5):
     """Per-call device time: median over `regions` event-timed regions of
     `reps` back-to-back calls, after ~warm_s seconds of warm-up calls (a
@@ -231,8 +234,9 @@ def leader_config(G, reps, warm=4, shuffle=True):
     # match/next/pstate/infl_pos written 21 B; messages 40 B x 3 (stored,
     # copied, written) per message; scans 16 B per group.
     algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
-    if not shuffle:
-        print(json.dumps({"config": "leader inbox step, records in group order (lab)",
+    if not shuffle or GPU_ONLY:
+        print(json.dumps({"config": "leader inbox step" + ("" if shuffle else
+                          ", records in group order (lab)"),
                           "per_launch_us": t * 1e6, "groups_per_s": G / t}), flush=True)
         return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
@@ -423,7 +427,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="3,4,5")
+    ap.add_argument("--gpu-only", action="store_true", help="leader: skip the CPU baseline (A/B)")
     a = ap.parse_args()
+    global GPU_ONLY
+    GPU_ONLY = a.gpu_only
     which = set(a.only.split(","))
     if "3" in which:
         csr_config("ragged", 1 << 24, a.reps)
