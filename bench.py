@@ -15,6 +15,11 @@ launch overlaps the ramp of the next.  HIP events on the launch streams bracket
 the timed region; the per-launch duration used for the roofline is the
 region's device time / K.
 
+``--workload ragged|joint`` runs BASELINE configs[2] / configs[3] instead
+(16M ragged 3-9-voter groups with learners / 8M JointConfig 5+5 groups per
+GPU, CSR layout, ``k_csr``) with the same timing and JSON contract; the default
+stays configs[1], the metric's headline config.
+
 Multi-GPU: one process per GPU (torch.distributed, RCCL), groups sharded by
 global group number (weak scaling, no collective in the timed region); for
 N > 1 the node-wide all-gather of one batch's commit/vote vectors is timed
@@ -124,13 +129,39 @@ def cpu_baseline(n: int, sample_groups: int, seconds: float):
     }
 
 
+def cpu_baseline_csr(kind: str, seconds: float):
+    """The oracle's C SoA restatement (majority.go / joint.go per group) on a
+    bounded 1M-group sample of the same CSR workload, 16 host threads."""
+    from tests import oracle_c as oc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    gs = 1 << 20
+    seed = {"ragged": 0x5EED0003, "joint": 0x5EED0004}[kind]
+    off, m, cfg, votes = oc.gen_csr(seed, kind, gs)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oc.csr_eval(off, m, cfg, votes, threads=threads)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": reps * gs / dt, "unit": "groups/s", "cores": threads, "kind": "port",
+            "sample": f"{gs} groups of the same {kind} workload, C SoA restatement of "
+                      f"majority.go/joint.go (oracle/quorum_oracle.c); {reps} passes on "
+                      f"{threads} threads"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warm-up steps (default 2000 x ~9 us for configs[1], 300 x "
+                         "~0.2 ms for the CSR workloads: ~20-60 ms of work lets the clocks "
+                         "settle; 20 warm-up steps measured 2-3 %% slow)")
     ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
     ap.add_argument("--voters", type=int, default=5)
+    ap.add_argument("--workload", default="fixed", choices=["fixed", "ragged", "joint"],
+                    help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]")
     ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
@@ -150,23 +181,45 @@ def main():
         else:  # rehearsal of the N > 1 path on fewer GPUs
             dist.init_process_group(args.backend)
 
+    csr = args.workload != "fixed"
+    if args.warmup is None:
+        args.warmup = 300 if csr else 2000
     n, G, B, K, W = args.voters, args.groups, max(1, args.batches), args.steps, args.warmup
     S = max(1, args.streams)
+    if csr:
+        # configs[2]: 16M ragged groups per GPU; configs[3]: 64M joint groups over
+        # 8 GPUs = 8M per GPU.  One batch is 0.7-1.3 GB (far beyond the 256 MB
+        # MALL), so 2 resident batches suffice to keep consecutive steps apart.
+        if args.groups == 1 << 20:
+            G = (1 << 24) if args.workload == "ragged" else (1 << 23)
+        B = min(B, 2)
     lib = _lib.load()
-    fn = lib.qb_dev_fixed_committed_vote
     main_stream = torch.cuda.current_stream(dev)
     msp = main_stream.cuda_stream
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
     # B resident batches; global group numbers shard by rank (weak scaling)
-    groups = [batch.FixedGroups.synth(SEED, n, G, g_begin=(rank * B + b) * G, device=dev)
-              for b in range(B)]
+    if csr:
+        fn = lib.qb_dev_csr_committed_vote
+        seed = {"ragged": 0x5EED0003, "joint": 0x5EED0004}[args.workload]
+        groups = [batch.CsrGroups.synth(seed, args.workload, G, g_begin=(rank * B + b) * G,
+                                        device=dev) for b in range(B)]
+        slots = sum(int(g.off[-1].item()) for g in groups) / B
+    else:
+        fn = lib.qb_dev_fixed_committed_vote
+        groups = [batch.FixedGroups.synth(SEED, n, G, g_begin=(rank * B + b) * G, device=dev)
+                  for b in range(B)]
     outs = [(torch.empty(G, dtype=torch.int64, device=dev),
              torch.empty(G, dtype=torch.uint8, device=dev)) for _ in range(B)]
     # per step k: batch k % B on stream k % S (precomputed ctypes argument tuples)
-    call_args = [[(n, G, g.match.data_ptr(), g.voted.data_ptr(), g.granted.data_ptr(),
-                   c.data_ptr(), v.data_ptr(), st.cuda_stream)
-                  for g, (c, v) in zip(groups, outs)] for st in streams]
+    if csr:
+        call_args = [[(G, g.max_slots, g.off.data_ptr(), g.match.data_ptr(), g.cfg.data_ptr(),
+                       g.votes.data_ptr(), c.data_ptr(), v.data_ptr(), st.cuda_stream)
+                      for g, (c, v) in zip(groups, outs)] for st in streams]
+    else:
+        call_args = [[(n, G, g.match.data_ptr(), g.voted.data_ptr(), g.granted.data_ptr(),
+                       c.data_ptr(), v.data_ptr(), st.cuda_stream)
+                      for g, (c, v) in zip(groups, outs)] for st in streams]
     torch.cuda.synchronize()
 
     def run_steps(count, fixed_batch=None):
@@ -176,7 +229,7 @@ def main():
             b = k % B if fixed_batch is None else fixed_batch
             rc = fn(*call_args[k % S][b])
             if rc:
-                _lib.check(rc, "qb_dev_fixed_committed_vote")
+                _lib.check(rc, "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote")
         for st in streams:
             main_stream.wait_stream(st)
 
@@ -228,9 +281,28 @@ def main():
     if rank == 0:
         total_groups = world * G * K
         value = total_groups / elapsed
-        bpg = bytes_per_group(n)
+        if csr:
+            # off 4 + cfg 4 + votes 4 + match 8 per slot + commit 8 + vote 1
+            bpg = 21 + 8 * slots / G
+            key = f"csr_{args.workload}_G{G}"
+            workload = {"ragged": "BASELINE configs[2]: 16M groups ragged 3-9 voters + learners "
+                                  "(CSR offsets) per GPU, CommittedIndex + VoteResult",
+                        "joint": "BASELINE configs[3]: JointConfig 5+5 CommittedIndex/VoteResult, "
+                                 "8M groups per GPU (64M over 8 GPUs)"}[args.workload]
+            cfg = {"workload": workload, "groups_per_gpu": G, "mean_slots": slots / G,
+                   "layout": "CSR (off u32, cfg masks, votes, group-major match)"}
+            ms = groups[0].max_slots
+            kname = f"k_csr<{4 if ms <= 4 else 8 if ms <= 8 else 12 if ms <= 12 else 16},true,true>"
+        else:
+            bpg = bytes_per_group(n)
+            key = f"fixed_n{n}_G{G}"
+            cfg = {"workload": "BASELINE configs[1]: 1M groups x 5 voters CommittedIndex + "
+                               "VoteResult, uint64 indexes, one MI355X per shard",
+                   "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA"}
+            kname = f"k_fixed<{n},2,true,true>"
+        cfg.update({"batches_resident": B, "streams": S,
+                    "parallelism": f"groups sharded by id over {world} GPU(s)"})
         achieved = bpg * G / avg_kernel_s / 1e9
-        key = f"fixed_n{n}_G{G}"
         traffic = load_traffic(key)
         out = {
             "metric": METRIC,
@@ -245,18 +317,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (counter-based splitmix64 spec, SURVEY.md §8d; HBM-resident)",
-            "config": {
-                "workload": "BASELINE configs[1]: 1M groups x 5 voters CommittedIndex + "
-                            "VoteResult, uint64 indexes, one MI355X per shard",
-                "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA",
-                "batches_resident": B, "streams": S,
-                "parallelism": f"groups sharded by id over {world} GPU(s)",
-            },
+            "config": cfg,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": f"k_fixed<{n},2,true,true>",
+                "kernel": kname,
                 "bytes_per_group": bpg,
                 "avg_kernel_us": avg_kernel_s * 1e6,
                 "timing": (f"HIP events around the timed region on the launch streams; per-launch "
@@ -266,8 +332,10 @@ def main():
             "value_mall_warm": world * G * K / warm_elapsed,
             "allgather_ms": allgather_ms,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not csr:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample, args.cpu_seconds)
+        elif world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_csr(args.workload, args.cpu_seconds)
         print(json.dumps(out), flush=True)
 
     if world > 1:
