@@ -236,124 +236,154 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
   if (A.err_id) A.err_id[g] = rc ? bad : 0;
 }
 
-// Carried Progress and inflight rings are copied by the whole workgroup
-// after the per-group pass: each thread lists its new slots' (destination,
-// source) pairs in LDS, then lanes copy rows (and consecutive words of the
-// rings) with loads batched ahead of stores.  The per-group pass itself
-// only stores, so its stores never stall a later load (gfx9 counts loads
-// and stores on one vector memory counter).
-constexpr u32 kNoSrc = 0xFFFFFFFFu;
-constexpr u32 kRows = kBlk * QB_MAX_SLOTS;
+// The per-group pass only stores: new IDs, masks, and initProgress for fresh
+// slots.  A carried slot (checkAndCopy's shallow copy) is marked in the new
+// pstate (kCarried, never a valid QB_PR_* byte) with its old slot index in
+// the new infl_pos; k_cc_copy then moves the Progress row and ring with one
+// thread per new slot and overwrites both.  Keeping the copy out of the
+// replay kernel keeps that kernel's LDS to the working tables (occupancy) and
+// gives the byte moving a full-occupancy streaming launch of its own.
+constexpr u8 kCarried = 0xFF;
 
 __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
   __shared__ u64 tabs[kTab][kBlk];
-  __shared__ u32 row_dst[kRows], row_src[kRows];
-  __shared__ u32 nrows;
-  if (threadIdx.x == 0) nrows = 0;
-  __syncthreads();
   const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
-  if (g < A.G) {
-    Tab t = tab_of(tabs);
-    Roles r;
-    bool al;
-    u64 bad = 0;
-    int n_old;
-    int rc = replay(A, g, t, r, al, &bad, &n_old);
-    const u32 s0 = A.off[g];
-    const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
-    if (d1 <= A.S_cap) {  // else the caller's capacity is exceeded (reported by the host call)
-      if (rc) {  // the old config is kept
-        r = Roles{};
-        r.n = n_old;
-        r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
-        const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
-        r.in = c & 0xFFFFu;
-        r.out = c >> 16;
-        r.lnext = e & 0xFFFFu;
-        al = (e >> 16) & 1u;
-      }
-      // surviving entries in ascending ID order (selection over <= 24 entries)
-      u32 left = r.prs, ncfg_in = 0, ncfg_out = 0, nlnext = 0;
-      const u64 last = A.last_index[g];
-      const u32 nnew = u32(__popc(r.prs));
-      const u32 row0 = atomicAdd(&nrows, nnew);
-      for (u32 j = 0; left; ++j) {
-        int best = -1;
-        for (int k = 0; k < r.n; ++k)
-          if (((left >> k) & 1u) && (best < 0 || t.id(k) < t.id(best))) best = k;
-        left &= ~(1u << best);
-        const u32 b = 1u << best;
-        if (r.in & b) ncfg_in |= 1u << j;
-        if (r.out & b) ncfg_out |= 1u << j;
-        if (r.lnext & b) nlnext |= 1u << j;
-        const u64 d = d0 + j;
-        A.n_ids[d] = t.id(best);
-        u32 src = kNoSrc;
-        if (best < n_old && !(r.fresh & b)) {  // carried Progress (checkAndCopy's shallow copy)
-          src = s0 + u32(best);                // copied by the workgroup below
-        } else {  // initProgress (confchange.go:258-281)
-          A.n_match[d] = 0;
-          A.n_next[d] = last;
-          A.n_psnap[d] = 0;
-          A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
-          A.n_infl_pos[d] = 0;
+  if (g >= A.G) return;
+  Tab t = tab_of(tabs);
+  Roles r;
+  bool al;
+  u64 bad = 0;
+  int n_old;
+  int rc = replay(A, g, t, r, al, &bad, &n_old);
+  const u32 s0 = A.off[g];
+  const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
+  if (d1 > A.S_cap) return;  // the caller's capacity is exceeded (reported by new_off[G])
+  if (rc) {  // the old config is kept
+    r = Roles{};
+    r.n = n_old;
+    r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
+    const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
+    r.in = c & 0xFFFFu;
+    r.out = c >> 16;
+    r.lnext = e & 0xFFFFu;
+    al = (e >> 16) & 1u;
+  }
+  u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
+  const u64 last = A.last_index[g];
+  auto emit = [&](u32 j, int best) {
+    const u32 b = 1u << best;
+    if (r.in & b) ncfg_in |= 1u << j;
+    if (r.out & b) ncfg_out |= 1u << j;
+    if (r.lnext & b) nlnext |= 1u << j;
+    const u64 d = d0 + j;
+    A.n_ids[d] = t.id(best);
+    if (best < n_old && !(r.fresh & b)) {  // carried Progress: k_cc_copy
+      A.n_pstate[d] = kCarried;
+      A.n_infl_pos[d] = s0 + u32(best);
+    } else {  // initProgress (confchange.go:258-281)
+      A.n_match[d] = 0;
+      A.n_next[d] = last;
+      A.n_psnap[d] = 0;
+      A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
+      A.n_infl_pos[d] = 0;
+    }
+  };
+  // Surviving entries in ascending ID order.  The old slots are already
+  // ascending (the CSR slot order) and the appended entries few, so they are
+  // merged (one LDS read per output); an input table that is not ascending
+  // takes the selection over all entries instead.
+  bool asc = true;
+  {
+    u64 prev = 0;
+    for (int k = 0; k < n_old; ++k) {
+      const u64 v = t.id(k);
+      asc = asc && (k == 0 || prev < v);
+      prev = v;
+    }
+  }
+  if (asc) {
+    const u32 oldm = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
+    u32 old_left = r.prs & oldm, add_left = r.prs & ~oldm;
+    // smallest remaining appended entry (few: usually one)
+    auto add_min = [&](u64& v) {
+      int best = -1;
+      for (u32 m = add_left; m; m &= m - 1u) {
+        const int k = __builtin_ctz(m);
+        const u64 x = t.id(k);
+        if (best < 0 || x < v) {
+          best = k;
+          v = x;
         }
-        row_dst[row0 + j] = u32(d);
-        row_src[row0 + j] = src;
       }
-      A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
-      A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
+      return best;
+    };
+    u64 ov = 0, av = 0;
+    int oi = old_left ? __builtin_ctz(old_left) : -1;
+    if (oi >= 0) ov = t.id(oi);
+    int ai = add_min(av);
+    for (u32 j = 0; oi >= 0 || ai >= 0; ++j) {
+      if (oi >= 0 && (ai < 0 || ov < av)) {
+        emit(j, oi);
+        old_left &= old_left - 1u;
+        oi = old_left ? __builtin_ctz(old_left) : -1;
+        if (oi >= 0) ov = t.id(oi);
+      } else {
+        emit(j, ai);
+        add_left &= ~(1u << ai);
+        ai = add_min(av);
+      }
+    }
+  } else {
+    u32 left = r.prs;
+    for (u32 j = 0; left; ++j) {
+      int best = -1;
+      for (int k = 0; k < r.n; ++k)
+        if (((left >> k) & 1u) && (best < 0 || t.id(k) < t.id(best))) best = k;
+      left &= ~(1u << best);
+      emit(j, best);
     }
   }
-  __syncthreads();
-  // Carried Progress: four rows per lane in flight (all loads, then all
-  // stores), so loads do not queue behind earlier stores on the shared
-  // vector memory counter.
-  const u32 nr = nrows;
-  for (u32 e0 = threadIdx.x; e0 < nr; e0 += 4 * kBlk) {
-    u64 m[4], nx[4], ps[4];
-    u32 ip[4];
-    u8 st[4];
-    u32 dst[4];
-    bool on[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const u32 e = e0 + u32(q) * kBlk;
-      const u32 src = e < nr ? row_src[e] : kNoSrc;
-      on[q] = src != kNoSrc;
-      dst[q] = e < nr ? row_dst[e] : 0u;
-      m[q] = on[q] ? A.match[src] : 0ull;
-      nx[q] = on[q] ? A.next[src] : 0ull;
-      ps[q] = on[q] ? A.psnap[src] : 0ull;
-      ip[q] = on[q] ? A.infl_pos[src] : 0u;
-      st[q] = on[q] ? A.pstate[src] : u8(0);
+  A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
+  A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
+}
+
+// One thread per new slot d < min(new_off[G], S_cap), grid-stride: a carried
+// slot's match / next / pendingSnapshot / inflight position / state byte and
+// its ring come from the old slot; a fresh slot's ring is zeroed.  A slot of
+// a group past the capacity was never written: the source bound keeps any
+// stale marker from reading outside the old arrays.
+__global__ __launch_bounds__(256) void k_cc_copy(Args A) {
+  const u64 total = A.new_cnt[A.G];
+  const u64 end = total < A.S_cap ? total : A.S_cap;
+  const u32 old_total = A.off[A.G];
+  const u32 K = A.K;
+  for (u64 d = u64(blockIdx.x) * 256 + threadIdx.x; d < end; d += u64(gridDim.x) * 256) {
+    const bool carried = A.n_pstate[d] == kCarried;
+    const u32 src = carried ? A.n_infl_pos[d] : 0u;
+    const bool ok = carried && src < old_total;
+    if (ok) {
+      const u64 m = A.match[src], nx = A.next[src], ps = A.psnap[src];
+      const u32 ip = A.infl_pos[src];
+      const u8 st = A.pstate[src];
+      A.n_match[d] = m;
+      A.n_next[d] = nx;
+      A.n_psnap[d] = ps;
+      A.n_infl_pos[d] = ip;
+      A.n_pstate[d] = st;
     }
+    if (K) {
+      const u64* sr = A.infl_buf + u64(src) * K;
+      u64* dr = A.n_infl_buf + d * K;
+      u32 k = 0;
+      for (; k + 4 <= K; k += 4) {
+        u64 v[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!on[q]) continue;
-      A.n_match[dst[q]] = m[q];
-      A.n_next[dst[q]] = nx[q];
-      A.n_psnap[dst[q]] = ps[q];
-      A.n_infl_pos[dst[q]] = ip[q];
-      A.n_pstate[dst[q]] = st[q];
+        for (int q = 0; q < 4; ++q) v[q] = ok ? sr[k + q] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dr[k + q] = v[q];
+      }
+      for (; k < K; ++k) dr[k] = ok ? sr[k] : 0ull;
     }
-  }
-  if (A.K == 0) return;  // uniform
-  const u32 K = A.K, words = nr * K;
-  constexpr int kB = 8;  // words per lane in flight
-  for (u32 w0 = threadIdx.x; w0 < words; w0 += kB * kBlk) {
-    u64 v[kB], at[kB];
-#pragma unroll
-    for (int q = 0; q < kB; ++q) {
-      const u32 w = w0 + u32(q) * kBlk;
-      const u32 e = w < words ? w / K : 0u, k = w - e * K;
-      const u32 src = w < words ? row_src[e] : kNoSrc;
-      at[q] = w < words ? u64(row_dst[e]) * K + k : ~0ull;
-      v[q] = src == kNoSrc ? 0ull : A.infl_buf[u64(src) * K + k];
-    }
-#pragma unroll
-    for (int q = 0; q < kB; ++q)
-      if (at[q] != ~0ull) A.n_infl_buf[at[q]] = v[q];
   }
 }
 
@@ -422,5 +452,7 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
   QB_CHECK_LAUNCH("scan(conf change)");
   hipLaunchKernelGGL(cc::k_cc_write, dim3(grid), dim3(cc::kBlk), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_write");
+  hipLaunchKernelGGL(cc::k_cc_copy, dim3(2048), dim3(256), 0, st, A);
+  QB_CHECK_LAUNCH("k_cc_copy");
   return QB_OK;
 }
