@@ -168,6 +168,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="launch the steps from a captured HIP graph of this many steps "
+                         "(0 = direct launches); the remainder of K is launched directly")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -232,6 +235,34 @@ def main():
                 _lib.check(rc, "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote")
         for st in streams:
             main_stream.wait_stream(st)
+
+    graph = None
+    if args.graph > 0:
+        # one captured graph = args.graph consecutive steps over the same
+        # batch/stream rotation as run_steps (forked from and joined back to
+        # the capture stream), replayed on the main stream
+        L = args.graph
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(dev)
+        with torch.cuda.graph(graph, stream=cap):
+            for st in streams:
+                st.wait_stream(cap)
+            for k in range(L):
+                rc = fn(*call_args[k % S][k % B])
+                if rc:
+                    _lib.check(rc, "capture")
+            for st in streams:
+                cap.wait_stream(st)
+        torch.cuda.synchronize()
+        eager_steps = run_steps
+
+        def run_steps(count, fixed_batch=None):  # noqa: F811
+            if fixed_batch is not None:
+                return eager_steps(count, fixed_batch)
+            for _ in range(count // L):
+                graph.replay()
+            if count % L:
+                eager_steps(count % L)
 
     def barrier():
         if world > 1:
@@ -300,7 +331,7 @@ def main():
                                "VoteResult, uint64 indexes, one MI355X per shard",
                    "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA"}
             kname = f"k_fixed<{n},2,true,true>"
-        cfg.update({"batches_resident": B, "streams": S,
+        cfg.update({"batches_resident": B, "streams": S, "graph_steps": args.graph,
                     "parallelism": f"groups sharded by id over {world} GPU(s)"})
         achieved = bpg * G / avg_kernel_s / 1e9
         traffic = load_traffic(key)
@@ -327,7 +358,9 @@ def main():
                 "avg_kernel_us": avg_kernel_s * 1e6,
                 "timing": (f"HIP events around the timed region on the launch streams; per-launch "
                            f"duration = region device time / K with {S} stream(s) overlapping "
-                           f"consecutive launches"),
+                           f"consecutive launches"
+                           + (f", launched from a HIP graph of {args.graph} steps"
+                              if args.graph else "")),
             },
             "value_mall_warm": world * G * K / warm_elapsed,
             "allgather_ms": allgather_ms,

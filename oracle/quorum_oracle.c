@@ -396,6 +396,29 @@ void orc_faithful_eval(u64 G, const orc_group_maps* maps, u64* commit, u8* vote)
   }
 }
 
+/* BASELINE configs[0]: BenchmarkMajorityConfig_CommittedIndex
+ * (quorum/bench_test.go:24-40) — one MajorityConfig with IDs 1..n and a
+ * mapAckIndexer of values in [0, MaxInt64), CommittedIndex called `iters`
+ * times in a loop on one thread.  Returns the sum of the results (so the loop
+ * is not elided); the caller times the call. */
+u64 orc_bench_plumbing(u32 n, u64 iters, u64 seed) {
+  orc_group_maps m;
+  memset(&m, 0, sizeof m);
+  for (u32 j = 0; j < n; ++j) {
+    u32 p;
+    tbl_put(m.cfg_key, j + 1, &p);
+    tbl_put(m.prs_key, j + 1, &p);
+    m.prs_val[p] = splitmix64(seed + j) % 0x7FFFFFFFFFFFFFFFull; /* rand.Int63n(MaxInt64) */
+  }
+  u64 acc = 0;
+  for (u64 i = 0; i < iters; ++i) {
+    /* defeat hoisting: the map is re-read every call, as Go's range is */
+    __asm__ __volatile__("" : : "r"(&m) : "memory");
+    acc += faithful_ci(&m);
+  }
+  return acc;
+}
+
 /* --------------------------------------------------- pthread drivers ----- */
 
 typedef struct {

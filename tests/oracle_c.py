@@ -33,6 +33,7 @@ SIG = {
     "orc_fixed_appresp_sequential": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                             _p, _p, _p, _p, _p]),
     "orc_fixed_commit_all": (None, [_u32, _u64, _p, _p, _p, _p]),
+    "orc_bench_plumbing": (_u64, [_u32, _u64, _u64]),
     "orc_leader_step": (_u64, [_p, _p, _p, _u64, _p, _p, _p, _i32]),
     "orc_ingest": (None, [_u64, _p, _u64, _p, _p, _u64, _p, _p] + [_p] * 7 + [_i32]),
 }

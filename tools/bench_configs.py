@@ -2,6 +2,8 @@
 """Throughput of every BASELINE config on one GPU (bench.py measures only
 configs[1]; these are the parity-test configs, measured the same way).
 
+  config 1  plumbing: BenchmarkMajorityConfig_CommittedIndex (bench_test.go:24-40),
+            voters 1..11, CPU ns/op beside GPU ns per group
   config 3  16M groups ragged 3-9 voters + 0-2 learners (CSR)
   config 4  joint 5+5 (overlap 0-5), 8M groups = one GPU's shard of 64M
   config 5  streaming tracker: 16M 5-voter groups, one MsgAppResp per group
@@ -78,6 +80,36 @@ def report(name, groups, t, algo_bytes, extra=None):
     if extra:
         d.update(extra)
     print(json.dumps(d), flush=True)
+
+
+def plumbing_config(reps):
+    """BASELINE configs[0]: BenchmarkMajorityConfig_CommittedIndex
+    (quorum/bench_test.go:24-40), voters in {1,3,5,7,9,11}.  CPU: the
+    faithful C restatement (map config + map AckedIndexer + insertion sort),
+    one config called in a loop on 1 thread, ns/op.  GPU beside it: the same
+    CommittedIndex over 16M groups of that width in one launch (fixed layout,
+    CommittedIndex only), device ns per group."""
+    import time
+    from tests import oracle_c as oc
+    lib = oc.load()
+    G = 1 << 24
+    for n in (1, 3, 5, 7, 9, 11):
+        iters, t = 1 << 20, 0.0
+        while True:
+            t0 = time.perf_counter()
+            lib.orc_bench_plumbing(n, iters, 0x5EED0001)
+            t = time.perf_counter() - t0
+            if t >= 0.5:
+                break
+            iters *= 4
+        fg = batch.FixedGroups.synth(0x5EED0001, n, G, device=dev)
+        c = torch.empty(G, dtype=torch.int64, device=dev)
+        tg = time_region(lambda: fg.committed_vote(c, want_vote=False), reps)
+        print(json.dumps({"config": f"plumbing voters={n}", "cpu_ns_per_op": t / iters * 1e9,
+                          "cpu_kind": "port (faithful C restatement of majority.go, 1 thread)",
+                          "gpu_ns_per_group": tg / G * 1e9, "gpu_groups_per_launch": G,
+                          "gpu_achieved_GBs": G * (8 * n + 8) / tg / 1e9}), flush=True)
+        del fg, c
 
 
 def csr_config(kind, G, reps):
@@ -432,6 +464,8 @@ def main():
     global GPU_ONLY
     GPU_ONLY = a.gpu_only
     which = set(a.only.split(","))
+    if "1" in which:
+        plumbing_config(a.reps)
     if "3" in which:
         csr_config("ragged", 1 << 24, a.reps)
     if "4" in which:
