@@ -9,7 +9,10 @@
 namespace qb {
 namespace bk {
 
-constexpr int kTile = 4096;          // records per histogram/scatter/split tile
+#ifndef QB_KTILE
+#define QB_KTILE 4096
+#endif
+constexpr int kTile = QB_KTILE;      // records per histogram/scatter/split tile
 constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
 using scan::kScanPer;
 constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
@@ -28,10 +31,28 @@ struct Cols {
 
 __host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
+// with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles
+// t, t+1, ... run on one XCD: the partial 128-byte lines that neighbouring
+// tiles write into the same bucket (K3 runs, K1 histogram columns) meet in
+// that XCD's L2 instead of reaching HBM as separate partial writes.  The grid
+// must be a multiple of kXcds (Geometry::tile_grid); logical tiles >= the real count exit.
+// Used only when a tile's mean run per super-bucket is shorter than two lines
+// (kTile / NSB < 32 u64): config 5 (NSB = 256, 16-record runs) K3 241 -> 200
+// us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
+// 41 -> 55 us with it, so it keeps the linear order.
+constexpr u32 kXcds = 8;
+__device__ __forceinline__ u32 xcd_major() {
+  return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
+}
+
 struct Geometry {
   u64 G, M;
   u32 n, CH, NC, NSB, NT;
+  u32 xcd;  // tiles of K1/K3 mapped XCD-major (see xcd_major)
   u64 nbins() const { return u64(NSB) * NT; }
+  u32 tile_grid() const { return xcd ? (NT + kXcds - 1) / kXcds * kXcds : NT; }
+  __device__ __forceinline__ u32 tile() const { return xcd ? xcd_major() : blockIdx.x; }
 };
 
 inline Geometry geometry(u32 n, u64 G, u64 M) {
@@ -43,6 +64,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M) {
   g.NC = u32((G + g.CH - 1) / g.CH);
   g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
   g.NT = u32((M + kTile - 1) / kTile);
+  g.xcd = g.NSB > 0 && u32(kTile) / g.NSB < 32u;
   return g;
 }
 

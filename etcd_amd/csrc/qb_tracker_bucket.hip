@@ -53,10 +53,12 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
                                                     u64* __restrict__ shards) {
   extern __shared__ __attribute__((aligned(16))) u32 lh[];  // NSB counters
   __shared__ u32 tl[2];
+  const u32 tile = geo.tile();
+  if (tile >= geo.NT) return;  // XCD-major grid is rounded up to a multiple of kXcds
   BlockTally<2> tally;
   for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) lh[b] = 0;
   __syncthreads();
-  const u64 t0 = u64(blockIdx.x) * kTile;
+  const u64 t0 = u64(tile) * kTile;
   const u32 sbgroups = geo.CH * kChunksPerSb;
   // The tile's group / flag loads are all issued before the first LDS
   // atomic (a load -> use loop waited one HBM round trip per iteration).
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
     tally.add(1, nonmember);
   }
   __syncthreads();
-  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) hist[u64(b) * geo.NT + blockIdx.x] = lh[b];
+  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) hist[u64(b) * geo.NT + tile] = lh[b];
   const int slot[2] = {QB_STAT_BAD_GROUP, QB_STAT_NON_MEMBER};
   tally.flush(tl, shard_of(shards), slot);
 }
@@ -168,7 +170,9 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   u32* start = dyn;               // NSB: count, then local exclusive start
   u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
   __shared__ TileLds L;
-  const u64 t0 = u64(blockIdx.x) * kTile;
+  const u32 tile = geo.tile();
+  if (tile >= geo.NT) return;
+  const u64 t0 = u64(tile) * kTile;
   const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
   u32 g[kPer], f[kPer];
   u64 vi[kPer], vt[kPer];
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   }
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     start[b] = 0;
-    gstart[b] = offsets[u64(b) * geo.NT + blockIdx.x];
+    gstart[b] = offsets[u64(b) * geo.NT + tile];
   }
   __syncthreads();
   const u32 sbgroups = geo.CH * kChunksPerSb;
@@ -560,7 +564,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
     hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
     return e == hipSuccess ? QB_OK : hip_fail(e, "hipMemsetAsync(parts)");
   }
-  hipLaunchKernelGGL(k_bk_hist, dim3(geo.NT), dim3(kBlock), lds_bins, st, geo, rec_group,
+  hipLaunchKernelGGL(k_bk_hist, dim3(geo.tile_grid()), dim3(kBlock), lds_bins, st, geo, rec_group,
                      rec_flags, hist, shards);
   QB_CHECK_LAUNCH("k_bk_hist");
   const u64 nb = geo.nbins();
@@ -569,7 +573,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
   hipLaunchKernelGGL(scan::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
   QB_CHECK_LAUNCH("k_scan");
-  hipLaunchKernelGGL(k_bk_scatter, dim3(geo.NT), dim3(kPartThreads), 2 * lds_bins, st, geo,
+  hipLaunchKernelGGL(k_bk_scatter, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st, geo,
                      rec_group, rec_flags, rec_index, rec_term, hist, buf1);
   QB_CHECK_LAUNCH("k_bk_scatter");
   hipLaunchKernelGGL(k_bk_parts, dim3(1), dim3(1024), 0, st, geo, hist, pt);

@@ -194,9 +194,11 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
         tr.apply_appresp(b)
         tr.commit_advance()
 
-    t_two = stream_time(two_call)
-    t_apply = stream_time(lambda b: tr.apply_appresp(b))
-    t_commit = time_region(lambda: tr.commit_advance(), reps)
+    t_two = t_apply = t_commit = float("nan")
+    if not GPU_ONLY:  # A/B runs time the bucketed step alone
+        t_two = stream_time(two_call)
+        t_apply = stream_time(lambda b: tr.apply_appresp(b))
+        t_commit = time_region(lambda: tr.commit_advance(), reps)
     t = stream_time(lambda b: tr.step(b))
     adv = torch.zeros(G, dtype=torch.uint8, device=dev)
     restore()
@@ -211,6 +213,9 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
     algo = G * (21 + 16) + G * 64
     # CPU beside it: the sequential one-record-at-a-time oracle (the Go
     # stepLeader loop restated) on a bounded sample, 1 thread
+    if GPU_ONLY:
+        report("streaming tracker (bucketed step)", G, t, algo, {"unit": "group-steps/s"})
+        return
     from tests import oracle_c as oc
     Gs = 1 << 20
     m0, _, _, ts0 = oc.gen_fixed(0x5EED0005, n, Gs)
