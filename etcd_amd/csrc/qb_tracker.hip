@@ -15,18 +15,49 @@ namespace qb {
 
 // ------------------------------------------------------------ QuorumActive --
 
+// Every voter has a Progress, so votes[id] = RecentActive is present for
+// each: yes = popcount(mask & active), voted = n (tracker.go:216-222).
+__device__ __forceinline__ u8 quorum_active_one(u32 c, u32 a) {
+  const u32 min_ = c & 0xFFFFu, mout = c >> 16;
+  const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & a), __popc(min_));
+  const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & a), __popc(mout));
+  return joint_vote(r1, r2) == QB_VOTE_WON ? 1 : 0;
+}
+
+// kQaGpt groups per thread: two 16-byte cfg loads, one 16-byte active load
+// and one 8-byte store, all nontemporal (7 B/group streamed once); the
+// thread-per-group form moved 1-4 bytes per lane and reached 4.2 TB/s.
+// VEC needs 16-byte aligned cfg/active, 8-byte aligned won; the last
+// partial group of 8 takes the scalar loop.
+constexpr u32 kQaGpt = 8;
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_quorum_active(u64 G, const u32* __restrict__ cfg,
                                                           const u16* __restrict__ active,
                                                           u8* __restrict__ won) {
-  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (g >= G) return;
-  const u32 c = cfg[g];
-  const u32 min_ = c & 0xFFFFu, mout = c >> 16, a = active[g];
-  // Every voter has a Progress, so votes[id] = RecentActive is present for
-  // each: yes = popcount(mask & active), voted = n (tracker.go:216-222).
-  const u8 r1 = vote_from_counts(__popc(min_), __popc(min_ & a), __popc(min_));
-  const u8 r2 = vote_from_counts(__popc(mout), __popc(mout & a), __popc(mout));
-  won[g] = joint_vote(r1, r2) == QB_VOTE_WON ? 1 : 0;
+  const u64 g0 = (u64(blockIdx.x) * kBlock + threadIdx.x) * kQaGpt;
+  if (g0 >= G) return;
+  if (VEC && g0 + kQaGpt <= G) {
+    using v4u = u32 __attribute__((ext_vector_type(4)));
+    using v2u = u32 __attribute__((ext_vector_type(2)));
+    const v4u c0 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(cfg + g0));
+    const v4u c1 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(cfg + g0 + 4));
+    const v4u a4 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(active + g0));
+    const u32 c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const u32 a[4] = {a4.x, a4.y, a4.z, a4.w};
+    u32 w[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32 ak = (a[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+      w[k >> 2] |= u32(quorum_active_one(c[k], ak)) << ((k & 3) * 8);
+    }
+    v2u out;
+    out.x = w[0];
+    out.y = w[1];
+    __builtin_nontemporal_store(out, reinterpret_cast<v2u*>(won + g0));
+    return;
+  }
+  const u64 g1 = g0 + kQaGpt < G ? g0 + kQaGpt : G;
+  for (u64 g = g0; g < g1; ++g) won[g] = quorum_active_one(cfg[g], active[g]);
 }
 
 // ---------------------------------------------------------- MsgAppResp -----
@@ -198,8 +229,16 @@ extern "C" int qb_dev_csr_quorum_active(uint64_t G, const uint32_t* cfg, const u
                                         uint8_t* won_out, void* stream) {
   if (G == 0) return QB_OK;
   QB_REQUIRE(cfg && active && won_out, "cfg/active/won_out NULL");
-  hipLaunchKernelGGL(k_quorum_active, dim3(grid_for(G)), dim3(kBlock), 0, as_stream(stream), G,
-                     cfg, active, won_out);
+  const bool vec = (reinterpret_cast<uintptr_t>(cfg) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(active) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(won_out) % 8) == 0;
+  const unsigned grid = grid_for((G + kQaGpt - 1) / kQaGpt);
+  if (vec)
+    hipLaunchKernelGGL(k_quorum_active<true>, dim3(grid), dim3(kBlock), 0, as_stream(stream), G,
+                       cfg, active, won_out);
+  else
+    hipLaunchKernelGGL(k_quorum_active<false>, dim3(grid), dim3(kBlock), 0, as_stream(stream), G,
+                       cfg, active, won_out);
   QB_CHECK_LAUNCH("k_quorum_active");
   return QB_OK;
 }

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from etcd_amd import quorum
+from etcd_amd import _lib, quorum
 from etcd_amd.quorum import VoteResult, batch
 from oracle import quorum_ref as q
 from tests import oracle_c as oc
@@ -259,13 +259,32 @@ def test_election_table(tables):
 
 
 def test_quorum_active_vs_oracle():
+    """Vector path (8 groups per thread), its scalar tail (G % 8 != 0) and the
+    scalar kernel (unaligned operands) against the C oracle."""
     rng = np.random.default_rng(5)
     for kind in ("ragged", "joint"):
-        grp = batch.CsrGroups.synth(0x5EED0005, kind, 30000)
+        for G in (30000, 30005, 7):
+            grp = batch.CsrGroups.synth(0x5EED0005, kind, G)
+            cfg = grp.cfg.cpu().numpy().view(np.uint32)
+            active = rng.integers(0, 1 << 16, size=G).astype(np.uint16)
+            got = grp.quorum_active(torch.from_numpy(active.view(np.int16)).to(DEV))
+            assert np.array_equal(got.cpu().numpy(), oc.quorum_active(cfg, active))
+        # unaligned: operands start one element into their allocations
+        G = 30001
+        grp = batch.CsrGroups.synth(0x5EED0006, kind, G)
         cfg = grp.cfg.cpu().numpy().view(np.uint32)
-        active = rng.integers(0, 1 << 16, size=30000).astype(np.uint16)
-        got = grp.quorum_active(torch.from_numpy(active.view(np.int16)).to(DEV))
-        assert np.array_equal(got.cpu().numpy(), oc.quorum_active(cfg, active))
+        active = rng.integers(0, 1 << 16, size=G).astype(np.uint16)
+        cfg_d = torch.zeros(G + 1, dtype=torch.int32, device=DEV)
+        cfg_d[1:] = grp.cfg
+        act_d = torch.zeros(G + 1, dtype=torch.int16, device=DEV)
+        act_d[1:] = torch.from_numpy(active.view(np.int16)).to(DEV)
+        won = torch.full((G + 1,), 9, dtype=torch.uint8, device=DEV)
+        _lib.call("qb_dev_csr_quorum_active", G, cfg_d[1:].data_ptr(), act_d[1:].data_ptr(),
+                  won[1:].data_ptr(), torch.cuda.current_stream(DEV).cuda_stream)
+        torch.cuda.synchronize()
+        w = won.cpu().numpy()
+        assert w[0] == 9
+        assert np.array_equal(w[1:], oc.quorum_active(cfg, active))
 
 
 @pytest.mark.timeout(300)
