@@ -23,11 +23,19 @@ constexpr int kShards = 256;         // stat counter shards (one 64-byte line ea
 //   meta = lg (bits 0-9) | chunk-low (10-16) | record flags byte (17-24:
 //          slot 17-20, kind 21-22, no-progress 23, reject 24),
 //   ridx = batch index of the record (step-down ordering).
+// term32 (optional, in the term column's space): the term as u32, or
+// kTermEscape when it does not fit, in which case the consumer reads the
+// full term from the original batch by ridx (the tracker step).
 struct Cols {
   u64* index;
   u64* term;
   u64* mr;
+  u32* term32;
 };
+constexpr u32 kTermEscape = 0xFFFFFFFFu;
+__host__ __device__ __forceinline__ u32 term_to32(u64 t) {
+  return t < u64(kTermEscape) ? u32(t) : kTermEscape;
+}
 
 __host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
 
@@ -94,9 +102,9 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
   const size_t col = up256(sizeof(u64) * M);
-  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base)};
+  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr};
   return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
-              reinterpret_cast<u64*>(base + 2 * col)};
+              reinterpret_cast<u64*>(base + 2 * col), nullptr};
 }
 
 
@@ -155,10 +163,11 @@ struct RunTable {
 // with group >= G are dropped and counted into shards[QB_STAT_BAD_GROUP], and
 // with n < 16 those with slot >= n into shards[QB_STAT_NON_MEMBER].
 // rec_index == rec_term == nullptr buckets the mr column alone (carve with
-// ncols = 1).
+// ncols = 1).  term32: the term column moves as u32 (term_to32), 4 bytes
+// per record less through both levels; read it with Cols::term32.
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st);
+                   hipStream_t st, bool term32 = false);
 
 }  // namespace bk
 }  // namespace qb

@@ -226,10 +226,18 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
     }
     __syncthreads();
     u64* dst = col == 0 ? out.index : col == 1 ? out.term : out.mr;
-    for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
-      const u32 k = L.perm[e];
-      const u32 b = L.bin[k];
-      dst[gstart[b] + (e - start[b])] = L.stage[k];
+    if (col == 1 && out.term32) {
+      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+        const u32 k = L.perm[e];
+        const u32 b = L.bin[k];
+        out.term32[gstart[b] + (e - start[b])] = term_to32(L.stage[k]);
+      }
+    } else {
+      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+        const u32 k = L.perm[e];
+        const u32 b = L.bin[k];
+        dst[gstart[b] + (e - start[b])] = L.stage[k];
+      }
     }
     __syncthreads();
   }
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
     for (int j = 0; j < kPer; ++j) {
       const u32 k = threadIdx.x + j * kPartThreads;
       vi[j] = k < nrec ? in.index[lo + k] : 0ull;
-      vt[j] = k < nrec ? in.term[lo + k] : 0ull;
+      vt[j] = k >= nrec ? 0ull : in.term32 ? u64(in.term32[lo + k]) : in.term[lo + k];
     }
   }
   u64 vm[kPer];  // loaded together: one round trip, not one per record
@@ -321,7 +329,12 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
       if (k < nrec) L.stage[k] = col == 0 ? vi[j] : vt[j];
     }
     __syncthreads();
-    for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) dst[lo + e] = L.stage[L.perm[e]];
+    if (col == 1 && out.term32) {
+      for (u32 e = threadIdx.x; e < nrec; e += blockDim.x)
+        out.term32[lo + e] = u32(L.stage[L.perm[e]]);
+    } else {
+      for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) dst[lo + e] = L.stage[L.perm[e]];
+    }
     __syncthreads();
   }
 }
@@ -334,6 +347,7 @@ template <int N, bool NEXT>
 __global__ __launch_bounds__(kBlock) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
+    const u64* __restrict__ rec_term,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
     u64* __restrict__ shards) {
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
         if (f < total) {
           const u32 i = rt.locate(f);
           rmr[r] = recs.mr[i];
-          rtm[r] = recs.term[i];
+          rtm[r] = recs.term32[i];
           rix[r] = recs.index[i];
         }
       }
@@ -410,7 +424,9 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
         const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
         bool stale = false, higher = false, applied = false, rejected = false;
         if (f < total) {
-          const u64 mr = rmr[r], term = rtm[r];
+          const u64 mr = rmr[r];
+          // a term past 32 bits comes from the original batch (kTermEscape)
+          const u64 term = rtm[r] != kTermEscape ? rtm[r] : rec_term[u32(mr >> 32)];
           const u32 meta = u32(mr), lg = meta & 1023u, s = (meta >> 17) & 15u;
           const u64 gt = gterm[lg];
           stale = term < gt;
@@ -455,7 +471,8 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
           const u64 mr = recs.mr[i];
           const u32 meta = u32(mr), ridx = u32(mr >> 32);
           const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
-          if (recs.term[i] == gterm[lg]) {
+          const u32 t32 = recs.term32[i];
+          if ((t32 != kTermEscape ? u64(t32) : rec_term[ridx]) == gterm[lg]) {
             if (ridx > first_hi[lg]) {
               after = true;
             } else {
@@ -519,23 +536,24 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
 
 template <int N>
 void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs, const u64* gt,
-                  const u64* ts, u64* match, u64* next, u16* active, u64* committed,
+                  const u64* ts, const u64* rterm, u64* match, u64* next, u16* active, u64* committed,
                   u32* stepdown, u8* adv, u64* stats, hipStream_t st) {
   if (next)
     hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
-                       cs, gt, ts, match, next, active, committed, stepdown, adv, stats);
+                       cs, gt, ts, rterm, match, next, active, committed, stepdown, adv, stats);
   else
     hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
-                       cs, gt, ts, match, next, active, committed, stepdown, adv, stats);
+                       cs, gt, ts, rterm, match, next, active, committed, stepdown, adv, stats);
 }
 
 template <int... Ns>
 void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
                     Cols recs, const u32* pt, const u32* cs, const u64* gt, const u64* ts,
+                    const u64* rterm,
                     u64* match,
                     u64* next, u16* active, u64* committed, u32* stepdown, u8* adv, u64* stats,
                     hipStream_t st) {
-  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, gt, ts, match, next, active,
+  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, gt, ts, rterm, match, next, active,
                                        committed, stepdown, adv, stats, st)
                 : void()),
    ...);
@@ -551,14 +569,18 @@ namespace bk {
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st) {
+                   hipStream_t st, bool term32) {
   u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
   u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
   const int ncols = rec_index ? 3 : 1;
-  const Cols buf1 = cols_at(ws + cv.buf1, geo.M, ncols);
-  const Cols buf2 = cols_at(ws + cv.buf2, geo.M, ncols);
+  Cols buf1 = cols_at(ws + cv.buf1, geo.M, ncols);
+  Cols buf2 = cols_at(ws + cv.buf2, geo.M, ncols);
+  if (term32 && rec_index) {
+    buf1.term32 = reinterpret_cast<u32*>(buf1.term);
+    buf2.term32 = reinterpret_cast<u32*>(buf2.term);
+  }
   const size_t lds_bins = sizeof(u32) * geo.NSB;
   if (geo.M == 0) {
     hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
@@ -618,7 +640,8 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M);
+  bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M);
+  buf2.term32 = reinterpret_cast<u32*>(buf2.term);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   hipError_t e0 = hipMemsetAsync(shards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
@@ -627,12 +650,14 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   {
     const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags,
                                       reinterpret_cast<const u64*>(rec_index),
-                                      reinterpret_cast<const u64*>(rec_term), shards, st);
+                                      reinterpret_cast<const u64*>(rec_term), shards, st,
+                                      /*term32=*/true);
     if (rc != QB_OK) return rc;
   }
   bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs,
                      reinterpret_cast<const u64*>(group_term),
-                     reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
+                     reinterpret_cast<const u64*>(term_start),
+                     reinterpret_cast<const u64*>(rec_term), reinterpret_cast<u64*>(match),
                      reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed),
                      stepdown_at, advanced_out, shards, st);
   QB_CHECK_LAUNCH("k_bk_apply");

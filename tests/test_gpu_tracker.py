@@ -76,10 +76,10 @@ def test_commit_table(tables):
         assert adv.cpu().tolist() == [int(c["want"] > 0) for c in cases]
 
 
-def _random_state(rng, n, G):
+def _random_state(rng, n, G, term_base=0):
     match, _, _, ts = oc.gen_fixed(0x5EED0005, n, G)
     last = match[0].copy()
-    term = rng.integers(2, 9, size=G).astype(np.uint64)
+    term = rng.integers(2, 9, size=G).astype(np.uint64) + np.uint64(term_base)
     st = {"match": match.copy(), "next": (match + np.uint64(1)).copy(),
           "active": np.zeros(G, np.uint16), "term": term, "term_start": ts,
           "last_index": last, "committed": np.zeros(G, np.uint64),
@@ -145,6 +145,30 @@ def test_appresp_then_commit_vs_sequential(mode, n, G, M, kw):
         assert got["after_stepdown"] == stats[6]
         # caller protocol: stepped-down groups are handed to the scalar path
         # (becomeFollower) and the marker is re-armed before the next batch
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
+
+
+@pytest.mark.parametrize("term_base", [0xFFFFFFFF - 5, 1 << 40, (1 << 64) - 16])
+def test_step_wide_terms_vs_sequential(term_base):
+    """Terms around and past 2^32: the bucketed step carries the term as u32
+    with an escape to the original batch (qb_bucket.h: term_to32); group
+    terms straddle the escape value so equal / stale / higher records land on
+    both sides of it."""
+    n, G, M = 5, 70001, 70001
+    rng = np.random.default_rng(term_base % 1000003)
+    st = _random_state(rng, n, G, term_base)
+    tr = _tracker_from(n, st)
+    seq = {k: v.copy() for k, v in st.items()}
+    for step in range(3):
+        group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, stale=0.05,
+                                                             higher=0.01)
+        stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, n, G)
+        got = tr.stats_dict()
+        assert got["applied"] == stats[0] and got["stale_term"] == stats[2]
+        assert got["higher_term"] == stats[4] and got["after_stepdown"] == stats[6]
         tr.stepdown_at.fill_(-1)
         seq["stepped_down"][:] = 0
 
