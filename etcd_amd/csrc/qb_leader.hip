@@ -348,7 +348,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
       for (u32 f = t; f < total; f += kBlock) {
         const u32 b = rt.locate(f);
         const u64 v = recs.mr[b];
-        const u64 term = recs.term[b], index = recs.index[b];
+        const u32 t32 = recs.term32[b];  // kTermEscape: the full term from the batch
+        const u64 term = t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
+        const u64 index = recs.index[b];
         const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
         cs_.mr[e] = v;
         cs_.term[e] = term;
@@ -394,7 +396,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     for (u32 f = t; f < total; f += kBlock) {
       const u32 b = rt.locate(f);
       const u64 v = recs.mr[b];
-      const u64 term = recs.term[b], index = recs.index[b];
+      const u32 t32 = recs.term32[b];
+      const u64 term = t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
+      const u64 index = recs.index[b];
       const u32 k = base + atomicAdd(&cur[u32(v) & 1023u], 1u);
       const u32 i = u32(v >> 32);
       const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
@@ -1142,14 +1146,16 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
     e = hipMemsetAsync(bshards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bucket shards)");
     const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags,
-                                      ld::U(in->index), ld::U(in->term), bshards, st);
+                                      ld::U(in->index), ld::U(in->term), bshards, st,
+                                      /*term32=*/true);
     if (rc != QB_OK) return rc;
     hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
                        dim3(kBlock), 0, st, c.geo, pt, cs, ctot);
     QB_CHECK_LAUNCH("k_ld_chunk_total");
     scan::launch(ctot, c.geo.NC, reinterpret_cast<u32*>(ws + c.cbsum), st);
     QB_CHECK_LAUNCH("scan(chunks)");
-    const bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 3);
+    bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 3);
+    b2.term32 = reinterpret_cast<u32*>(b2.term);
     hipLaunchKernelGGL(ld::k_ld_chunk_runs, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo,
                        b2, pt, cs, ctot, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");

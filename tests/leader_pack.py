@@ -101,7 +101,7 @@ def state_key(g: L.LeaderGroup):
 # --------------------------------------------------------------- fuzzing ---
 
 def random_groups(rng: np.random.Generator, G: int, inflight_cap: int, readq_cap: int,
-                  max_slots: int = 9):
+                  max_slots: int = 9, term_base: int = 0):
     groups = []
     for _ in range(G):
         ns = int(rng.integers(1, max_slots + 1))
@@ -116,7 +116,7 @@ def random_groups(rng: np.random.Generator, G: int, inflight_cap: int, readq_cap
                 if rng.random() < 0.5:
                     mout |= 1 << s
         del leader_mask
-        term = int(rng.integers(1, 50))
+        term = int(rng.integers(1, 50)) + term_base
         first = int(rng.integers(1, 40))
         last = first - 1 + int(rng.integers(0, 60))
         # term runs over [first-1, last]: ascending starts, the leader's term last

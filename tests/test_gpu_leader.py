@@ -69,9 +69,9 @@ def test_reference_scenarios_on_device(sc):
 
 
 def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_groups=0,
-          hot_frac=0.0):
+          hot_frac=0.0, term_base=0):
     rng = np.random.default_rng(seed)
-    groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots)
+    groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots, term_base)
     for g in groups:
         g.read_only = read_only
     recs = LP.random_records(rng, groups, M, hot_groups=hot_groups, hot_frac=hot_frac)
@@ -110,6 +110,12 @@ def test_fuzz_small(seed):
 
 def test_fuzz_lease_based_and_wide():
     _fuzz(11, G=300, M=1200, inflight_cap=5, readq_cap=2, read_only=1, max_slots=16)
+
+
+def test_fuzz_terms_past_32_bits():
+    """Group, record and log terms straddling 2^32 - 1: the bucketing moves
+    the term as u32 with an escape to the original batch (qb_bucket.h)."""
+    _fuzz(51, G=3000, M=9000, inflight_cap=6, readq_cap=3, term_base=(1 << 32) - 25)
 
 
 def test_fuzz_larger():
