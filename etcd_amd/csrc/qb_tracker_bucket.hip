@@ -38,12 +38,28 @@ __device__ __forceinline__ u64* shard_of(u64* shards) {
   return shards + u64(blockIdx.x % kShards) * QB_STAT_COUNT;
 }
 
-__global__ void k_stats_fold(const u64* __restrict__ shards, u64* __restrict__ stats) {
-  const int k = threadIdx.x;  // one thread per counter
-  if (k >= QB_STAT_COUNT) return;
-  u64 s = 0;
-  for (int i = 0; i < kShards; ++i) s += shards[i * QB_STAT_COUNT + k];
-  stats[k] += s;
+// One thread per shard (its 64-byte line in one go), wave sums by shuffles:
+// a thread per counter walking the 256 shards serially took 7 us.
+__global__ __launch_bounds__(kShards) void k_stats_fold(const u64* __restrict__ shards,
+                                                        u64* __restrict__ stats) {
+  __shared__ u64 part[kShards / 64][QB_STAT_COUNT];
+  const int i = threadIdx.x, lane = i & 63, w = i >> 6;
+  u64 x[QB_STAT_COUNT];
+#pragma unroll
+  for (int k = 0; k < QB_STAT_COUNT; ++k) x[k] = shards[i * QB_STAT_COUNT + k];
+#pragma unroll
+  for (int k = 0; k < QB_STAT_COUNT; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x[k] += __shfl_xor(x[k], o, 64);
+    if (lane == 0) part[w][k] = x[k];
+  }
+  __syncthreads();
+  if (i < QB_STAT_COUNT) {
+    u64 s = 0;
+#pragma unroll
+    for (int q = 0; q < kShards / 64; ++q) s += part[q][i];
+    stats[i] += s;
+  }
 }
 
 // ---------------------------------------------------------------- K1 ----
@@ -64,18 +80,41 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
   // atomic (a load -> use loop waited one HBM round trip per iteration).
   constexpr int kHistPer = kTile / kBlock;
   u32 gg[kHistPer];
-  u8 ff[kHistPer];
+  u32 ff[kHistPer];
+  u32 valid = 0;  // bit k: record k of this thread exists
+  // A full tile of aligned columns is read 4 records per lane (16-byte
+  // group and 4-byte flag loads: 5 load instructions instead of 32); the
+  // histogram does not depend on which thread counts which record.
+  const bool vec = t0 + kTile <= geo.M && (reinterpret_cast<uintptr_t>(rg) & 15u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(rf) & 3u) == 0;
+  if (vec) {
 #pragma unroll
-  for (int k = 0; k < kHistPer; ++k) {
-    const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
-    gg[k] = i < geo.M ? rg[i] : 0xFFFFFFFFu;
-    ff[k] = i < geo.M ? rf[i] : u8(0);
+    for (int q = 0; q < kHistPer / 4; ++q) {
+      const u64 i = t0 + u64(q) * (4 * kBlock) + 4u * threadIdx.x;
+      const uint4 gv = *reinterpret_cast<const uint4*>(rg + i);
+      const u32 fv = *reinterpret_cast<const u32*>(rf + i);
+      gg[4 * q] = gv.x;
+      gg[4 * q + 1] = gv.y;
+      gg[4 * q + 2] = gv.z;
+      gg[4 * q + 3] = gv.w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ff[4 * q + r] = (fv >> (8 * r)) & 0xFFu;
+    }
+    valid = (1u << kHistPer) - 1u;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) {
+      const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
+      const bool in = i < geo.M;
+      gg[k] = in ? rg[i] : 0xFFFFFFFFu;
+      ff[k] = in ? rf[i] : 0u;
+      valid |= u32(in) << k;
+    }
   }
 #pragma unroll
   for (int k = 0; k < kHistPer; ++k) {
-    const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
     bool bad = false, nonmember = false;
-    if (i < geo.M) {
+    if ((valid >> k) & 1u) {
       const u32 g = gg[k];
       bad = g >= geo.G;
       nonmember = !bad && (ff[k] & 0x0Fu) >= geo.n;
@@ -101,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
 constexpr u16 kNoBin = 0xFFFF;
 constexpr int kPartThreads = 1024;
 
-struct TileLds {
+struct alignas(16) TileLds {
   u16 bin[kTile];
   u16 rank[kTile];
   u16 perm[kTile];
@@ -176,14 +215,55 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
   u32 g[kPer], f[kPer];
   u64 vi[kPer], vt[kPer];
+  // A full tile of aligned columns is read as 4 consecutive records per
+  // lane (16-byte loads: 6 load instructions per thread instead of 16);
+  // record k of thread j is then rk(j).  Runs within a bucket carry no
+  // order (the LDS ranks are atomic), so the mapping is free.
+  static_assert(kPer == 4, "vector loads assume 4 records per thread");
+  const bool vec = nrec == u32(kTile) && (reinterpret_cast<uintptr_t>(rg) & 15u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(rf) & 3u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(ri) & 15u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(rt) & 15u) == 0;
+  auto rk = [&](int j) -> u32 {
+    return vec ? 4u * threadIdx.x + u32(j) : threadIdx.x + u32(j) * kPartThreads;
+  };
+  if (vec) {
+    const u64 i = t0 + 4u * threadIdx.x;
+    const uint4 gv = *reinterpret_cast<const uint4*>(rg + i);
+    const u32 fv = *reinterpret_cast<const u32*>(rf + i);
+    g[0] = gv.x;
+    g[1] = gv.y;
+    g[2] = gv.z;
+    g[3] = gv.w;
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const u32 k = threadIdx.x + j * kPartThreads;
-    const bool in = k < nrec;
-    g[j] = in ? rg[t0 + k] : 0xFFFFFFFFu;
-    f[j] = in ? rf[t0 + k] : 0u;
-    vi[j] = (in && ri) ? ri[t0 + k] : 0ull;
-    vt[j] = (in && ri) ? rt[t0 + k] : 0ull;
+    for (int j = 0; j < kPer; ++j) f[j] = (fv >> (8 * j)) & 0xFFu;
+    if (ri) {
+      const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ri + i);
+      const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(ri + i + 2);
+      const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(rt + i);
+      const ulonglong2 d = *reinterpret_cast<const ulonglong2*>(rt + i + 2);
+      vi[0] = a.x;
+      vi[1] = a.y;
+      vi[2] = b.x;
+      vi[3] = b.y;
+      vt[0] = c.x;
+      vt[1] = c.y;
+      vt[2] = d.x;
+      vt[3] = d.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) vi[j] = vt[j] = 0ull;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = rk(j);
+      const bool in = k < nrec;
+      g[j] = in ? rg[t0 + k] : 0xFFFFFFFFu;
+      f[j] = in ? rf[t0 + k] : 0u;
+      vi[j] = (in && ri) ? ri[t0 + k] : 0ull;
+      vt[j] = (in && ri) ? rt[t0 + k] : 0ull;
+    }
   }
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     start[b] = 0;
@@ -191,38 +271,60 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   }
   __syncthreads();
   const u32 sbgroups = geo.CH * kChunksPerSb;
+  if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
+    u64 bins = 0, ranks = 0;
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const u32 k = threadIdx.x + j * kPartThreads;
-    if (k >= nrec) continue;
-    u16 b = kNoBin;
-    if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
-      b = u16(g[j] / sbgroups);
-      L.rank[k] = u16(atomicAdd(&start[b], 1u));
+    for (int j = 0; j < kPer; ++j) {
+      u32 b = kNoBin, r = 0;
+      if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
+        b = g[j] / sbgroups;
+        r = atomicAdd(&start[b], 1u);
+      }
+      bins |= u64(b) << (16 * j);
+      ranks |= u64(r & 0xFFFFu) << (16 * j);
     }
-    L.bin[k] = b;
+    *reinterpret_cast<u64*>(&L.bin[4u * threadIdx.x]) = bins;
+    *reinterpret_cast<u64*>(&L.rank[4u * threadIdx.x]) = ranks;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = rk(j);
+      if (k >= nrec) continue;
+      u16 b = kNoBin;
+      if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
+        b = u16(g[j] / sbgroups);
+        L.rank[k] = u16(atomicAdd(&start[b], 1u));
+      }
+      L.bin[k] = b;
+    }
   }
   __syncthreads();
   const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
   tile_perm(L, start, nrec);
   // three payload columns: index, term, mr = meta | ridx << 32
   for (int col = ri ? 0 : 2; col < 3; ++col) {
+    u64 v[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      const u32 k = threadIdx.x + j * kPartThreads;
-      if (k >= nrec) continue;
-      u64 v;
+      const u32 k = rk(j);
       if (col == 0) {
-        v = vi[j];
+        v[j] = vi[j];
       } else if (col == 1) {
-        v = vt[j];
+        v[j] = vt[j];
       } else {
         const u32 chunk = g[j] / geo.CH;
         const u32 meta = (g[j] - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
                          ((f[j] & 0xFFu) << 17);
-        v = u64(meta) | (u64(u32(t0 + k)) << 32);
+        v[j] = u64(meta) | (u64(u32(t0 + k)) << 32);
       }
-      L.stage[k] = v;
+    }
+    if (vec) {  // two 16-byte LDS stores per lane (8-byte stores at a 32-byte stride conflict)
+      *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x]) = ulonglong2{v[0], v[1]};
+      *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x + 2]) = ulonglong2{v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (rk(j) < nrec) L.stage[rk(j)] = v[j];
     }
     __syncthreads();
     u64* dst = col == 0 ? out.index : col == 1 ? out.term : out.mr;
@@ -661,7 +763,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                      reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed),
                      stepdown_at, advanced_out, shards, st);
   QB_CHECK_LAUNCH("k_bk_apply");
-  hipLaunchKernelGGL(bk::k_stats_fold, dim3(1), dim3(64), 0, st, shards, stt);
+  hipLaunchKernelGGL(bk::k_stats_fold, dim3(1), dim3(bk::kShards), 0, st, shards, stt);
   QB_CHECK_LAUNCH("k_stats_fold");
   return QB_OK;
 }
