@@ -25,12 +25,14 @@ constexpr int kShards = 256;         // stat counter shards (one 64-byte line ea
 //   ridx = batch index of the record (step-down ordering).
 // term32 (optional, in the term column's space): the term as u32, or
 // kTermEscape when it does not fit, in which case the consumer reads the
-// full term from the original batch by ridx (the tracker step).
+// full term from the original batch by ridx (the leader step).  The tracker
+// step uses the packed form (two columns): index, and mr = meta | term32 << 32.
 struct Cols {
   u64* index;
   u64* term;
   u64* mr;
   u32* term32;
+  u32 packed;  // no term column and no ridx: mr = meta | term_to32(term) << 32
 };
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
 __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
@@ -78,17 +80,20 @@ inline Geometry geometry(u32 n, u64 G, u64 M) {
 
 // Workspace carve (all offsets 256-byte aligned).
 struct Carve {
-  size_t shards, hist, bsum, parts, chunk_start, buf1, buf2, total;
+  size_t shards, flags, chunk_flags, hist, bsum, parts, chunk_start, buf1, buf2, total;
 };
 // Upper bound on parts: every super-bucket contributes at most one partial.
 inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
-// ncols = 3: index, term and mr move with the records; ncols = 1: only mr
-// (callers that read the payload from the original batch by ridx).
+// ncols = 3: index, term and mr move with the records; ncols = 2: index and a
+// packed mr (Cols::packed); ncols = 1: only mr (callers that read the payload
+// from the original batch by ridx).
 inline Carve carve(const Geometry& g, int ncols = 3) {
   Carve c{};
   size_t o = 0;
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
+  c.flags = o;  o += 256;  // u32 words zeroed with the shards (any_slow)
+  c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
   c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
   c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
   // part table: pfirst[NSB+1], part_sb[max_parts], nparts
@@ -102,9 +107,12 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
   const size_t col = up256(sizeof(u64) * M);
-  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr};
+  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, 0};
+  if (ncols == 2)
+    return Cols{reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u64*>(base + col), nullptr,
+                1};
   return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
-              reinterpret_cast<u64*>(base + 2 * col), nullptr};
+              reinterpret_cast<u64*>(base + 2 * col), nullptr, 0};
 }
 
 
@@ -164,10 +172,11 @@ struct RunTable {
 // with n < 16 those with slot >= n into shards[QB_STAT_NON_MEMBER].
 // rec_index == rec_term == nullptr buckets the mr column alone (carve with
 // ncols = 1).  term32: the term column moves as u32 (term_to32), 4 bytes
-// per record less through both levels; read it with Cols::term32.
+// per record less through both levels; read it with Cols::term32.  packed
+// (carve with ncols = 2): index + mr = meta | term_to32 << 32, no batch index.
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32 = false);
+                   hipStream_t st, bool term32 = false, bool packed = false);
 
 }  // namespace bk
 }  // namespace qb

@@ -301,8 +301,10 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   __syncthreads();
   const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
   tile_perm(L, start, nrec);
-  // three payload columns: index, term, mr = meta | ridx << 32
+  // three payload columns: index, term, mr = meta | ridx << 32 (packed: index
+  // and mr = meta | term32 << 32)
   for (int col = ri ? 0 : 2; col < 3; ++col) {
+    if (col == 1 && out.packed) continue;
     u64 v[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
         const u32 chunk = g[j] / geo.CH;
         const u32 meta = (g[j] - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
                          ((f[j] & 0xFFu) << 17);
-        v[j] = u64(meta) | (u64(u32(t0 + k)) << 32);
+        v[j] = u64(meta) | (u64(out.packed ? term_to32(vt[j]) : u32(t0 + k)) << 32);
       }
     }
     if (vec) {  // two 16-byte LDS stores per lane (8-byte stores at a 32-byte stride conflict)
@@ -395,7 +397,9 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
     for (int j = 0; j < kPer; ++j) {
       const u32 k = threadIdx.x + j * kPartThreads;
       vi[j] = k < nrec ? in.index[lo + k] : 0ull;
-      vt[j] = k >= nrec ? 0ull : in.term32 ? u64(in.term32[lo + k]) : in.term[lo + k];
+      vt[j] = k >= nrec || in.packed ? 0ull
+              : in.term32            ? u64(in.term32[lo + k])
+                                     : in.term[lo + k];
     }
   }
   u64 vm[kPer];  // loaded together: one round trip, not one per record
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   tile_perm(L, start, nrec);
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
   __syncthreads();
-  for (int col = in.index ? 0 : 2; col < 2; ++col) {
+  for (int col = in.index ? 0 : 2; col < (in.packed ? 1 : 2); ++col) {
     u64* dst = col == 0 ? out.index : out.term;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -443,26 +447,32 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 
 
 // ---------------------------------------------------------------- K5 ----
+// Records arrive packed (index, mr = meta | term32 << 32): no batch index.
+// A chunk whose records all compare exactly against their group's term and
+// none of which is higher (the steady state) is applied here.  A chunk with
+// a higher-term record (the sequential leader steps down there and ignores
+// what follows, raft.go:875-879: batch order matters) or with a term32 escape
+// against a group term >= 2^32 - 1 (ambiguous compare) is "slow": K5 leaves
+// its state untouched, flags it, and k_bk_slow_* apply it from the original
+// batch in batch order (the exact two-pass form of qb_tracker.hip).
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
-// first_hi[CH] u32, act[CH] u32.
+// act[CH] u32.
 template <int N, bool NEXT>
 __global__ __launch_bounds__(kBlock) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
-    const u64* __restrict__ rec_term,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
-    u64* __restrict__ shards) {
+    u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards) {
   constexpr u32 CH = chunk_groups(N);
   constexpr u32 GPT = CH / kBlock;  // groups per thread in the commit phase
-  __shared__ u32 tl[5];
-  BlockTally<7> tally;  // 5, 6: the fused pass's applied / rejected
+  __shared__ u32 tl[3];
+  BlockTally<3> tally;
   __shared__ u64 acc_m[N * CH];
   __shared__ u64 acc_n[NEXT ? N * CH : 1];
   __shared__ u64 gterm[CH];
-  __shared__ u32 first_hi[CH];
   __shared__ u32 act[CH];
-  __shared__ u32 any_higher;
+  __shared__ u32 slow;
   const u32 c = blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
@@ -485,58 +495,49 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   }
   for (u32 k = threadIdx.x; k < CH; k += kBlock) {
     gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
-    first_hi[k] = 0xFFFFFFFFu;
     act[k] = 0;
   }
-  if (threadIdx.x == 0) any_higher = 0;
+  if (threadIdx.x == 0) slow = 0;
   // This chunk's records: one short run per part of its super-bucket,
   // flattened into one index space (RunTable) so every thread has a record
-  // in flight at once.
+  // in flight at once; kRecPer records per thread, both columns of each
+  // loaded before the first is classified.
   const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
   __shared__ RunTable rt;
-  // Fused pass: the term filter and, optimistically (no step-down in the
-  // chunk, the common case), MaybeUpdate as LDS atomic max and RecentActive.
-  // A higher-term record makes the sequential leader step down and ignore
-  // everything after it (raft.go:875-879): then the updates are redone
-  // below with the step-down order known.
-  // kRecPer records per thread are in flight at once: all three columns of
-  // each are loaded before the first is classified (one HBM round trip per
-  // kBlock * kRecPer records instead of two per kBlock).
   constexpr int kRecPer = 4;
   for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);
     for (u32 f0 = 0; f0 < total; f0 += kBlock * kRecPer) {
-      u64 rmr[kRecPer], rtm[kRecPer], rix[kRecPer];
+      u64 rmr[kRecPer], rix[kRecPer];
 #pragma unroll
       for (int r = 0; r < kRecPer; ++r) {
         const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
         rmr[r] = 0;
-        rtm[r] = 0;
         rix[r] = 0;
         if (f < total) {
           const u32 i = rt.locate(f);
           rmr[r] = recs.mr[i];
-          rtm[r] = recs.term32[i];
           rix[r] = recs.index[i];
         }
       }
 #pragma unroll
       for (int r = 0; r < kRecPer; ++r) {
         const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
-        bool stale = false, higher = false, applied = false, rejected = false;
+        bool stale = false, applied = false, rejected = false;
         if (f < total) {
           const u64 mr = rmr[r];
-          // a term past 32 bits comes from the original batch (kTermEscape)
-          const u64 term = rtm[r] != kTermEscape ? rtm[r] : rec_term[u32(mr >> 32)];
-          const u32 meta = u32(mr), lg = meta & 1023u, s = (meta >> 17) & 15u;
+          const u32 t32 = u32(mr >> 32), meta = u32(mr);
+          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
           const u64 gt = gterm[lg];
-          stale = term < gt;
-          higher = term > gt;
-          if (higher) {
-            atomicMin(&first_hi[lg], u32(mr >> 32));
-            any_higher = 1;
-          } else if (!stale) {
+          // t32 == kTermEscape: term >= 2^32 - 1, higher than any smaller group
+          // term and not comparable with a group term >= 2^32 - 1
+          const bool esc = t32 == kTermEscape;
+          if (esc || u64(t32) > gt) {
+            slow = 1;  // higher term (step-down order) or ambiguous compare
+          } else if (u64(t32) < gt) {
+            stale = true;                                   // raft.go:883-921
+          } else {
             atomicOr(&act[lg], 1u << s);                    // raft.go:1107
             if (meta & (1u << 24)) {  // QB_REC_REJECT
               rejected = true;                              // raft.go:1109: not MaybeUpdate
@@ -549,57 +550,25 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
           }
         }
         tally.add(0, stale);
-        tally.add(1, higher);
-        tally.add(5, applied);
-        tally.add(6, rejected);
+        tally.add(1, applied);
+        tally.add(2, rejected);
       }
     }
   }
   __syncthreads();
-  if (any_higher) {  // block-uniform: redo the updates in step-down order
-    for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
-      acc_m[k] = 0;
-      if constexpr (NEXT) acc_n[k] = 0;
+  if (slow) {  // block-uniform: state left for k_bk_slow_*, counts discarded
+#pragma unroll
+    for (u32 k = 0; k < GPT; ++k) {
+      const u32 lg = threadIdx.x + k * kBlock;
+      if (lg < ng) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
     }
-    for (u32 k = threadIdx.x; k < CH; k += kBlock) act[k] = 0;
-    __syncthreads();
-    for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
-      const u32 total = rt.build(cs, pb, p1, cl);
-      for (u32 f0 = 0; f0 < total; f0 += kBlock) {
-        const u32 f = f0 + threadIdx.x;
-        bool applied = false, rejected = false, after = false;
-        if (f < total) {
-          const u32 i = rt.locate(f);
-          const u64 mr = recs.mr[i];
-          const u32 meta = u32(mr), ridx = u32(mr >> 32);
-          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
-          const u32 t32 = recs.term32[i];
-          if ((t32 != kTermEscape ? u64(t32) : rec_term[ridx]) == gterm[lg]) {
-            if (ridx > first_hi[lg]) {
-              after = true;
-            } else {
-              atomicOr(&act[lg], 1u << s);
-              if (meta & (1u << 24)) {  // QB_REC_REJECT
-                rejected = true;
-              } else {
-                applied = true;
-                const u64 idx = recs.index[i];
-                atomicMax(&acc_m[s * CH + lg], idx);
-                if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);
-              }
-            }
-          }
-        }
-        tally.add(2, applied);
-        tally.add(3, rejected);
-        tally.add(4, after);
-      }
+    if (threadIdx.x == 0) {
+      chunk_slow[c] = 1;
+      atomicOr(any_slow, 1u);
     }
-    __syncthreads();
-  } else {
-    tally.t[2] = tally.t[5];
-    tally.t[3] = tally.t[6];
+    return;
   }
+  if (threadIdx.x == 0) chunk_slow[c] = 0;
   // maybeCommit for every group of the chunk + write-back (coalesced rows).
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
@@ -623,42 +592,158 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     const bool adv = ci > cm[k] && ci >= ts[k];  // log.go:328-334
     if (adv) committed[g] = ci;
     if (advanced) advanced[g] = adv ? 1 : 0;
-    stepdown_at[g] = first_hi[lg];
+    stepdown_at[g] = 0xFFFFFFFFu;
     if (act[lg]) active[g] = u16(active[g] | act[lg]);
   }
-  __shared__ u32 tl7[7];
-  (void)tl;
-  const int slot[7] = {QB_STAT_STALE_TERM, QB_STAT_HIGHER_TERM, QB_STAT_APPLIED,
-                       QB_STAT_REJECTED, QB_STAT_AFTER_STEPDOWN, QB_STAT_COUNT - 1,
-                       QB_STAT_COUNT - 1};
-  tally.t[5] = 0;
-  tally.t[6] = 0;
-  tally.flush(tl7, shard_of(shards), slot);
+  const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
+  tally.flush(tl, shard_of(shards), slot);
+}
+
+// ------------------------------------------------------ slow chunks ----
+// The flagged chunks' records, from the original batch in batch order,
+// exactly as qb_tracker.hip's two passes (k_appresp_stepdown/apply) and
+// k_commit_advance restricted to those chunks.  Every launch returns at once
+// when no chunk was flagged (*any_slow == 0, a uniform scalar load).
+constexpr unsigned kSlowBlocks = 2048;
+inline unsigned slow_grid(u64 units) {
+  const u64 g = (units + kBlock - 1) / kBlock;
+  return unsigned(g < 1 ? 1 : g < kSlowBlocks ? g : kSlowBlocks);
+}
+
+__device__ __forceinline__ bool in_slow_chunk(const Geometry& geo, u32 g, u32 f,
+                                              const u8* __restrict__ chunk_slow) {
+  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[g / geo.CH];
+}
+
+__global__ __launch_bounds__(kBlock) void k_bk_slow_stepdown(
+    Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
+    const u64* __restrict__ rt, const u64* __restrict__ group_term,
+    const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
+    u32* __restrict__ stepdown_at, u64* __restrict__ shards) {
+  if (*any_slow == 0) return;
+  __shared__ u32 tl[1];
+  BlockTally<1> tally;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < geo.M; i += stride) {
+    const u32 g = rg[i];
+    bool higher = false;
+    if (in_slow_chunk(geo, g, rf[i], chunk_slow) && rt[i] > group_term[g]) {
+      atomicMin(stepdown_at + g, u32(i));  // raft.go:875-879: first one in batch order
+      higher = true;
+    }
+    tally.add(0, higher);
+  }
+  const int slot[1] = {QB_STAT_HIGHER_TERM};
+  tally.flush(tl, shard_of(shards), slot);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bk_slow_apply(
+    Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
+    const u64* __restrict__ ri, const u64* __restrict__ rt, const u64* __restrict__ group_term,
+    const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
+    const u32* __restrict__ stepdown_at, u64* __restrict__ match, u64* __restrict__ next,
+    u16* __restrict__ active, u64* __restrict__ shards) {
+  if (*any_slow == 0) return;
+  __shared__ u32 tl[4];
+  BlockTally<4> tally;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < geo.M; i += stride) {
+    const u32 g = rg[i], f = rf[i];
+    bool stale = false, applied = false, rejected = false, after = false;
+    if (in_slow_chunk(geo, g, f, chunk_slow)) {
+      const u64 t = rt[i], gt = group_term[g];
+      stale = t < gt;
+      if (t == gt) {
+        if (stepdown_at[g] < u32(i)) {
+          after = true;  // the leader stepped down at an earlier record
+        } else {
+          const u32 s = f & 0x0Fu;
+          // RecentActive (raft.go:1107) as an atomic or on the aligned word
+          // holding active[g] (no 4-byte alignment asked of the caller)
+          const uintptr_t a = reinterpret_cast<uintptr_t>(active + g);
+          atomicOr(reinterpret_cast<u32*>(a & ~uintptr_t(3)), (1u << s) << ((a & 2u) * 8u));
+          if (f & QB_REC_REJECT) {
+            rejected = true;
+          } else {
+            applied = true;
+            const u64 idx = ri[i];
+            atomicMax(match + u64(s) * geo.G + g, idx);                  // progress.go:146-150
+            if (next) atomicMax(next + u64(s) * geo.G + g, idx + 1ull);  // progress.go:151
+          }
+        }
+      }
+    }
+    tally.add(0, stale);
+    tally.add(1, applied);
+    tally.add(2, rejected);
+    tally.add(3, after);
+  }
+  const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED,
+                       QB_STAT_AFTER_STEPDOWN};
+  tally.flush(tl, shard_of(shards), slot);
 }
 
 template <int N>
-void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs, const u64* gt,
-                  const u64* ts, const u64* rterm, u64* match, u64* next, u16* active, u64* committed,
-                  u32* stepdown, u8* adv, u64* stats, hipStream_t st) {
-  if (next)
+__global__ __launch_bounds__(kBlock) void k_bk_slow_commit(
+    Geometry geo, const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
+    const u64* __restrict__ match, const u64* __restrict__ term_start,
+    u64* __restrict__ committed, u8* __restrict__ advanced) {
+  if (*any_slow == 0) return;
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 g = u64(blockIdx.x) * kBlock + threadIdx.x; g < geo.G; g += stride) {
+    if (!chunk_slow[g / geo.CH]) continue;
+    u64 v[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) v[s] = match[u64(s) * geo.G + g];
+    const u64 ci = select_quorum<N>(v);
+    const u64 cm = committed[g];
+    const bool adv = ci > cm && ci >= term_start[g];  // log.go:328-334
+    if (adv) committed[g] = ci;
+    if (advanced) advanced[g] = adv ? 1 : 0;
+  }
+}
+
+struct ApplyArgs {
+  const u64 *gt, *ts;
+  u64 *match, *next;
+  u16* active;
+  u64* committed;
+  u32* stepdown;
+  u8* adv;
+  u8* chunk_slow;
+  u32* any_slow;
+  u64* stats;
+};
+
+template <int N>
+void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+                  const ApplyArgs& a, hipStream_t st) {
+  if (a.next)
     hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
-                       cs, gt, ts, rterm, match, next, active, committed, stepdown, adv, stats);
+                       cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
+                       a.chunk_slow, a.any_slow, a.stats);
   else
     hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
-                       cs, gt, ts, rterm, match, next, active, committed, stepdown, adv, stats);
+                       cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
+                       a.chunk_slow, a.any_slow, a.stats);
+}
+
+template <int N>
+void launch_slow_commit(const Geometry& geo, const ApplyArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_bk_slow_commit<N>), dim3(slow_grid(geo.G)), dim3(kBlock), 0, st, geo,
+                     a.chunk_slow, a.any_slow, a.match, a.ts, a.committed, a.adv);
 }
 
 template <int... Ns>
-void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
-                    Cols recs, const u32* pt, const u32* cs, const u64* gt, const u64* ts,
-                    const u64* rterm,
-                    u64* match,
-                    u64* next, u16* active, u64* committed, u32* stepdown, u8* adv, u64* stats,
-                    hipStream_t st) {
-  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, gt, ts, rterm, match, next, active,
-                                       committed, stepdown, adv, stats, st)
-                : void()),
-   ...);
+void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& geo, Cols recs,
+                    const u32* pt, const u32* cs, const ApplyArgs& a, hipStream_t st) {
+  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, a, st) : void()), ...);
+}
+
+template <int... Ns>
+void dispatch_slow_commit(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
+                          const ApplyArgs& a, hipStream_t st) {
+  ((n == Ns + 1 ? launch_slow_commit<Ns + 1>(geo, a, st) : void()), ...);
 }
 
 }  // namespace bk
@@ -671,15 +756,15 @@ namespace bk {
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32) {
+                   hipStream_t st, bool term32, bool packed) {
   u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
   u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const int ncols = rec_index ? 3 : 1;
+  const int ncols = !rec_index ? 1 : packed ? 2 : 3;
   Cols buf1 = cols_at(ws + cv.buf1, geo.M, ncols);
   Cols buf2 = cols_at(ws + cv.buf2, geo.M, ncols);
-  if (term32 && rec_index) {
+  if (term32 && ncols == 3) {
     buf1.term32 = reinterpret_cast<u32*>(buf1.term);
     buf2.term32 = reinterpret_cast<u32*>(buf2.term);
   }
@@ -713,7 +798,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
 
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
-  return bk::carve(bk::geometry(n, G, M)).total;
+  return bk::carve(bk::geometry(n, G, M), 2).total;
 }
 
 extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
@@ -733,7 +818,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
              "record pointer is NULL");
   const bk::Geometry geo = bk::geometry(n, G, M);
-  const bk::Carve cv = bk::carve(geo);
+  const bk::Carve cv = bk::carve(geo, 2);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
              "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv.total);
   QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
@@ -742,27 +827,44 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M);
-  buf2.term32 = reinterpret_cast<u32*>(buf2.term);
+  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M, 2);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
-  hipError_t e0 = hipMemsetAsync(shards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
+  // stat shards and the any_slow word (contiguous) start at zero
+  hipError_t e0 = hipMemsetAsync(shards, 0, cv.flags + 256 - cv.shards, st);
   if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(stat shards)");
-
+  const auto* rg = reinterpret_cast<const u32*>(rec_group);
+  const auto* ri = reinterpret_cast<const u64*>(rec_index);
+  const auto* rtm = reinterpret_cast<const u64*>(rec_term);
   {
-    const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags,
-                                      reinterpret_cast<const u64*>(rec_index),
-                                      reinterpret_cast<const u64*>(rec_term), shards, st,
-                                      /*term32=*/true);
+    const int rc = bk::bucket_records(geo, cv, ws, rg, rec_flags, ri, rtm, shards, st,
+                                      /*term32=*/false, /*packed=*/true);
     if (rc != QB_OK) return rc;
   }
-  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs,
-                     reinterpret_cast<const u64*>(group_term),
-                     reinterpret_cast<const u64*>(term_start),
-                     reinterpret_cast<const u64*>(rec_term), reinterpret_cast<u64*>(match),
-                     reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed),
-                     stepdown_at, advanced_out, shards, st);
+  const bk::ApplyArgs a{reinterpret_cast<const u64*>(group_term),
+                        reinterpret_cast<const u64*>(term_start),
+                        reinterpret_cast<u64*>(match),
+                        reinterpret_cast<u64*>(next),
+                        active,
+                        reinterpret_cast<u64*>(committed),
+                        stepdown_at,
+                        advanced_out,
+                        reinterpret_cast<u8*>(ws + cv.chunk_flags),
+                        reinterpret_cast<u32*>(ws + cv.flags),
+                        shards};
+  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs, a,
+                     st);
   QB_CHECK_LAUNCH("k_bk_apply");
+  if (M > 0) {  // chunks flagged slow by K5 (none in the steady state: each launch returns at once)
+    const dim3 rgrid(bk::slow_grid(M));
+    hipLaunchKernelGGL(bk::k_bk_slow_stepdown, rgrid, dim3(kBlock), 0, st, geo, rg, rec_flags, rtm,
+                       a.gt, a.chunk_slow, a.any_slow, stepdown_at, shards);
+    hipLaunchKernelGGL(bk::k_bk_slow_apply, rgrid, dim3(kBlock), 0, st, geo, rg, rec_flags, ri, rtm,
+                       a.gt, a.chunk_slow, a.any_slow, stepdown_at, a.match, a.next, active,
+                       shards);
+    bk::dispatch_slow_commit(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, st);
+    QB_CHECK_LAUNCH("k_bk_slow");
+  }
   hipLaunchKernelGGL(bk::k_stats_fold, dim3(1), dim3(bk::kShards), 0, st, shards, stt);
   QB_CHECK_LAUNCH("k_stats_fold");
   return QB_OK;
