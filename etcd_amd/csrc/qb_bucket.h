@@ -60,7 +60,7 @@ struct Geometry {
   u64 G, M;
   u32 n, CH, NC, NSB, NT;
   u32 xcd;  // tiles of K1/K3 mapped XCD-major (see xcd_major)
-  u64 nbins() const { return u64(NSB) * NT; }
+  __host__ __device__ u64 nbins() const { return u64(NSB) * NT; }
   u32 tile_grid() const { return xcd ? (NT + kXcds - 1) / kXcds * kXcds : NT; }
   __device__ __forceinline__ u32 tile() const { return xcd ? xcd_major() : blockIdx.x; }
 };
@@ -80,7 +80,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M) {
 
 // Workspace carve (all offsets 256-byte aligned).
 struct Carve {
-  size_t shards, flags, chunk_flags, hist, bsum, parts, chunk_start, buf1, buf2, total;
+  size_t shards, flags, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, total;
 };
 // Upper bound on parts: every super-bucket contributes at most one partial.
 inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
@@ -94,6 +94,7 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
   c.flags = o;  o += 256;  // u32 words zeroed with the shards (any_slow)
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
+  c.inval = o;  o += up256(sizeof(u32) * 2 * (u64(g.NT) + 1));  // per tile: bad, non-member
   c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
   c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
   // part table: pfirst[NSB+1], part_sb[max_parts], nparts
@@ -174,6 +175,9 @@ struct RunTable {
 // ncols = 1).  term32: the term column moves as u32 (term_to32), 4 bytes
 // per record less through both levels; read it with Cols::term32.  packed
 // (carve with ncols = 2): index + mr = meta | term_to32 << 32, no batch index.
+// K2 zeroes [cv.shards, cv.flags + 256) (stat shards and flag words) before
+// anything counts into them, so the caller needs no memset; K2's add-back is folded into its readers
+// (the hist array keeps per-4096 local scans, see off_at).
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
                    hipStream_t st, bool term32 = false, bool packed = false);

@@ -39,9 +39,11 @@ __device__ __forceinline__ u64* shard_of(u64* shards) {
 }
 
 // One thread per shard (its 64-byte line in one go), wave sums by shuffles:
-// a thread per counter walking the 256 shards serially took 7 us.
-__global__ __launch_bounds__(kShards) void k_stats_fold(const u64* __restrict__ shards,
-                                                        u64* __restrict__ stats) {
+// a thread per counter walking the 256 shards serially took 7 us.  Run by
+// one block of kShards threads (block 0 of k_bk_finish).
+static_assert(kShards == kBlock, "the fold runs in one kBlock-thread block");
+__device__ __forceinline__ void stats_fold_block(const u64* __restrict__ shards,
+                                                 u64* __restrict__ stats) {
   __shared__ u64 part[kShards / 64][QB_STAT_COUNT];
   const int i = threadIdx.x, lane = i & 63, w = i >> 6;
   u64 x[QB_STAT_COUNT];
@@ -63,15 +65,17 @@ __global__ __launch_bounds__(kShards) void k_stats_fold(const u64* __restrict__ 
 }
 
 // ---------------------------------------------------------------- K1 ----
+// Invalid records (group >= G, slot >= n) are counted per tile into inval[2
+// * tile + {0, 1}] with plain stores; k_bk_sums_parts adds them to the stat
+// shards after zeroing those (so the step needs no memset).
 __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __restrict__ rg,
                                                     const u8* __restrict__ rf,
                                                     u32* __restrict__ hist,
-                                                    u64* __restrict__ shards) {
+                                                    u32* __restrict__ inval) {
   extern __shared__ __attribute__((aligned(16))) u32 lh[];  // NSB counters
   __shared__ u32 tl[2];
   const u32 tile = geo.tile();
   if (tile >= geo.NT) return;  // XCD-major grid is rounded up to a multiple of kXcds
-  BlockTally<2> tally;
   for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) lh[b] = 0;
   __syncthreads();
   const u64 t0 = u64(tile) * kTile;
@@ -111,25 +115,35 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
       valid |= u32(in) << k;
     }
   }
+  if (threadIdx.x < 2) tl[threadIdx.x] = 0;
+  u32 nbad = 0, nnon = 0;  // wave-uniform counts
 #pragma unroll
   for (int k = 0; k < kHistPer; ++k) {
-    bool bad = false, nonmember = false;
-    if ((valid >> k) & 1u) {
-      const u32 g = gg[k];
-      bad = g >= geo.G;
-      nonmember = !bad && (ff[k] & 0x0Fu) >= geo.n;
-      if (!bad && !nonmember) atomicAdd(&lh[g / sbgroups], 1u);
-    }
-    tally.add(0, bad);
-    tally.add(1, nonmember);
+    const u32 g = gg[k];
+    const bool in = (valid >> k) & 1u, bad = in && g >= geo.G;
+    const bool non = in && !bad && (ff[k] & 0x0Fu) >= geo.n;
+    if (in && !bad && !non) atomicAdd(&lh[g / sbgroups], 1u);
+    nbad += wave_popc(bad);
+    nnon += wave_popc(non);
   }
   __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    if (nbad) atomicAdd(&tl[0], nbad);
+    if (nnon) atomicAdd(&tl[1], nnon);
+  }
   for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) hist[u64(b) * geo.NT + tile] = lh[b];
-  const int slot[2] = {QB_STAT_BAD_GROUP, QB_STAT_NON_MEMBER};
-  tally.flush(tl, shard_of(shards), slot);
+  __syncthreads();
+  if (threadIdx.x < 2) inval[2 * tile + threadIdx.x] = tl[threadIdx.x];
 }
 
-// K2 is scan::k_scan_* (qb_scan.h).
+// K2: scan::k_scan_local (qb_scan.h) leaves per-4096 local exclusive scans in
+// hist; k_bk_sums_parts scans the block sums and derives the parts.  The
+// add-back pass is folded into the readers: offset i = hist[i] + bsum[i/4096]
+// (off_at), and hist[nbins] = total.
+__device__ __forceinline__ u32 off_at(const u32* __restrict__ hist, const u32* __restrict__ bsum,
+                                      u64 nb, u64 i) {
+  return i < nb ? hist[i] + bsum[i / kScanPer] : hist[nb];
+}
 
 // ------------------------------------------------ LDS tile partition ----
 // Counting sort of one tile (<= kTile records) by a small key, in LDS.  The
@@ -204,7 +218,7 @@ constexpr int kPer = kTile / kPartThreads;  // records per thread
 __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
-    Cols out) {
+    const u32* __restrict__ bsum, Cols out) {
   extern __shared__ __attribute__((aligned(16))) u32 dyn[];
   u32* start = dyn;               // NSB: count, then local exclusive start
   u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
@@ -265,9 +279,10 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
       vt[j] = (in && ri) ? rt[t0 + k] : 0ull;
     }
   }
+  const u64 nb = geo.nbins();
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     start[b] = 0;
-    gstart[b] = offsets[u64(b) * geo.NT + tile];
+    gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
   }
   __syncthreads();
   const u32 sbgroups = geo.CH * kChunksPerSb;
@@ -348,17 +363,56 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
 }
 
 // --------------------------------------------------------------- K3b ----
-// Parts: super-bucket sb (records [lo, hi) of buf1) is cut into
-// ceil((hi - lo) / kTile) parts.  pfirst[sb] = first part of sb,
-// part_sb[p] = its super-bucket, nparts = pfirst[NSB].
-__global__ __launch_bounds__(1024) void k_bk_parts(Geometry geo, const u32* __restrict__ offsets,
-                                                   u32* __restrict__ pt) {
+// One block: exclusive scan of the per-4096 scan-block sums (bsum, in
+// place; hist[nbins] = total), then the parts: super-bucket sb (records
+// [lo, hi) of buf1) is cut into ceil((hi - lo) / kTile) parts.  pfirst[sb] =
+// first part of sb, part_sb[p] = its super-bucket, nparts = pfirst[NSB].
+// It also zeroes the stat shards / flag words ([zero, zero + nzero) u64) and
+// puts K1's invalid-record counts (inval) into shard 0.
+__global__ __launch_bounds__(1024) void k_bk_sums_parts(Geometry geo, u32* __restrict__ hist,
+                                                        u32* __restrict__ bsum, u32 nblk,
+                                                        u32* __restrict__ pt,
+                                                        const u32* __restrict__ inval,
+                                                        u64* __restrict__ zero, u32 nzero) {
+  __shared__ u32 sh[1024 + 32];
+  {
+    u64 nbad = 0, nnon = 0;
+    for (u32 t = threadIdx.x; t < geo.NT; t += blockDim.x) {
+      nbad += inval[2 * t];
+      nnon += inval[2 * t + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      nbad += __shfl_xor(nbad, o, 64);
+      nnon += __shfl_xor(nnon, o, 64);
+    }
+    for (u32 k = threadIdx.x; k < nzero; k += blockDim.x) zero[k] = 0;
+    __threadfence();  // the zeros reach L2 before this block's atomics below
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {  // shard 0 (one line): zeroed above by this block
+      if (nbad) atomicAdd(zero + QB_STAT_BAD_GROUP, nbad);
+      if (nnon) atomicAdd(zero + QB_STAT_NON_MEMBER, nnon);
+    }
+  }
+  const u64 nb = geo.nbins();
+  u32 carry = 0;
+  for (u32 base = 0; base < nblk; base += 1024) {
+    const u32 i = base + threadIdx.x;
+    const u32 v = i < nblk ? bsum[i] : 0u;
+    u32 total;
+    const u32 ex = scan::block_exclusive_scan_1024(v, sh, &total);
+    if (i < nblk) bsum[i] = ex + carry;
+    carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) hist[nb] = carry;
+  __threadfence_block();
+  __syncthreads();  // this block's bsum / hist[nb] stores are visible to it
   u32* pfirst = pt;                  // NSB + 1
   u32* part_sb = pt + geo.NSB + 2;   // max_parts
   __shared__ u32 cnt[4096];
   __shared__ u32 wsum[16];
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
-    const u32 n = offsets[u64(b + 1) * geo.NT] - offsets[u64(b) * geo.NT];
+    const u32 n = off_at(hist, bsum, nb, u64(b + 1) * geo.NT) - off_at(hist, bsum, nb, u64(b) * geo.NT);
     cnt[b] = (n + kTile - 1) / kTile;
   }
   __syncthreads();
@@ -377,6 +431,7 @@ __global__ __launch_bounds__(1024) void k_bk_parts(Geometry geo, const u32* __re
 // in part p (cs[p][128] = part end).
 __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
                                                            const u32* __restrict__ offsets,
+                                                           const u32* __restrict__ bsum,
                                                            const u32* __restrict__ pt, Cols in,
                                                            Cols out, u32* __restrict__ cs) {
   const u32* pfirst = pt;
@@ -386,7 +441,8 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   __shared__ TileLds L;
   __shared__ u32 start[kChunksPerSb];
   const u32 sb = part_sb[p];
-  const u32 sb_lo = offsets[u64(sb) * geo.NT], sb_hi = offsets[u64(sb + 1) * geo.NT];
+  const u32 sb_lo = off_at(offsets, bsum, geo.nbins(), u64(sb) * geo.NT);
+  const u32 sb_hi = off_at(offsets, bsum, geo.nbins(), u64(sb + 1) * geo.NT);
   const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
   const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
   const u32 nrec = hi - lo;
@@ -683,11 +739,16 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow_apply(
   tally.flush(tl, shard_of(shards), slot);
 }
 
+// Last kernel of the step: block 0 folds the stat shards into the caller's
+// stats (every counting kernel has finished), then maybeCommit for the
+// groups of flagged chunks.
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bk_slow_commit(
+__global__ __launch_bounds__(kBlock) void k_bk_finish(
     Geometry geo, const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
     const u64* __restrict__ match, const u64* __restrict__ term_start,
-    u64* __restrict__ committed, u8* __restrict__ advanced) {
+    u64* __restrict__ committed, u8* __restrict__ advanced, const u64* __restrict__ shards,
+    u64* __restrict__ stats) {
+  if (blockIdx.x == 0) stats_fold_block(shards, stats);
   if (*any_slow == 0) return;
   const u64 stride = u64(gridDim.x) * kBlock;
   for (u64 g = u64(blockIdx.x) * kBlock + threadIdx.x; g < geo.G; g += stride) {
@@ -729,9 +790,9 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
 }
 
 template <int N>
-void launch_slow_commit(const Geometry& geo, const ApplyArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((k_bk_slow_commit<N>), dim3(slow_grid(geo.G)), dim3(kBlock), 0, st, geo,
-                     a.chunk_slow, a.any_slow, a.match, a.ts, a.committed, a.adv);
+void launch_finish(const Geometry& geo, const ApplyArgs& a, u64* stats, hipStream_t st) {
+  hipLaunchKernelGGL((k_bk_finish<N>), dim3(slow_grid(geo.G)), dim3(kBlock), 0, st, geo,
+                     a.chunk_slow, a.any_slow, a.match, a.ts, a.committed, a.adv, a.stats, stats);
 }
 
 template <int... Ns>
@@ -741,9 +802,9 @@ void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& ge
 }
 
 template <int... Ns>
-void dispatch_slow_commit(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
-                          const ApplyArgs& a, hipStream_t st) {
-  ((n == Ns + 1 ? launch_slow_commit<Ns + 1>(geo, a, st) : void()), ...);
+void dispatch_finish(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
+                     const ApplyArgs& a, u64* stats, hipStream_t st) {
+  ((n == Ns + 1 ? launch_finish<Ns + 1>(geo, a, stats, st) : void()), ...);
 }
 
 }  // namespace bk
@@ -769,26 +830,29 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
     buf2.term32 = reinterpret_cast<u32*>(buf2.term);
   }
   const size_t lds_bins = sizeof(u32) * geo.NSB;
+  // k_bk_sums_parts zeroes the stat shards and flag words: [cv.shards, cv.flags + 256)
+  u64* zero = reinterpret_cast<u64*>(ws + cv.shards);
+  u32* inval = reinterpret_cast<u32*>(ws + cv.inval);
+  const u32 nzero = u32((cv.flags + 256 - cv.shards) / sizeof(u64));
   if (geo.M == 0) {
     hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
+    if (e == hipSuccess) e = hipMemsetAsync(zero, 0, sizeof(u64) * nzero, st);
     return e == hipSuccess ? QB_OK : hip_fail(e, "hipMemsetAsync(parts)");
   }
   hipLaunchKernelGGL(k_bk_hist, dim3(geo.tile_grid()), dim3(kBlock), lds_bins, st, geo, rec_group,
-                     rec_flags, hist, shards);
+                     rec_flags, hist, inval);
   QB_CHECK_LAUNCH("k_bk_hist");
   const u64 nb = geo.nbins();
   const u32 nblk = u32((nb + kScanPer - 1) / kScanPer);
   hipLaunchKernelGGL(scan::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
-  hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nblk, hist + nb);
-  hipLaunchKernelGGL(scan::k_scan_add, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
+  hipLaunchKernelGGL(k_bk_sums_parts, dim3(1), dim3(1024), 0, st, geo, hist, bsum, nblk, pt,
+                     inval, zero, nzero);
   QB_CHECK_LAUNCH("k_scan");
   hipLaunchKernelGGL(k_bk_scatter, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st, geo,
-                     rec_group, rec_flags, rec_index, rec_term, hist, buf1);
+                     rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1);
   QB_CHECK_LAUNCH("k_bk_scatter");
-  hipLaunchKernelGGL(k_bk_parts, dim3(1), dim3(1024), 0, st, geo, hist, pt);
-  QB_CHECK_LAUNCH("k_bk_parts");
   hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
-                     geo, hist, pt, buf1, buf2, cs);
+                     geo, hist, bsum, pt, buf1, buf2, cs);
   QB_CHECK_LAUNCH("k_bk_split");
   return QB_OK;
 }
@@ -830,9 +894,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M, 2);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
-  // stat shards and the any_slow word (contiguous) start at zero
-  hipError_t e0 = hipMemsetAsync(shards, 0, cv.flags + 256 - cv.shards, st);
-  if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(stat shards)");
+  // the stat shards and the any_slow word start at zero (bucket_records: K1)
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
@@ -862,10 +924,10 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
     hipLaunchKernelGGL(bk::k_bk_slow_apply, rgrid, dim3(kBlock), 0, st, geo, rg, rec_flags, ri, rtm,
                        a.gt, a.chunk_slow, a.any_slow, stepdown_at, a.match, a.next, active,
                        shards);
-    bk::dispatch_slow_commit(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, st);
     QB_CHECK_LAUNCH("k_bk_slow");
   }
-  hipLaunchKernelGGL(bk::k_stats_fold, dim3(1), dim3(bk::kShards), 0, st, shards, stt);
-  QB_CHECK_LAUNCH("k_stats_fold");
+  // stat fold + maybeCommit of flagged chunks
+  bk::dispatch_finish(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, stt, st);
+  QB_CHECK_LAUNCH("k_bk_finish");
   return QB_OK;
 }
