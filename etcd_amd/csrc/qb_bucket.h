@@ -94,7 +94,7 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
   c.flags = o;  o += 256;  // u32 words zeroed with the shards (any_slow)
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
-  c.inval = o;  o += up256(sizeof(u32) * 2 * (u64(g.NT) + 1));  // per tile: bad, non-member
+  c.inval = o;  o += up256(sizeof(u32) * 2 * (u64(g.NT) + 2));  // per tile: bad, non-member
   c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
   c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
   // part table: pfirst[NSB+1], part_sb[max_parts], nparts

@@ -1143,8 +1143,7 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
     u32* ctot = reinterpret_cast<u32*>(ws + c.ctot);
     const u32* pt = reinterpret_cast<const u32*>(bws + c.bcv.parts);
     const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
-    e = hipMemsetAsync(bshards, 0, sizeof(u64) * QB_STAT_COUNT * bk::kShards, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bucket shards)");
+    // bucket_records zeroes bshards itself (before its first count)
     const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags,
                                       ld::U(in->index), ld::U(in->term), bshards, st,
                                       /*term32=*/true);

@@ -367,30 +367,33 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
 // place; hist[nbins] = total), then the parts: super-bucket sb (records
 // [lo, hi) of buf1) is cut into ceil((hi - lo) / kTile) parts.  pfirst[sb] =
 // first part of sb, part_sb[p] = its super-bucket, nparts = pfirst[NSB].
-// It also zeroes the stat shards / flag words ([zero, zero + nzero) u64) and
-// puts K1's invalid-record counts (inval) into shard 0.
+// It also writes the stat shards / flag words ([zero, zero + nzero) u64):
+// zero, except K1's invalid-record counts (inval) in shard 0.
 __global__ __launch_bounds__(1024) void k_bk_sums_parts(Geometry geo, u32* __restrict__ hist,
                                                         u32* __restrict__ bsum, u32 nblk,
                                                         u32* __restrict__ pt,
                                                         const u32* __restrict__ inval,
                                                         u64* __restrict__ zero, u32 nzero) {
   __shared__ u32 sh[1024 + 32];
-  {
-    u64 nbad = 0, nnon = 0;
-    for (u32 t = threadIdx.x; t < geo.NT; t += blockDim.x) {
-      nbad += inval[2 * t];
-      nnon += inval[2 * t + 1];
+  __shared__ u32 red[2][16];
+  // K1's per-tile (bad, non-member) pairs: 16-byte loads issued before the
+  // block-sum scan so their latency overlaps it (the carve pads inval to
+  // whole 16-byte pieces; pieces past 2 * NT are masked)
+  const u32 ne = 2 * geo.NT, nq = (ne + 3) / 4;
+  const uint4* iv4 = reinterpret_cast<const uint4*>(inval);
+  u32 nbad = 0, nnon = 0;
+  for (u32 q0 = 0; q0 < nq; q0 += 4 * 1024) {
+    uint4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const u32 q = q0 + u32(r) * 1024 + threadIdx.x;
+      v[r] = q < nq ? iv4[q] : make_uint4(0, 0, 0, 0);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      nbad += __shfl_xor(nbad, o, 64);
-      nnon += __shfl_xor(nnon, o, 64);
-    }
-    for (u32 k = threadIdx.x; k < nzero; k += blockDim.x) zero[k] = 0;
-    __threadfence();  // the zeros reach L2 before this block's atomics below
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) {  // shard 0 (one line): zeroed above by this block
-      if (nbad) atomicAdd(zero + QB_STAT_BAD_GROUP, nbad);
-      if (nnon) atomicAdd(zero + QB_STAT_NON_MEMBER, nnon);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const u32 e = 4 * (q0 + u32(r) * 1024 + threadIdx.x);
+      if (e < ne) nbad += v[r].x, nnon += v[r].y;
+      if (e + 2 < ne) nbad += v[r].z, nnon += v[r].w;
     }
   }
   const u64 nb = geo.nbins();
@@ -405,6 +408,21 @@ __global__ __launch_bounds__(1024) void k_bk_sums_parts(Geometry geo, u32* __res
     __syncthreads();
   }
   if (threadIdx.x == 0) hist[nb] = carry;
+  // stat shards / flag words start at zero, except shard 0's invalid counts
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nbad += __shfl_xor(nbad, o, 64);
+    nnon += __shfl_xor(nnon, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = nbad;
+    red[1][threadIdx.x >> 6] = nnon;
+  }
+  __syncthreads();
+  u64 tb = 0, tn = 0;
+  for (u32 w = 0; w < blockDim.x / 64; ++w) tb += red[0][w], tn += red[1][w];
+  for (u32 k = threadIdx.x; k < nzero; k += blockDim.x)
+    zero[k] = k == QB_STAT_BAD_GROUP ? tb : k == QB_STAT_NON_MEMBER ? tn : 0ull;
   __threadfence_block();
   __syncthreads();  // this block's bsum / hist[nb] stores are visible to it
   u32* pfirst = pt;                  // NSB + 1
