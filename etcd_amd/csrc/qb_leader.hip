@@ -1129,8 +1129,8 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
   u32* pool = reinterpret_cast<u32*>(ws + c.pool);
   u64* shards = reinterpret_cast<u64*>(ws + c.shards);
-  hipError_t e = hipMemsetAsync(pool, 0, sizeof(u32) * 2, st);
-  if (e == hipSuccess) e = hipMemsetAsync(shards, 0, sizeof(u64) * QB_LSTAT_COUNT * 64, st);
+  // pool and stat shards are adjacent in the carve: one memset zeroes both
+  hipError_t e = hipMemsetAsync(pool, 0, c.shards - c.pool + sizeof(u64) * QB_LSTAT_COUNT * 64, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
   u64* bshards = nullptr;
   // QB_LEADER_GROUPING=atomic selects the per-record-atomic grouping even
