@@ -69,12 +69,16 @@ class HipEvents:
         self.hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
         self.hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
         self.hip.hipEventDestroy.argtypes = [C.c_void_p]
+        self.hip.hipEventSynchronize.argtypes = [C.c_void_p]
         self.ev = []
         for _ in range(count):
             e = C.c_void_p()
             assert self.hip.hipEventCreate(C.byref(e)) == 0
             self.ev.append(e)
         self.record = self.hip.hipEventRecord
+
+    def synchronize(self, a: int):
+        assert self.hip.hipEventSynchronize(self.ev[a]) == 0
 
     def elapsed_ms(self, a: int, b: int) -> float:
         ms = C.c_float()
@@ -149,6 +153,263 @@ def cpu_baseline_csr(kind: str, seconds: float):
                       f"majority.go/joint.go (oracle/quorum_oracle.c); {reps} passes on "
                       f"{threads} threads"}
 
+# ------------------------------------------------------------------ tracker ---
+# BASELINE configs[4]: "Streaming ProgressTracker: batched MsgAppResp
+# scatter-max + commit advance, 128M groups x8 GPUs" = 16M 5-voter groups per
+# GPU.  One step = one qb_dev_fixed_tracker_step over one batch of G records
+# (one MsgAppResp per group on average, random arrival order, 1 % stale term)
+# on HBM-resident leader state.  A live stream: the leader holds E new entries
+# per step, batch k acknowledges last + (k+1)E - lag (lag < 96) for a random
+# follower (slot 1..4) of a random group, so every step raises matches and
+# advances commits (a replayed batch would leave the state unchanged after its
+# first application).  Every step's batch is distinct and resident before the
+# timed region (336 MB each).
+TRACKER_E = 64
+TRACKER_SEED = 0x5EED0005
+TRACKER_MAX_BATCHES = 64
+# SURVEY.md §8d per group-step: record 21 B (group 4, flags 1, index 8, term 8)
+# + match RMW 16 B + commit advance 64 B (match 40 + term_start 8 + committed 8
+# read, committed 8 written)
+TRACKER_BYTES = 101
+
+
+def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7):
+    """nb distinct streaming batches (device tensors)."""
+    out = []
+    for k in range(nb):
+        group = torch.randint(0, G, (G,), generator=gen, device=dev, dtype=torch.int32)
+        slot = n_slots_fn(group, gen)
+        lag = torch.randint(0, 96, (G,), generator=gen, device=dev, dtype=torch.int64)
+        index = last[group.long()] + (k + 1) * TRACKER_E - lag
+        term = torch.where(torch.rand(G, generator=gen, device=dev) < 0.01, seed_term - 1,
+                           seed_term).to(torch.int64)
+        out.append(batch.AppRespBatch(group, slot.to(torch.uint8), index, term))
+    return out
+
+
+def tracker_cpu_baseline(seconds: float, csr: bool):
+    """The oracle's sequential stepLeader restatement (one record at a time in
+    batch order: term filter, MaybeUpdate, maybeCommit when updated;
+    oracle/quorum_oracle.c appresp_range) on a bounded sample of the same
+    stream: 1M groups, 8 consecutive 1M-record batches per pass, groups
+    partitioned over 16 host threads (each scans the batch for its own groups
+    — exactly the sequential result) and on 1 thread."""
+    from tests import oracle_c as oc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    Gs, R, n = 1 << 20, 8, 5
+    rng = np.random.default_rng(5)
+    if csr:
+        off, m0, cfg, _ = oc.gen_csr(0x5EED0003, "ragged", Gs)
+        sizes = np.diff(off.astype(np.int64))
+        last = m0[off[:-1]].copy()            # slot 0 holds the leader's own match
+        ts0 = last - np.uint64(64)
+    else:
+        m0, _, _, ts0 = oc.gen_fixed(TRACKER_SEED, n, Gs)
+        last = m0[0].copy()
+    batches = []
+    for k in range(R):
+        grp = rng.integers(0, Gs, size=Gs).astype(np.uint32)
+        if csr:
+            slot = (1 + (rng.integers(0, 1 << 30, size=Gs) % (sizes[grp] - 1))).astype(np.uint8)
+        else:
+            slot = rng.integers(1, n, size=Gs).astype(np.uint8)
+        lag = rng.integers(0, 96, size=Gs).astype(np.uint64)
+        idx = last[grp] + np.uint64((k + 1) * TRACKER_E) - lag
+        trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
+        batches.append((grp, slot, idx, trm))
+    m_start = m0.copy()
+    if csr:
+        m_start[off[:-1]] = last + np.uint64(R * TRACKER_E)
+    else:
+        m_start[0] = last + np.uint64(R * TRACKER_E)
+
+    def fresh():
+        st = {"match": m_start.copy(), "active": np.zeros(Gs, np.uint16),
+              "term": np.full(Gs, 7, np.uint64), "term_start": ts0.copy(),
+              "committed": np.zeros(Gs, np.uint64), "stepped_down": np.zeros(Gs, np.uint8)}
+        if csr:
+            oc.csr_commit_all(off, cfg, st["match"], ts0, st["committed"])
+        else:
+            oc.commit_all(n, st["match"], ts0, st["committed"])
+        return st
+
+    def rate(th):
+        busy, passes = 0.0, 0
+        while busy < seconds:
+            st = fresh()
+            t = time.perf_counter()
+            for b in batches:
+                if csr:
+                    oc.csr_appresp_sequential(off, cfg, b, st, threads=th)
+                else:
+                    oc.appresp_sequential(n, Gs, b, st, threads=th)
+            busy += time.perf_counter() - t
+            passes += 1
+        return passes * R * Gs / busy, passes
+
+    rn, pn = rate(threads)
+    r1, p1 = rate(1)
+    return {"value": rn, "unit": "group-steps/s", "cores": threads, "kind": "port",
+            "sample": (f"{Gs} {'ragged CSR' if csr else '5-voter'} groups x {R} consecutive "
+                       f"{Gs}-record batches of the same stream per pass, {pn} passes on {threads} "
+                       f"threads (groups partitioned; GOMAXPROCS-equivalent {threads}); "
+                       f"1 thread: {r1:.4g} group-steps/s over {p1} passes; sequential C "
+                       f"restatement of stepLeader's MsgAppResp path (oracle/quorum_oracle.c)"),
+            "value_1thread": r1}
+
+
+def tracker_main(args, world, rank, dev):
+    from etcd_amd.shard import route_records
+    csr = args.workload == "tracker-csr"
+    G = args.groups if args.groups != 1 << 20 else 1 << 24
+    K = args.steps if args.steps != 1000 else 20
+    W = args.warmup if args.warmup is not None else 4
+    nb = W + K
+    if nb > TRACKER_MAX_BATCHES:
+        raise SystemExit(f"--workload {args.workload} keeps one distinct batch per step resident: "
+                         f"--steps + --warmup must be <= {TRACKER_MAX_BATCHES}")
+    n = 5
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(TRACKER_SEED + 7919 * rank)
+    if csr:
+        grp = batch.CsrGroups.synth(0x5EED0003, "ragged", G, g_begin=rank * G, device=dev)
+        tr = batch.CsrTracker(grp.off, grp.cfg, max_slots=grp.max_slots, device=dev)
+        tr.match.copy_(grp.match[: tr.S])
+        first = grp.off[:-1].long()
+        last = tr.match[first].clone()        # slot 0: the leader's own match
+        tr.term_start.copy_(last - 64)
+        sizes = (grp.off[1:] - grp.off[:-1]).long()
+        del grp
+
+        def slots(group, g_):
+            s_g = sizes[group.long()]
+            r = torch.randint(0, 1 << 30, group.shape, generator=g_, device=dev)
+            return 1 + r % (s_g - 1)
+        slots_mean = float(sizes.float().mean())
+    else:
+        tr = batch.FixedTracker(n, G, dev)
+        fg = batch.FixedGroups.synth(TRACKER_SEED, n, G, g_begin=rank * G, device=dev,
+                                     with_term_start=True)
+        tr.match.copy_(fg.match)
+        tr.term_start.copy_(fg.term_start)
+        last = fg.match[0].clone()
+        del fg
+
+        def slots(group, g_):
+            return torch.randint(1, n, group.shape, generator=g_, device=dev)
+        slots_mean = float(n)
+    tr.term.fill_(7)
+    tr.commit_advance()
+    batches = tracker_batches(G, nb, last, slots, gen, dev)
+    if csr:
+        tr.match[first] = last + nb * TRACKER_E   # the leader appended nb*E entries
+    else:
+        tr.match[0].copy_(last + nb * TRACKER_E)
+    names = ("match", "committed", "active", "stepdown_at")
+    snap = {k: getattr(tr, k).clone() for k in names}
+
+    def restore():
+        for k in names:
+            getattr(tr, k).copy_(snap[k])
+
+    def step(b):
+        tr.step(b, reset_stats=False)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # pre-roll: whole passes over the batches, state restored before each
+    preroll_steps, tp = 0, time.perf_counter()
+    while time.perf_counter() - tp < max(0.0, args.preroll_ms) / 1e3:
+        restore()
+        for b in batches:
+            step(b)
+        preroll_steps += nb
+        torch.cuda.synchronize()
+    preroll_ms = (time.perf_counter() - tp) * 1e3
+    restore()
+    for k in range(W):
+        step(batches[k])
+    tr.stats.zero_()
+    st = torch.cuda.current_stream(dev)
+    ev = HipEvents(2)
+    barrier()
+    ev.record(ev.ev[0], st.cuda_stream)
+    t0 = time.perf_counter()
+    for k in range(W, nb):
+        step(batches[k])
+    ev.record(ev.ev[1], st.cuda_stream)
+    ev.synchronize(1)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = t1 - t0
+    step_s = ev.elapsed_ms(0, 1) / 1e3 / K
+    ev.close()
+    stats = tr.stats_dict()
+    route_ms = None
+    if world > 1:
+        t = torch.tensor([elapsed, step_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, step_s = (float(x) for x in t.tolist())
+        # records arriving at arbitrary ranks: deliver one batch (G records per
+        # rank, global group numbers over all shards) to the owning ranks
+        # (etcd_amd.shard.route_records: RCCL all-to-all), timed apart
+        b = batches[0]
+        gl = torch.randint(0, world * G, (G,), generator=gen, device=dev, dtype=torch.int64)
+        cols = {"group": gl.to(torch.int32), "flags": b.flags, "index": b.index, "term": b.term}
+        for _ in range(2):
+            route_records(cols, world * G)
+        barrier()
+        tr_ = time.perf_counter()
+        for _ in range(5):
+            route_records(cols, world * G)
+        barrier()
+        route_ms = (time.perf_counter() - tr_) / 5 * 1e3
+    if rank != 0:
+        return
+    bpg = TRACKER_BYTES if not csr else None
+    if csr:
+        # record 21 + match RMW 16 + commit advance: off 8, cfg 4, match 8 s,
+        # term_start 8, committed 8 read + committed 8 written
+        bpg = 21 + 16 + 8 + 4 + 8 * slots_mean + 8 + 8 + 8
+    key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
+    achieved = bpg * G / step_s / 1e9
+    kern = ("k_bk_hist, k_scan_local, k_bk_sums_parts, k_bk_scatter, k_bk_split, "
+            + ("k_csr_apply<16,false>, k_csr_slow" if csr else "k_bk_apply<5,false>, k_bk_slow<5>"))
+    out = {
+        "metric": METRIC + " — configs[4] streaming tracker: group-steps/s",
+        "value": world * G * K / elapsed,
+        "unit": "group-steps/s",
+        "n_gpus": world, "steps": K, "warmup": W, "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic streaming MsgAppResp batches (torch RNG on device, seeded per rank); "
+                "leader state from the counter-based splitmix64 spec; HBM-resident",
+        "config": {"workload": ("BASELINE configs[4]: streaming ProgressTracker, batched MsgAppResp "
+                                "scatter-max + commit advance, 16M groups per GPU (128M over 8)"
+                                + (" — ragged CSR groups (3-9 voters + 0-2 learners)" if csr
+                                   else ", 5 voters")),
+                   "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
+                   "stale_term_fraction": 0.01, "mean_slots": slots_mean,
+                   "parallelism": f"groups sharded by id over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key),
+                     "kernel": f"{'qb_dev_csr_tracker_step' if csr else 'qb_dev_fixed_tracker_step'}"
+                               f" (one step = {kern})",
+                     "bytes_per_group": bpg, "avg_kernel_us": step_s * 1e6,
+                     "timing": "HIP events around the K timed steps on the launch stream; "
+                               "per-step device time = region / K (every kernel of the step)"},
+        "preroll_ms": preroll_ms, "preroll_steps": preroll_steps,
+        "last_region_stats": {k: int(v) for k, v in stats.items()},
+        "route_ms": route_ms,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
+    print(json.dumps(out), flush=True)
+
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -160,14 +421,19 @@ def main():
                          "settle; 20 warm-up steps measured 2-3 %% slow)")
     ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
     ap.add_argument("--voters", type=int, default=5)
-    ap.add_argument("--workload", default="fixed", choices=["fixed", "ragged", "joint"],
-                    help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]")
+    ap.add_argument("--workload", default="fixed",
+                    choices=["fixed", "ragged", "joint", "tracker", "tracker-csr"],
+                    help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]; "
+                         "tracker = configs[4] (streaming MsgAppResp step, FIXED 5 voters); "
+                         "tracker-csr = the same stream over ragged CSR groups")
     ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--preroll-ms", type=float, default=300.0,
+                    help="untimed clock-settle pre-roll before the warm-up steps (wall ms)")
     ap.add_argument("--graph", type=int, default=0,
                     help="launch the steps from a captured HIP graph of this many steps "
                          "(0 = direct launches); the remainder of K is launched directly")
@@ -184,6 +450,11 @@ def main():
         else:  # rehearsal of the N > 1 path on fewer GPUs
             dist.init_process_group(args.backend)
 
+    if args.workload.startswith("tracker"):
+        tracker_main(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     csr = args.workload != "fixed"
     if args.warmup is None:
         args.warmup = 300 if csr else 2000
@@ -198,7 +469,6 @@ def main():
         B = min(B, 2)
     lib = _lib.load()
     main_stream = torch.cuda.current_stream(dev)
-    msp = main_stream.cuda_stream
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
     # B resident batches; global group numbers shard by rank (weak scaling)
@@ -225,16 +495,22 @@ def main():
                       for g, (c, v) in zip(groups, outs)] for st in streams]
     torch.cuda.synchronize()
 
-    def run_steps(count, fixed_batch=None):
-        for st in streams:
-            st.wait_stream(main_stream)
+    def run_steps(count, fixed_batch=None, fork=True):
+        # fork=False: the caller has synchronised the device, so the launch
+        # streams need no cross-stream wait on the main stream (each such hop
+        # costs device time: a fork + join around a 20-step region measured
+        # ~30 us, 10.1 vs 8.6 us per launch)
+        if fork:
+            for st in streams:
+                st.wait_stream(main_stream)
         for k in range(count):
             b = k % B if fixed_batch is None else fixed_batch
             rc = fn(*call_args[k % S][b])
             if rc:
                 _lib.check(rc, "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote")
-        for st in streams:
-            main_stream.wait_stream(st)
+        if fork:
+            for st in streams:
+                main_stream.wait_stream(st)
 
     graph = None
     if args.graph > 0:
@@ -256,9 +532,9 @@ def main():
         torch.cuda.synchronize()
         eager_steps = run_steps
 
-        def run_steps(count, fixed_batch=None):  # noqa: F811
+        def run_steps(count, fixed_batch=None, fork=True):  # noqa: F811
             if fixed_batch is not None:
-                return eager_steps(count, fixed_batch)
+                return eager_steps(count, fixed_batch, fork)
             for _ in range(count // L):
                 graph.replay()
             if count % L:
@@ -269,18 +545,48 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # Clock-settle pre-roll: untimed steps of the same workload until at least
+    # --preroll-ms of wall time has passed, whatever --warmup is (a 5-step
+    # warm-up leaves the clocks ramping: the round-1 driver line measured
+    # 9.85 us per launch against 8.6 us settled).  Then the W warm-up steps.
+    preroll_steps, tp = 0, time.perf_counter()
+    preroll_s = max(0.0, args.preroll_ms) / 1e3
+    while time.perf_counter() - tp < preroll_s:
+        run_steps(64)
+        preroll_steps += 64
+        torch.cuda.synchronize()
+    preroll_ms = (time.perf_counter() - tp) * 1e3
     run_steps(W)
-    ev = HipEvents(4)
+    # Timed region: K steps between barrier + synchronize.  Device time = from
+    # the earliest start event to the latest end event, one event pair per
+    # launch stream (no cross-stream hop inside the region: a fork + join
+    # around a 20-step region cost ~30 us of device time).  The start events
+    # are recorded after the barrier (device idle, so they stamp at once) and
+    # before t0; the wall clock stops when the host sees every stream's end
+    # event complete (hipEventSynchronize: all K steps are done), then the
+    # device-wide synchronize runs (tools/lab/sync_overhead.py: a
+    # torch.cuda.synchronize() costs ~20 us more than the event waits, a fixed
+    # cost that is 10 % of a 20-step region).
+    # (graph replays run on the main stream, forked inside the graph)
+    tstreams = [main_stream] if graph is not None else streams
+    TS = len(tstreams)
+    ev = HipEvents(2 * TS)
     barrier()
+    for s_, st in enumerate(tstreams):
+        ev.record(ev.ev[s_], st.cuda_stream)
     t0 = time.perf_counter()
-    ev.record(ev.ev[0], msp)
-    run_steps(K)
-    ev.record(ev.ev[1], msp)
-    torch.cuda.synchronize()
+    run_steps(K, fork=graph is not None)
+    for s_, st in enumerate(tstreams):
+        ev.record(ev.ev[TS + s_], st.cuda_stream)
+    for s_ in range(TS):
+        ev.synchronize(TS + s_)
     t1 = time.perf_counter()
+    torch.cuda.synchronize()
     barrier()
     elapsed = t1 - t0
-    avg_kernel_s = ev.elapsed_ms(0, 1) / 1e3 / K
+    starts = [0.0] + [ev.elapsed_ms(0, s_) for s_ in range(1, TS)]
+    ends = [ev.elapsed_ms(0, TS + s_) for s_ in range(TS)]
+    avg_kernel_s = (max(ends) - min(starts)) / 1e3 / K
 
     # MALL-warm single-batch rate (informational)
     run_steps(W, fixed_batch=0)
@@ -356,12 +662,16 @@ def main():
                 "kernel": kname,
                 "bytes_per_group": bpg,
                 "avg_kernel_us": avg_kernel_s * 1e6,
-                "timing": (f"HIP events around the timed region on the launch streams; per-launch "
-                           f"duration = region device time / K with {S} stream(s) overlapping "
-                           f"consecutive launches"
+                "timing": (f"HIP events at the start and end of the timed region on each of the "
+                           f"{S} launch stream(s); per-launch duration = (latest end - earliest "
+                           f"start) / K, consecutive launches overlapping across the streams; "
+                           f"wall clock from after the barrier to the host seeing every end "
+                           f"event complete"
                            + (f", launched from a HIP graph of {args.graph} steps"
                               if args.graph else "")),
             },
+            "preroll_ms": preroll_ms,
+            "preroll_steps": preroll_steps,
             "value_mall_warm": world * G * K / warm_elapsed,
             "allgather_ms": allgather_ms,
         }

@@ -26,7 +26,8 @@ QB_REC_REJECT = 0x80
 QB_STAT_NAMES = ("applied", "rejected", "stale_term", "non_member", "higher_term",
                  "bad_group", "after_stepdown")
 QB_STAT_COUNT = 8
-QB_VSTAT_NAMES = ("recorded", "duplicate", "stale_term", "higher_term", "after_stepdown", "bad")
+QB_VSTAT_NAMES = ("recorded", "duplicate", "stale_term", "higher_term", "after_stepdown", "bad",
+                  "after_decision")
 QB_VOTE_MODE_VOTE = 0
 QB_VOTE_MODE_PREVOTE = 1
 
@@ -51,6 +52,7 @@ SIGNATURES = {
     "qb_stream_create": (_i32, [C.POINTER(C.c_void_p)]),
     "qb_stream_destroy": (_i32, [_p]),
     "qb_stream_sync": (_i32, [_p]),
+    "qb_host_compile_configs": (_i32, [_u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _p]),
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_validate": (_i32, [_u64, _u32, _p, _p, _p]),
@@ -62,8 +64,10 @@ SIGNATURES = {
     "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
     "qb_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
     "qb_dev_fixed_tracker_step": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
+    "qb_csr_tracker_workspace_bytes": (C.c_size_t, [_u64, _u32, _u64]),
+    "qb_dev_csr_tracker_step": (_i32, [_u64, _u32, _p, _p, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_votes_workspace_bytes": (C.c_size_t, [_u64]),
-    "qb_dev_record_votes": (_i32, [_i32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
+    "qb_dev_record_votes": (_i32, [_i32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                    C.c_size_t, _p]),
     "qb_dev_csr_tally_votes": (_i32, [_u64, _p, _p, _p, _p, _p, _p]),
     "qb_leader_workspace_bytes": (C.c_size_t, [_u64, _u64]),
@@ -72,6 +76,12 @@ SIGNATURES = {
                                       _p, _p, _p, _p, _p]),
     "qb_conf_change_workspace_bytes": (C.c_size_t, [_u64]),
     "qb_dev_conf_change": (_i32, [_p, _p, _p, C.c_size_t, _p]),
+    "qb_shard_range": (_i32, [_u64, _i32, _i32, _p, _p]),
+    "qb_comm_get_unique_id": (_i32, [_p]),
+    "qb_comm_init": (_i32, [C.POINTER(C.c_void_p), _i32, _i32, _p]),
+    "qb_comm_destroy": (_i32, [_p]),
+    "qb_allgather_workspace_bytes": (C.c_size_t, [_u64, _i32]),
+    "qb_dev_allgather_results": (_i32, [_p, _u64, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
     "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
     "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),

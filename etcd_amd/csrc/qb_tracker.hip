@@ -250,13 +250,26 @@ extern "C" int qb_dev_fixed_apply_appresp(uint32_t n, uint64_t G, uint64_t M,
                                           uint64_t* next, uint16_t* active,
                                           uint32_t* stepdown_at, uint64_t* stats, void* stream) {
   QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
-  if (M == 0) return QB_OK;
+  if (M == 0 || G == 0) {
+    if (G && stepdown_at) {
+      const hipError_t e = hipMemsetAsync(stepdown_at, 0xFF, sizeof(uint32_t) * G, as_stream(stream));
+      if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(stepdown_at)");
+    }
+    return QB_OK;
+  }
   QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
   QB_REQUIRE(rec_group && rec_flags && rec_index && rec_term && group_term && match && active &&
                  stepdown_at && stats,
              "required pointer is NULL");
   QB_REQUIRE((reinterpret_cast<uintptr_t>(active) % 4) == 0, "active must be 4-byte aligned");
   hipStream_t st = as_stream(stream);
+  // stepdown_at is self-initialising (every group UINT32_MAX, then pass 1's
+  // atomic min), so a marker left from an earlier batch cannot shadow this
+  // one; G * 4 bytes, small beside the record passes' atomics.
+  {
+    const hipError_t e = hipMemsetAsync(stepdown_at, 0xFF, sizeof(uint32_t) * G, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(stepdown_at)");
+  }
   const dim3 grid(rec_grid(M));
   hipLaunchKernelGGL(k_appresp_stepdown, grid, dim3(kBlock), 0, st, n, G, M, rec_group, rec_flags,
                      reinterpret_cast<const u64*>(rec_term),

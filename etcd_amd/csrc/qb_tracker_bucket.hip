@@ -28,41 +28,10 @@
 //                    as LDS atomic or, then maybeCommit for the chunk's groups
 //                    and a coalesced write-back of match/next/active/committed.
 #include "qb_bucket.h"
+#include "qb_tracker_slow.h"
 
 namespace qb {
 namespace bk {
-
-// Counters of block b go to shard b % kShards (QB_STAT_COUNT u64 each, one
-// cache line), folded into the caller's stats by k_stats_fold.
-__device__ __forceinline__ u64* shard_of(u64* shards) {
-  return shards + u64(blockIdx.x % kShards) * QB_STAT_COUNT;
-}
-
-// One thread per shard (its 64-byte line in one go), wave sums by shuffles:
-// a thread per counter walking the 256 shards serially took 7 us.  Run by
-// one block of kShards threads (block 0 of k_bk_finish).
-static_assert(kShards == kBlock, "the fold runs in one kBlock-thread block");
-__device__ __forceinline__ void stats_fold_block(const u64* __restrict__ shards,
-                                                 u64* __restrict__ stats) {
-  __shared__ u64 part[kShards / 64][QB_STAT_COUNT];
-  const int i = threadIdx.x, lane = i & 63, w = i >> 6;
-  u64 x[QB_STAT_COUNT];
-#pragma unroll
-  for (int k = 0; k < QB_STAT_COUNT; ++k) x[k] = shards[i * QB_STAT_COUNT + k];
-#pragma unroll
-  for (int k = 0; k < QB_STAT_COUNT; ++k) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x[k] += __shfl_xor(x[k], o, 64);
-    if (lane == 0) part[w][k] = x[k];
-  }
-  __syncthreads();
-  if (i < QB_STAT_COUNT) {
-    u64 s = 0;
-#pragma unroll
-    for (int q = 0; q < kShards / 64; ++q) s += part[q][i];
-    stats[i] += s;
-  }
-}
 
 // ---------------------------------------------------------------- K1 ----
 // Invalid records (group >= G, slot >= n) are counted per tile into inval[2
@@ -527,7 +496,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 // a higher-term record (the sequential leader steps down there and ignores
 // what follows, raft.go:875-879: batch order matters) or with a term32 escape
 // against a group term >= 2^32 - 1 (ambiguous compare) is "slow": K5 leaves
-// its state untouched, flags it, and k_bk_slow_* apply it from the original
+// its state untouched, flags it, and k_bk_slow applies it from the original
 // batch in batch order (the exact two-pass form of qb_tracker.hip).
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
 // act[CH] u32.
@@ -630,7 +599,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     }
   }
   __syncthreads();
-  if (slow) {  // block-uniform: state left for k_bk_slow_*, counts discarded
+  if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
 #pragma unroll
     for (u32 k = 0; k < GPT; ++k) {
       const u32 lg = threadIdx.x + k * kBlock;
@@ -666,120 +635,10 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     const bool adv = ci > cm[k] && ci >= ts[k];  // log.go:328-334
     if (adv) committed[g] = ci;
     if (advanced) advanced[g] = adv ? 1 : 0;
-    stepdown_at[g] = 0xFFFFFFFFu;
     if (act[lg]) active[g] = u16(active[g] | act[lg]);
   }
   const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
   tally.flush(tl, shard_of(shards), slot);
-}
-
-// ------------------------------------------------------ slow chunks ----
-// The flagged chunks' records, from the original batch in batch order,
-// exactly as qb_tracker.hip's two passes (k_appresp_stepdown/apply) and
-// k_commit_advance restricted to those chunks.  Every launch returns at once
-// when no chunk was flagged (*any_slow == 0, a uniform scalar load).
-constexpr unsigned kSlowBlocks = 2048;
-inline unsigned slow_grid(u64 units) {
-  const u64 g = (units + kBlock - 1) / kBlock;
-  return unsigned(g < 1 ? 1 : g < kSlowBlocks ? g : kSlowBlocks);
-}
-
-__device__ __forceinline__ bool in_slow_chunk(const Geometry& geo, u32 g, u32 f,
-                                              const u8* __restrict__ chunk_slow) {
-  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[g / geo.CH];
-}
-
-__global__ __launch_bounds__(kBlock) void k_bk_slow_stepdown(
-    Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
-    const u64* __restrict__ rt, const u64* __restrict__ group_term,
-    const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
-    u32* __restrict__ stepdown_at, u64* __restrict__ shards) {
-  if (*any_slow == 0) return;
-  __shared__ u32 tl[1];
-  BlockTally<1> tally;
-  const u64 stride = u64(gridDim.x) * kBlock;
-  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < geo.M; i += stride) {
-    const u32 g = rg[i];
-    bool higher = false;
-    if (in_slow_chunk(geo, g, rf[i], chunk_slow) && rt[i] > group_term[g]) {
-      atomicMin(stepdown_at + g, u32(i));  // raft.go:875-879: first one in batch order
-      higher = true;
-    }
-    tally.add(0, higher);
-  }
-  const int slot[1] = {QB_STAT_HIGHER_TERM};
-  tally.flush(tl, shard_of(shards), slot);
-}
-
-__global__ __launch_bounds__(kBlock) void k_bk_slow_apply(
-    Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
-    const u64* __restrict__ ri, const u64* __restrict__ rt, const u64* __restrict__ group_term,
-    const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
-    const u32* __restrict__ stepdown_at, u64* __restrict__ match, u64* __restrict__ next,
-    u16* __restrict__ active, u64* __restrict__ shards) {
-  if (*any_slow == 0) return;
-  __shared__ u32 tl[4];
-  BlockTally<4> tally;
-  const u64 stride = u64(gridDim.x) * kBlock;
-  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < geo.M; i += stride) {
-    const u32 g = rg[i], f = rf[i];
-    bool stale = false, applied = false, rejected = false, after = false;
-    if (in_slow_chunk(geo, g, f, chunk_slow)) {
-      const u64 t = rt[i], gt = group_term[g];
-      stale = t < gt;
-      if (t == gt) {
-        if (stepdown_at[g] < u32(i)) {
-          after = true;  // the leader stepped down at an earlier record
-        } else {
-          const u32 s = f & 0x0Fu;
-          // RecentActive (raft.go:1107) as an atomic or on the aligned word
-          // holding active[g] (no 4-byte alignment asked of the caller)
-          const uintptr_t a = reinterpret_cast<uintptr_t>(active + g);
-          atomicOr(reinterpret_cast<u32*>(a & ~uintptr_t(3)), (1u << s) << ((a & 2u) * 8u));
-          if (f & QB_REC_REJECT) {
-            rejected = true;
-          } else {
-            applied = true;
-            const u64 idx = ri[i];
-            atomicMax(match + u64(s) * geo.G + g, idx);                  // progress.go:146-150
-            if (next) atomicMax(next + u64(s) * geo.G + g, idx + 1ull);  // progress.go:151
-          }
-        }
-      }
-    }
-    tally.add(0, stale);
-    tally.add(1, applied);
-    tally.add(2, rejected);
-    tally.add(3, after);
-  }
-  const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED,
-                       QB_STAT_AFTER_STEPDOWN};
-  tally.flush(tl, shard_of(shards), slot);
-}
-
-// Last kernel of the step: block 0 folds the stat shards into the caller's
-// stats (every counting kernel has finished), then maybeCommit for the
-// groups of flagged chunks.
-template <int N>
-__global__ __launch_bounds__(kBlock) void k_bk_finish(
-    Geometry geo, const u8* __restrict__ chunk_slow, const u32* __restrict__ any_slow,
-    const u64* __restrict__ match, const u64* __restrict__ term_start,
-    u64* __restrict__ committed, u8* __restrict__ advanced, const u64* __restrict__ shards,
-    u64* __restrict__ stats) {
-  if (blockIdx.x == 0) stats_fold_block(shards, stats);
-  if (*any_slow == 0) return;
-  const u64 stride = u64(gridDim.x) * kBlock;
-  for (u64 g = u64(blockIdx.x) * kBlock + threadIdx.x; g < geo.G; g += stride) {
-    if (!chunk_slow[g / geo.CH]) continue;
-    u64 v[N];
-#pragma unroll
-    for (int s = 0; s < N; ++s) v[s] = match[u64(s) * geo.G + g];
-    const u64 ci = select_quorum<N>(v);
-    const u64 cm = committed[g];
-    const bool adv = ci > cm && ci >= term_start[g];  // log.go:328-334
-    if (adv) committed[g] = ci;
-    if (advanced) advanced[g] = adv ? 1 : 0;
-  }
 }
 
 struct ApplyArgs {
@@ -807,10 +666,15 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                        a.chunk_slow, a.any_slow, a.stats);
 }
 
+
+
 template <int N>
-void launch_finish(const Geometry& geo, const ApplyArgs& a, u64* stats, hipStream_t st) {
-  hipLaunchKernelGGL((k_bk_finish<N>), dim3(slow_grid(geo.G)), dim3(kBlock), 0, st, geo,
-                     a.chunk_slow, a.any_slow, a.match, a.ts, a.committed, a.adv, a.stats, stats);
+void launch_slow(const Geometry& geo, const ApplyArgs& a, const SlowArgs& s, u64* stats,
+                 hipStream_t st) {
+  hipLaunchKernelGGL((k_bk_slow<FixedLay<N>>), dim3(s.grid), dim3(kBlock), 0, st, geo,
+                     FixedLay<N>{geo.G}, s.rg, s.rf, s.ri,
+                     s.rt, a.gt, a.ts, a.chunk_slow, a.any_slow, s.bar, a.stepdown, a.match, a.next,
+                     a.active, a.committed, a.adv, a.stats, stats);
 }
 
 template <int... Ns>
@@ -820,10 +684,12 @@ void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& ge
 }
 
 template <int... Ns>
-void dispatch_finish(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
-                     const ApplyArgs& a, u64* stats, hipStream_t st) {
-  ((n == Ns + 1 ? launch_finish<Ns + 1>(geo, a, stats, st) : void()), ...);
+void dispatch_slow(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
+                   const ApplyArgs& a, const SlowArgs& s, u64* stats, hipStream_t st) {
+  ((n == Ns + 1 ? launch_slow<Ns + 1>(geo, a, s, stats, st) : void()), ...);
 }
+
+
 
 }  // namespace bk
 }  // namespace qb
@@ -935,17 +801,11 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs, a,
                      st);
   QB_CHECK_LAUNCH("k_bk_apply");
-  if (M > 0) {  // chunks flagged slow by K5 (none in the steady state: each launch returns at once)
-    const dim3 rgrid(bk::slow_grid(M));
-    hipLaunchKernelGGL(bk::k_bk_slow_stepdown, rgrid, dim3(kBlock), 0, st, geo, rg, rec_flags, rtm,
-                       a.gt, a.chunk_slow, a.any_slow, stepdown_at, shards);
-    hipLaunchKernelGGL(bk::k_bk_slow_apply, rgrid, dim3(kBlock), 0, st, geo, rg, rec_flags, ri, rtm,
-                       a.gt, a.chunk_slow, a.any_slow, stepdown_at, a.match, a.next, active,
-                       shards);
-    QB_CHECK_LAUNCH("k_bk_slow");
-  }
-  // stat fold + maybeCommit of flagged chunks
-  bk::dispatch_finish(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, stt, st);
-  QB_CHECK_LAUNCH("k_bk_finish");
+  // chunks flagged slow by K5 (none in the steady state: the launch folds
+  // the stat shards and returns) + the stat fold
+  const bk::SlowArgs sa{rg, rec_flags, ri, rtm, reinterpret_cast<u32*>(ws + cv.flags) + 16,
+                        bk::slow_blocks()};
+  bk::dispatch_slow(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, sa, stt, st);
+  QB_CHECK_LAUNCH("k_bk_slow");
   return QB_OK;
 }

@@ -1,0 +1,312 @@
+// qb_tracker_csr.hip — one leader tick over G groups of the CSR layout
+// (ragged voter counts, learners, joint configs): a batch of MsgAppResp
+// records applied and the commit advanced, records bucketed by group on the
+// device so every MaybeUpdate is an LDS atomic.
+//
+// Reference semantics (paths relative to the reference's raft/):
+//   node.run / RawNode.Step: responses from a non-member are dropped first
+//                                        node.go:356-360, rawnode.go:110-119
+//   raft.Step term filter                raft.go:847-921
+//   stepLeader MsgAppResp (quorum part)  raft.go:1100-1109, 1237-1259
+//   Progress.MaybeUpdate                 tracker/progress.go:144-153
+//   ProgressTracker.Committed            tracker/tracker.go:162-179 ->
+//     JointConfig.CommittedIndex         quorum/joint.go:49-56 (learners have
+//                                        a Progress and ack, but never count)
+//   raft.maybeCommit (also on a joint transition, raft.go:1682)
+//                                        raft.go:585-588, log.go:328-334
+//
+// Pipeline: K1-K4 are the FIXED step's bucketing (qb_bucket.h, records cut
+// into chunks of CH consecutive groups, one run per part of the chunk's
+// super-bucket).  K5 = k_csr_apply: one workgroup per chunk.  The chunk's
+// groups own one contiguous slot run match[off[g0] .. off[g0 + CH]), at most
+// CH * WMAX slots; an LDS accumulator per slot of the run takes the records'
+// MaybeUpdate (ds_max_u64), the old run is streamed into registers meanwhile,
+// then one coalesced pass writes the raised slots and leaves max(old, acc) in
+// LDS, and each thread evaluates its group's JointConfig.CommittedIndex from
+// LDS (compacted half sorts, qb_csr.h) and the maybeCommit gate.  Chunks with
+// a higher-term record (batch order matters) go to the slow path
+// (qb_tracker_slow.h) exactly as in the FIXED step.
+#include "qb_tracker_slow.h"
+
+namespace qb {
+namespace bk {
+
+template <int WMAX, bool NEXT>
+__global__ __launch_bounds__(kBlock) void k_csr_apply(
+    Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
+    const u32* __restrict__ off, const u32* __restrict__ cfg, const u64* __restrict__ group_term,
+    const u64* __restrict__ term_start, u64* __restrict__ match, u64* __restrict__ next,
+    u16* __restrict__ active, u64* __restrict__ committed, u32* __restrict__ stepdown_at,
+    u8* __restrict__ advanced, u8* __restrict__ chunk_slow, u32* __restrict__ any_slow,
+    u64* __restrict__ shards) {
+  constexpr u32 CH = chunk_groups(WMAX);
+  constexpr u32 GPT = CH / kBlock;     // groups per thread in the commit phase
+  constexpr u32 CAP = CH * WMAX;       // slot-run capacity
+  constexpr u32 PER = CAP / kBlock;    // run slots per thread
+  __shared__ u64 acc[CAP];
+  __shared__ u64 accn[NEXT ? CAP : 1];
+  __shared__ u32 offs[CH + 1];
+  __shared__ u64 gterm[CH];
+  __shared__ u32 act[CH];
+  __shared__ u32 slow;
+  __shared__ u32 tl[4];
+  __shared__ RunTable rtab;
+  BlockTally<4> tally;  // stale, applied, rejected, non-member
+  const u32 c = blockIdx.x;
+  const u64 g0 = u64(c) * CH;
+  const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
+  // commit-phase inputs of this thread's groups, issued first
+  u64 cm[GPT], ts[GPT];
+  u32 cf[GPT];
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * kBlock;
+    const bool live = lg < ng;
+    cm[k] = live ? committed[g0 + lg] : 0ull;
+    ts[k] = live ? term_start[g0 + lg] : 0ull;
+    cf[k] = live ? cfg[g0 + lg] : 0u;
+  }
+  for (u32 k = threadIdx.x; k <= CH; k += kBlock) offs[k] = off[g0 + (k < ng ? k : ng)];
+  for (u32 k = threadIdx.x; k < CH; k += kBlock) {
+    gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
+    act[k] = 0;
+  }
+  if (threadIdx.x == 0) slow = 0;
+  __syncthreads();
+  const u32 a0 = offs[0], run = offs[CH] - a0;
+  // A table breaking its max_slots bound cannot stage its run in LDS: the
+  // chunk takes the slow path (exact per-record semantics, global atomics).
+  const bool fits = run <= CAP;
+  u64 old[PER];
+#pragma unroll
+  for (u32 p = 0; p < PER; ++p) {
+    const u32 j = threadIdx.x + p * kBlock;
+    old[p] = (fits && j < run) ? match[a0 + j] : 0ull;
+  }
+  for (u32 k = threadIdx.x; k < CAP; k += kBlock) {
+    acc[k] = 0;
+    if constexpr (NEXT) accn[k] = 0;
+  }
+  if (!fits && threadIdx.x == 0) slow = 1;
+  // the chunk's records: one short run per part of its super-bucket
+  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
+  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  constexpr int kRecPer = 4;
+  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
+    const u32 total = rtab.build(cs, pb, p1, cl);  // synchronises (acc zeroed, offs ready)
+    for (u32 f0 = 0; f0 < total; f0 += kBlock * kRecPer) {
+      u64 rmr[kRecPer], rix[kRecPer];
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) {
+        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        rmr[r] = 0;
+        rix[r] = 0;
+        if (f < total) {
+          const u32 i = rtab.locate(f);
+          rmr[r] = recs.mr[i];
+          rix[r] = recs.index[i];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) {
+        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        bool stale = false, applied = false, rejected = false, non = false;
+        if (f < total && fits) {
+          const u64 mr = rmr[r];
+          const u32 t32 = u32(mr >> 32), meta = u32(mr);
+          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+          const u32 base = offs[lg] - a0, sg = offs[lg + 1] - offs[lg];
+          const u64 gt = gterm[lg];
+          if (s >= sg) {
+            non = true;                                     // no Progress: raft.go:1100-1104
+          } else if (t32 == kTermEscape || u64(t32) > gt) {
+            slow = 1;  // higher term (step-down order) or ambiguous compare
+          } else if (u64(t32) < gt) {
+            stale = true;                                   // raft.go:883-921
+          } else {
+            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+            if (meta & (1u << 24)) {  // QB_REC_REJECT
+              rejected = true;                              // raft.go:1109: not MaybeUpdate
+            } else {
+              applied = true;
+              const u64 idx = rix[r];
+              atomicMax(&acc[base + s], idx);               // progress.go:146-150
+              if constexpr (NEXT) atomicMax(&accn[base + s], idx + 1ull);  // :151
+            }
+          }
+        }
+        tally.add(0, stale);
+        tally.add(1, applied);
+        tally.add(2, rejected);
+        tally.add(3, non);
+      }
+    }
+  }
+  __syncthreads();
+  if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
+    for (u32 lg = threadIdx.x; lg < ng; lg += kBlock) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) {
+      chunk_slow[c] = 1;
+      atomicOr(any_slow, 1u);
+    }
+    return;
+  }
+  if (threadIdx.x == 0) chunk_slow[c] = 0;
+  // MaybeUpdate write-back over the run (coalesced), leaving max(old, acc)
+  // in LDS for the CommittedIndex of every group
+#pragma unroll
+  for (u32 p = 0; p < PER; ++p) {
+    const u32 j = threadIdx.x + p * kBlock;
+    if (j < run) {
+      const u64 a = acc[j];
+      if (a > old[p]) {
+        match[a0 + j] = a;
+        old[p] = a;
+      }
+      acc[j] = old[p];
+      if constexpr (NEXT) {
+        const u64 nn = accn[j];
+        if (nn) {
+          u64* q = next + a0 + j;
+          if (nn > *q) *q = nn;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // maybeCommit per group (every lane takes part: csr_ci's width is
+  // wave-uniform)
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * kBlock;
+    const bool live = lg < ng;
+    const u32 base = live ? offs[lg] - a0 : 0u;
+    u32 sg = live ? offs[lg + 1] - offs[lg] : 0u;
+    sg = sg > u32(WMAX) ? u32(WMAX) : sg;
+    const u64 ci = csr_ci<WMAX>(acc + base, sg, cf[k] & 0xFFFFu, cf[k] >> 16);
+    if (!live) continue;
+    const u64 g = g0 + lg;
+    // log.go:328-334; an empty config's ci = MaxUint64 is past lastIndex,
+    // whose term is 0 (log.go:271-273): never committed
+    const bool adv = ci != kInf && ci > cm[k] && ci >= ts[k];
+    if (adv) committed[g] = ci;
+    if (advanced) advanced[g] = adv ? 1 : 0;
+    if (act[lg]) active[g] = u16(active[g] | act[lg]);
+  }
+  const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
+  tally.flush(tl, shard_of(shards), slot);
+}
+
+struct CsrStepArgs {
+  const u32 *off, *cfg;
+  const u64 *gt, *ts;
+  u64 *match, *next;
+  u16* active;
+  u64* committed;
+  u32* stepdown;
+  u8* adv;
+  u8* chunk_slow;
+  u32* any_slow;
+  u64* shards;
+};
+
+template <int WMAX>
+void launch_csr_step(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+                     const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
+  if (a.next)
+    hipLaunchKernelGGL((k_csr_apply<WMAX, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
+                       cs, a.off, a.cfg, a.gt, a.ts, a.match, a.next, a.active, a.committed,
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.shards);
+  else
+    hipLaunchKernelGGL((k_csr_apply<WMAX, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs,
+                       pt, cs, a.off, a.cfg, a.gt, a.ts, a.match, a.next, a.active, a.committed,
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.shards);
+  hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
+                     CsrLay<WMAX>{a.off, a.cfg}, sa.rg, sa.rf, sa.ri, sa.rt, a.gt, a.ts,
+                     a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,
+                     a.committed, a.adv, a.shards, stats);
+}
+
+}  // namespace bk
+}  // namespace qb
+
+using namespace qb;
+
+namespace {
+u32 csr_wmax(uint32_t max_slots) {
+  const u32 w = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
+  return w <= 4 ? 4u : w <= 8 ? 8u : w <= 12 ? 12u : 16u;
+}
+}  // namespace
+
+extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
+  if (max_slots > QB_MAX_SLOTS) return 0;
+  return bk::carve(bk::geometry(csr_wmax(max_slots), G, M), 2).total;
+}
+
+extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                                       const uint32_t* cfg, uint64_t M, const uint32_t* rec_group,
+                                       const uint8_t* rec_flags, const uint64_t* rec_index,
+                                       const uint64_t* rec_term, const uint64_t* group_term,
+                                       const uint64_t* term_start, uint64_t* match,
+                                       uint64_t* next, uint16_t* active, uint64_t* committed,
+                                       uint32_t* stepdown_at, uint8_t* advanced_out,
+                                       uint64_t* stats, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+  QB_REQUIRE(max_slots <= QB_MAX_SLOTS, "max_slots must be 0..%d", QB_MAX_SLOTS);
+  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
+  QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(off && cfg && group_term && term_start && match && active && committed &&
+                 stepdown_at && stats,
+             "required state pointer is NULL");
+  QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
+             "record pointer is NULL");
+  const u32 wmax = csr_wmax(max_slots);
+  // the bucketing filters slot >= the table bound (geo.n) as non-member; the
+  // chunk size follows the LDS run capacity (chunk_groups(wmax))
+  bk::Geometry geo = bk::geometry(wmax, G, M);
+  geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
+  const bk::Carve cv = bk::carve(geo, 2);
+  QB_REQUIRE(workspace && workspace_bytes >= cv.total,
+             "workspace too small: need %zu bytes (qb_csr_tracker_workspace_bytes)", cv.total);
+  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
+             (unsigned long long)G);
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
+  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
+  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M, 2);
+  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
+  const auto* ri = reinterpret_cast<const u64*>(rec_index);
+  const auto* rtm = reinterpret_cast<const u64*>(rec_term);
+  {
+    const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags, ri, rtm, shards, st,
+                                      /*term32=*/false, /*packed=*/true);
+    if (rc != QB_OK) return rc;
+  }
+  const bk::CsrStepArgs a{off,
+                          cfg,
+                          reinterpret_cast<const u64*>(group_term),
+                          reinterpret_cast<const u64*>(term_start),
+                          reinterpret_cast<u64*>(match),
+                          reinterpret_cast<u64*>(next),
+                          active,
+                          reinterpret_cast<u64*>(committed),
+                          stepdown_at,
+                          advanced_out,
+                          reinterpret_cast<u8*>(ws + cv.chunk_flags),
+                          reinterpret_cast<u32*>(ws + cv.flags),
+                          shards};
+  const bk::SlowArgs sa{rec_group, rec_flags, ri, rtm, reinterpret_cast<u32*>(ws + cv.flags) + 16,
+                        bk::slow_blocks()};
+  u64* stt = reinterpret_cast<u64*>(stats);
+  switch (wmax) {
+    case 4: bk::launch_csr_step<4>(geo, buf2, pt, cs, a, sa, stt, st); break;
+    case 8: bk::launch_csr_step<8>(geo, buf2, pt, cs, a, sa, stt, st); break;
+    case 12: bk::launch_csr_step<12>(geo, buf2, pt, cs, a, sa, stt, st); break;
+    default: bk::launch_csr_step<16>(geo, buf2, pt, cs, a, sa, stt, st); break;
+  }
+  QB_CHECK_LAUNCH("k_csr_apply / k_bk_slow");
+  return QB_OK;
+}

@@ -131,33 +131,58 @@ class CompiledConfigs:
         return self.slot_ids[self.off[g]:self.off[g + 1]]
 
 
+def _id_csr(lists, G):
+    """Per-group ID iterables -> (off uint32 [G+1], ids uint64)."""
+    off = np.zeros(G + 1, dtype=np.uint32)
+    flat = []
+    for g, ids in enumerate(lists):
+        ids = list(ids)
+        off[g + 1] = off[g] + len(ids)
+        flat.extend(ids)
+    return off, np.asarray(flat if flat else [0], dtype=np.uint64)
+
+
 def compile_configs(voters_in: Sequence[Iterable[int]], voters_out: Sequence[Iterable[int]] = None,
                     learners: Sequence[Iterable[int]] = None) -> CompiledConfigs:
-    """tracker.Config (tracker.go:27-78) per group -> CSR slots and masks.
+    """tracker.Config (tracker.go:27-78) per group -> CSR slots and masks, by
+    the C ABI's qb_host_compile_configs (the call a cgo embedder makes).
 
-    Learners must not intersect the voters (tracker.go:40-46; enforced by
-    confchange, confchange.go:307-318) — a violation raises ValueError."""
+    Learners must not intersect the voters (confchange.go:307-318) and a group
+    holds at most QB_MAX_SLOTS members — a violation raises ValueError with
+    the reference's message."""
     G = len(voters_in)
     voters_out = voters_out if voters_out is not None else [()] * G
     learners = learners if learners is not None else [()] * G
     if len(voters_out) != G or len(learners) != G:
         raise ValueError("voters_in, voters_out and learners must have one entry per group")
+    return compile_configs_csr(*_id_csr(voters_in, G), *_id_csr(voters_out, G),
+                               *_id_csr(learners, G))
+
+
+def compile_configs_csr(in_off, in_ids, out_off=None, out_ids=None, lrn_off=None,
+                        lrn_ids=None) -> CompiledConfigs:
+    """qb_host_compile_configs over ID lists already in CSR form (numpy:
+    uint32 offsets [G+1], uint64 IDs)."""
+    in_off = np.ascontiguousarray(in_off, np.uint32)
+    G = len(in_off) - 1
+    arrs = [in_off, np.ascontiguousarray(in_ids, np.uint64)]
+    for o, i in ((out_off, out_ids), (lrn_off, lrn_ids)):
+        arrs += [None, None] if o is None else [np.ascontiguousarray(o, np.uint32),
+                                                np.ascontiguousarray(i, np.uint64)]
+    ptrs = [None if a is None else a.ctypes.data for a in arrs]
     off = np.zeros(G + 1, dtype=np.uint32)
-    cfg = np.zeros(G, dtype=np.uint32)
-    ids = []
-    for g in range(G):
-        vi, vo, lr = set(voters_in[g]), set(voters_out[g]), set(learners[g])
-        if lr & (vi | vo):
-            raise ValueError(f"group {g}: learners {sorted(lr & (vi | vo))} are also voters")
-        slot = sorted(vi | vo | lr)
-        if len(slot) > _lib.QB_MAX_SLOTS:
-            raise ValueError(f"group {g}: {len(slot)} slots > {_lib.QB_MAX_SLOTS}")
-        m_in = sum(1 << j for j, i in enumerate(slot) if i in vi)
-        m_out = sum(1 << j for j, i in enumerate(slot) if i in vo)
-        cfg[g] = m_in | (m_out << 16)
-        off[g + 1] = off[g] + len(slot)
-        ids.extend(slot)
-    return CompiledConfigs(off, cfg, np.asarray(ids, dtype=np.uint64))
+    cfg = np.zeros(max(G, 1), dtype=np.uint32)
+    bad = np.zeros(1, dtype=np.uint64)
+    lib = _lib.load()
+    rc = lib.qb_host_compile_configs(G, *ptrs, off.ctypes.data, cfg.ctypes.data, None, 0,
+                                     bad.ctypes.data)
+    if rc == _lib.QB_EINVAL:
+        raise ValueError(lib.qb_last_error().decode(errors="replace"))
+    _lib.check(rc, "qb_host_compile_configs")
+    ids = np.zeros(max(int(off[G]), 1), dtype=np.uint64)
+    _lib.call("qb_host_compile_configs", G, *ptrs, off.ctypes.data, cfg.ctypes.data,
+              ids.ctypes.data, ids.size, None)
+    return CompiledConfigs(off, cfg[:G], ids[: int(off[G])])
 
 
 @dataclass
@@ -331,21 +356,26 @@ class CsrGroups:
 
     def record_votes(self, batch: "AppRespBatch", group_term: torch.Tensor, prevote: bool = False,
                      stepdown_at: Optional[torch.Tensor] = None,
+                     decided_at: Optional[torch.Tensor] = None,
                      stats: Optional[torch.Tensor] = None):
         """RecordVote for a batch of MsgVoteResp (or MsgPreVoteResp) records,
-        first vote wins in batch order (tracker.go:258-263, raft.go:847-921).
-        Returns (stepdown_at, stats)."""
+        first vote wins in batch order, polling stops at the group's VoteWon /
+        VoteLost (tracker.go:258-288, raft.go:847-921, 1391-1414).
+        Returns (stepdown_at, decided_at, stats)."""
         if stepdown_at is None:
-            stepdown_at = torch.full((self.G,), -1, dtype=torch.int32, device=self.device)
+            stepdown_at = torch.empty(self.G, dtype=torch.int32, device=self.device)
+        if decided_at is None:
+            decided_at = torch.empty(self.G, dtype=torch.int32, device=self.device)
         if stats is None:
             stats = torch.zeros(8, dtype=torch.int64, device=self.device)
         need = _lib.load().qb_votes_workspace_bytes(batch.M)
         ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         _lib.call("qb_dev_record_votes", _lib.QB_VOTE_MODE_PREVOTE if prevote else
                   _lib.QB_VOTE_MODE_VOTE, self.G, batch.M, _ptr(batch.group), _ptr(batch.flags),
-                  _ptr(batch.term), _ptr(group_term), _ptr(self.votes), _ptr(stepdown_at),
-                  _ptr(stats), _ptr(ws), ws.numel(), _stream(self.device))
-        return stepdown_at, stats
+                  _ptr(batch.term), _ptr(group_term), _ptr(self.cfg), _ptr(self.votes),
+                  _ptr(stepdown_at), _ptr(decided_at), _ptr(stats), _ptr(ws), ws.numel(),
+                  _stream(self.device))
+        return stepdown_at, decided_at, stats
 
     def validate(self, max_slots: Optional[int] = None) -> int:
         """Number of groups breaking the CSR invariants (off[0] == 0,
@@ -427,6 +457,74 @@ class FixedTracker:
                   _ptr(self.term_start), _ptr(self.match), _ptr(self.next), _ptr(self.active),
                   _ptr(self.committed), _ptr(self.stepdown_at), _ptr(advanced_out),
                   _ptr(self.stats), _ptr(self._ws), self._ws.numel(), _stream(self.device))
+        return advanced_out
+
+    def stats_dict(self) -> dict:
+        v = self.stats.cpu().tolist()
+        return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}
+
+    def stepped_down(self) -> torch.Tensor:
+        return self.stepdown_at != -1
+
+
+class CsrTracker:
+    """Leader-side ProgressTracker state of G groups of the CSR layout (ragged
+    voter counts, learners, joint configs): Progress.Match per slot, the
+    leader's term, the first index of its term, the commit index and the
+    RecentActive bits per group.  ``step`` = qb_dev_csr_tracker_step: a
+    MsgAppResp batch applied and maybeCommit with the JointConfig
+    CommittedIndex (tracker.go:162-179, joint.go:49-56, raft.go:585-588)."""
+
+    def __init__(self, off: torch.Tensor, cfg: torch.Tensor, max_slots: Optional[int] = None,
+                 device="cuda", track_next: bool = False):
+        _require_device(off, "off")
+        _require_device(cfg, "cfg")
+        self.off, self.cfg = off, cfg
+        self.device = torch.device(device)
+        self.G = cfg.numel()
+        self.S = int(off[-1].item()) if self.G else 0
+        if max_slots is None:
+            max_slots = int((off[1:].long() - off[:-1].long()).max().item()) if self.G else 0
+        self.max_slots = max(1, min(int(max_slots), _lib.QB_MAX_SLOTS))
+        dev, G, S = self.device, self.G, max(self.S, 2)
+        self.match = torch.zeros(S, dtype=torch.int64, device=dev)
+        self.next = torch.ones(S, dtype=torch.int64, device=dev) if track_next else None
+        self.active = torch.zeros(G + (G & 1), dtype=torch.int16, device=dev)
+        self.term = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.term_start = torch.full((G,), -1, dtype=torch.int64, device=dev)  # ∞
+        self.committed = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.stepdown_at = torch.full((G,), -1, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(_lib.QB_STAT_COUNT, dtype=torch.int64, device=dev)
+        self._ws = None
+
+    def committed_index(self) -> torch.Tensor:
+        """ProgressTracker.Committed per group (JointConfig.CommittedIndex)."""
+        c = torch.empty(self.G, dtype=torch.int64, device=self.device)
+        _lib.call("qb_dev_csr_committed_vote", self.G, self.max_slots, _ptr(self.off),
+                  _ptr(self.match), _ptr(self.cfg), None, _ptr(c), None, _stream(self.device))
+        return c
+
+    def commit_advance(self, advanced_out: Optional[torch.Tensor] = None):
+        """maybeCommit for every group: the step with an empty batch."""
+        empty = AppRespBatch(torch.zeros(1, dtype=torch.int32, device=self.device)[:0],
+                             torch.zeros(1, dtype=torch.uint8, device=self.device)[:0],
+                             torch.zeros(1, dtype=torch.int64, device=self.device)[:0],
+                             torch.zeros(1, dtype=torch.int64, device=self.device)[:0])
+        return self.step(empty, advanced_out, reset_stats=False)
+
+    def step(self, batch: AppRespBatch, advanced_out: Optional[torch.Tensor] = None,
+             reset_stats: bool = True) -> Optional[torch.Tensor]:
+        if reset_stats:
+            self.stats.zero_()
+        need = _lib.load().qb_csr_tracker_workspace_bytes(self.G, self.max_slots, batch.M)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        _lib.call("qb_dev_csr_tracker_step", self.G, self.max_slots, _ptr(self.off),
+                  _ptr(self.cfg), batch.M, _ptr(batch.group), _ptr(batch.flags),
+                  _ptr(batch.index), _ptr(batch.term), _ptr(self.term), _ptr(self.term_start),
+                  _ptr(self.match), _ptr(self.next), _ptr(self.active), _ptr(self.committed),
+                  _ptr(self.stepdown_at), _ptr(advanced_out), _ptr(self.stats), _ptr(self._ws),
+                  self._ws.numel(), _stream(self.device))
         return advanced_out
 
     def stats_dict(self) -> dict:

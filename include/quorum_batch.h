@@ -102,8 +102,9 @@ enum {
   QB_VSTAT_DUPLICATE = 1,      /* the slot had already voted (first vote wins)   */
   QB_VSTAT_STALE_TERM = 2,     /* m.Term < group term: dropped                   */
   QB_VSTAT_HIGHER_TERM = 3,    /* the candidate steps down (raft.go:872-879)     */
-  QB_VSTAT_AFTER_STEPDOWN = 4, /* polled record behind the group's step-down     */
+  QB_VSTAT_AFTER_STEPDOWN = 4, /* any record behind the group's step-down        */
   QB_VSTAT_BAD = 5,            /* group index >= G                               */
+  QB_VSTAT_AFTER_DECISION = 6, /* behind the group's VoteWon / VoteLost          */
   QB_VSTAT_COUNT = 8
 };
 
@@ -133,6 +134,30 @@ int qb_copy_d2h_async(void* dst, const void* src, size_t bytes, void* stream);
 int qb_stream_create(void** out);
 int qb_stream_destroy(void* stream);
 int qb_stream_sync(void* stream);
+
+/* ----------------------------------------------------------------------- */
+/* Config compile (host)                                                   */
+/* ----------------------------------------------------------------------- */
+
+/* tracker.Config per group (tracker/tracker.go:27-78) -> the CSR layout:
+ * slots = the sorted union of Voters[0], Voters[1] and Learners (the order of
+ * MajorityConfig.Slice, quorum/majority.go:106-113; LearnersNext members are
+ * outgoing voters until LeaveJoint, so they are in Voters[1]); cfg[g] =
+ * mask_in | mask_out << 16 over those slots; a learner is in neither mask.
+ * Each input is a CSR of IDs: group g's Voters[0] are in_ids[in_off[g] ..
+ * in_off[g+1]) (out_off/out_ids, lrn_off/lrn_ids nullable = empty sets);
+ * duplicate IDs within a list are one member.  Writes off[G+1], cfg[G] and,
+ * if slot_ids is non-NULL, the slot IDs (slot_cap entries available; call
+ * once with slot_ids NULL to size it: off[G] = slots needed).  A group whose
+ * learners intersect its voters (confchange.go:307-318: "%d is in Learners
+ * and Voters[1]" / "[0]") or with more than QB_MAX_SLOTS members fails the
+ * call with QB_EINVAL, *bad_group (nullable) = the first such group and the
+ * reference's message in qb_last_error().  Host memory only; no device. */
+int qb_host_compile_configs(uint64_t G, const uint32_t* in_off, const uint64_t* in_ids,
+                            const uint32_t* out_off, const uint64_t* out_ids,
+                            const uint32_t* lrn_off, const uint64_t* lrn_ids,
+                            uint32_t* off, uint32_t* cfg, uint64_t* slot_ids,
+                            uint64_t slot_cap, uint64_t* bad_group);
 
 /* ----------------------------------------------------------------------- */
 /* Quorum math (raft/quorum)                                               */
@@ -202,11 +227,11 @@ int qb_dev_csr_quorum_active(uint64_t G, const uint32_t* cfg,
  *   group_term[G]   the leader's current term per group
  *   match[n][G], next[n][G] (nullable), active[G] (uint16 bits; the array
  *                   must be 4-byte aligned and padded to an even length)
- *   stepdown_at[G]  uint32, must hold UINT32_MAX on entry for every group;
- *                   on return it holds the batch index of the first
- *                   higher-term record of a group that must step down
- *                   (raft.go:875-879), UINT32_MAX otherwise.  Records after
- *                   it are not applied, as in the sequential reference.
+ *   stepdown_at[G]  uint32 output, written for every group (no entry
+ *                   requirement): the batch index of the first higher-term
+ *                   record of a group that must step down (raft.go:875-879),
+ *                   UINT32_MAX otherwise.  Records after it are not applied,
+ *                   as in the sequential reference.
  *   stats[QB_STAT_COUNT] device uint64 counters (required; zero them per
  *                   batch — a non-zero HIGHER_TERM count only makes the
  *                   apply pass consult stepdown_at, it never changes results). */
@@ -238,7 +263,14 @@ int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
  * The records are bucketed by group on the device (counting sort into
  * LDS-sized chunks) so every MaybeUpdate is an LDS atomic; this is the path
  * for large batches (M ~ G).  Differences from the two-call form:
- *   - stepdown_at[g] is written for every group (no entry requirement);
+ *   - stepdown_at[g] must hold UINT32_MAX on entry (the two-call form
+ *     initialises it itself) and is written only where it can change: for
+ *     every group of a chunk (256-512 consecutive groups) holding a
+ *     higher-term record it is reset to UINT32_MAX and then receives the
+ *     step-down record's batch index; every other entry is left untouched
+ *     (no per-group write in the steady state).  A caller re-arming a group
+ *     that stepped down resets its entry; stats[QB_STAT_HIGHER_TERM] > 0 says
+ *     whether any group stepped down;
  *   - workspace: device scratch of qb_fixed_tracker_workspace_bytes(n, G, M)
  *     bytes (caller-owned, reusable across calls of the same or smaller
  *     size; no allocation inside, so the call can be graph-captured).
@@ -257,22 +289,66 @@ int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                               void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* The same leader tick over G groups of the CSR layout (ragged voter
+ * counts, learners, joint configs): a MsgAppResp batch applied (MaybeUpdate on
+ * the slot's Progress, learners included; a slot >= s_g has no Progress and
+ * is dropped before the term filter, node.go:356-360) and maybeCommit for
+ * every group with ProgressTracker.Committed = JointConfig.CommittedIndex
+ * over the voters of both halves (tracker/tracker.go:162-179,
+ * quorum/joint.go:49-56) — the commit advance a joint transition runs on
+ * every ack (raft.go:1259, 1682).  An empty config (both masks 0) never
+ * commits: its CommittedIndex is MaxUint64, past lastIndex, whose term is 0
+ * (log.go:271-273, 328-334).
+ *   off[G+1], cfg[G]   CSR config as qb_dev_csr_committed_vote; max_slots
+ *                      bounds every s_g (0 = QB_MAX_SLOTS) and sizes the
+ *                      kernel (a chunk whose slot run breaks the bound is
+ *                      applied by the exact slow path);
+ *   match[off[G]], next[off[G]] (nullable)  Progress per slot;
+ *   group_term, term_start, active, committed, stepdown_at, advanced_out,
+ *   stats, workspace: as qb_dev_fixed_tracker_step (same stepdown_at rule). */
+size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M);
+int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                            const uint32_t* cfg, uint64_t M,
+                            const uint32_t* rec_group, const uint8_t* rec_flags,
+                            const uint64_t* rec_index, const uint64_t* rec_term,
+                            const uint64_t* group_term,
+                            const uint64_t* term_start, uint64_t* match,
+                            uint64_t* next, uint16_t* active,
+                            uint64_t* committed, uint32_t* stepdown_at,
+                            uint8_t* advanced_out, uint64_t* stats,
+                            void* workspace, size_t workspace_bytes,
+                            void* stream);
+
 /* Elections.  A batch of vote responses of one kind (mode), records
  * {group, flags = slot | reject << 7, term} in batch order, applied to the
  * CSR votes words (voted | granted << 16) exactly as the sequential
  * (pre-)candidate does: raft.Step's term filter (raft.go:847-921, with the
  * MsgPreVoteResp exception of raft.go:866-871), stepCandidate -> poll ->
- * RecordVote with first-vote-wins (tracker/tracker.go:258-263), and nothing
- * after the group's first step-down (stepdown_at as in
- * qb_dev_fixed_apply_appresp: UINT32_MAX on entry).  VoteResult is monotone
- * once decided, so qb_dev_csr_tally_votes after the batch gives the outcome
- * the sequential candidate reaches (raft.go:1402-1414).
- * workspace: qb_votes_workspace_bytes(M) bytes of device scratch. */
+ * RecordVote with first-vote-wins (tracker/tracker.go:258-263) and
+ * TallyVotes against cfg (mask_in | mask_out << 16, learners in neither).
+ * At the first response after which the result is VoteWon / VoteLost the
+ * node changes state (raft.go:1402-1414) and polls nothing more:
+ *   decided_at[g]  batch index of that response (UINT32_MAX: still pending);
+ *                  votes[g] is left as it stood there, so
+ *                  qb_dev_csr_tally_votes gives the decision;
+ *   stepdown_at[g] batch index of the response that makes the node
+ *                  becomeFollower at a higher term (UINT32_MAX: none): before
+ *                  the decision any response above the group term (a granted
+ *                  MsgPreVoteResp excepted); after a pre-candidate's VoteWon
+ *                  the node campaigned at term + 1 (raft.go:1403 ->
+ *                  becomeCandidate), so only a rejection above term + 1; after
+ *                  a candidate's VoteWon / any VoteLost, a response above the
+ *                  group term.  Nothing after the step-down is applied.
+ * Both outputs are written for every group (no entry requirement).  The
+ * state change itself (campaign with ResetVotes, becomeLeader, becomeFollower)
+ * is the host's.  workspace: qb_votes_workspace_bytes(M) bytes of device
+ * scratch. */
 size_t qb_votes_workspace_bytes(uint64_t M);
 int qb_dev_record_votes(int mode, uint64_t G, uint64_t M,
                         const uint32_t* rec_group, const uint8_t* rec_flags,
                         const uint64_t* rec_term, const uint64_t* group_term,
-                        uint32_t* votes, uint32_t* stepdown_at, uint64_t* stats,
+                        const uint32_t* cfg, uint32_t* votes, uint32_t* stepdown_at,
+                        uint32_t* decided_at, uint64_t* stats,
                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ProgressTracker.TallyVotes (tracker/tracker.go:267-288) per group:
@@ -551,6 +627,36 @@ size_t qb_conf_change_workspace_bytes(uint64_t G);
  * new_off[G] after the call. */
 int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_change_out* out,
                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* ----------------------------------------------------------------------- */
+/* Sharding over the GPUs of a node                        */
+/* ----------------------------------------------------------------------- */
+
+/* One process per GPU; rank r owns the contiguous global groups
+ * [begin, end) = qb_shard_range(total, world, r) (sizes differ by at most
+ * one; etcd_amd/shard.py shard_range).  Groups are independent, so the hot
+ * path exchanges nothing; the one collective is at its edge: the node-wide
+ * CommittedIndex / VoteResult vectors assembled from the shards by an RCCL
+ * all-gather over xGMI.  The host distributes the 128-byte unique ID from
+ * rank 0 over its own transport (the reference's peer transport is
+ * rafthttp, server/etcdserver/api/rafthttp/peer.go:178). */
+#define QB_COMM_ID_BYTES 128
+typedef struct qb_comm qb_comm;
+int qb_shard_range(uint64_t total, int world, int rank, uint64_t* begin, uint64_t* end);
+int qb_comm_get_unique_id(void* id_out);
+/* ncclCommInitRank on the calling thread's current device (qb_set_device);
+ * collective: every rank calls it with the same id. */
+int qb_comm_init(qb_comm** out, int world, int rank, const void* id);
+int qb_comm_destroy(qb_comm* comm);
+size_t qb_allgather_workspace_bytes(uint64_t total, int world);
+/* commit_all[total] / vote_all[total] (device; either nullable) receive every
+ * rank's shard in rank order.  Collective over the comm, enqueued on stream.
+ * The workspace (device, qb_allgather_workspace_bytes) is needed only when
+ * total % world != 0 (padded shards compacted by rank). */
+int qb_dev_allgather_results(qb_comm* comm, uint64_t total,
+                             const uint64_t* commit_shard, const uint8_t* vote_shard,
+                             uint64_t* commit_all, uint8_t* vote_all,
+                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */

@@ -187,7 +187,7 @@ static u8 joint_vote(u8 r1, u8 r2) { /* joint.go:61-75 */
 
 /* CSR group: members of one half given by mask; non-members ignored. */
 static u64 csr_half_ci(const u64* m, u32 s, u32 mask) {
-  u64 vals[16];
+  u64 vals[16] = {0};
   int n = 0;
   for (u32 j = 0; j < s; ++j)
     if ((mask >> j) & 1) vals[n++] = m[j];
@@ -529,51 +529,184 @@ void orc_csr_eval_mt(u64 G, const u32* off, const u64* match, const u32* cfg, co
 
 /* ------------------------------------------------ sequential tracker ----- */
 
-/* Sequential MsgAppResp processing for FIXED-layout leaders (n voters, slot
- * s <-> voter), records in batch order.  stepped_down[g] is set to 1 when a
- * higher-term record makes the leader step down (raft.go:875-879); later
- * records of that group are not applied (they are stale for the follower).
- * committed[] advances via maybeCommit after every MaybeUpdate that returned
- * true, gated by term(ci) == term  <=>  ci >= term_start[g].
+/* Leader-side tracker state in either layout: FIXED (n voters, slot-major
+ * rows of G: match[s * G + g]) or CSR (n == 0: slots off[g] .. off[g+1]-1,
+ * group-major, cfg = mask_in | mask_out << 16; a slot in neither mask is a
+ * learner, which has a Progress but no vote, tracker.go:27-78). */
+typedef struct {
+  u32 n;
+  u64 G;
+  const u32* off;
+  const u32* cfg;
+} orc_layout;
+
+static inline u32 lay_slots(const orc_layout* L, u64 g) {
+  return L->n ? L->n : L->off[g + 1] - L->off[g];
+}
+static inline u64 lay_at(const orc_layout* L, u64 g, u32 s) {
+  return L->n ? (u64)s * L->G + g : (u64)L->off[g] + s;
+}
+/* ProgressTracker.Committed (tracker.go:177-179): JointConfig.CommittedIndex
+ * (joint.go:49-56) over the voters' Match; FIXED is one n-voter half. */
+static u64 lay_ci(const orc_layout* L, const u64* match, u64 g) {
+  if (L->n) {
+    u64 vals[16];
+    for (u32 k = 0; k < L->n; ++k) vals[k] = match[(u64)k * L->G + g];
+    return majority_ci(vals, (int)L->n);
+  }
+  const u64* m = match + L->off[g];
+  u32 s = L->off[g + 1] - L->off[g];
+  u64 c0 = csr_half_ci(m, s, L->cfg[g] & 0xFFFF), c1 = csr_half_ci(m, s, L->cfg[g] >> 16);
+  return c0 < c1 ? c0 : c1;
+}
+/* raftLog.maybeCommit (log.go:328-334): ci > committed && term(ci) == Term.
+ * For a leader term(i) == Term <=> term_start <= i <= lastIndex; no voter acks
+ * past lastIndex, and an empty config's ci = MaxUint64 lies past it
+ * (raftLog.term of an index beyond lastIndex is 0, log.go:271-273). */
+static int commit_gate(u64 ci, u64 committed, u64 term_start) {
+  return ci != INF && ci > committed && ci >= term_start;
+}
+
+/* Sequential MsgAppResp processing, records in batch order, restricted to
+ * groups [lo, hi) (the partitioned multi-thread form: groups are independent,
+ * so each thread scanning the whole batch for its own groups is exactly the
+ * sequential result).  stepped_down[g] is set to 1 when a higher-term record
+ * makes the leader step down (raft.go:875-879); later records of that group
+ * are not applied.  committed[] advances via maybeCommit after every
+ * MaybeUpdate that returned true (raft.go:1259 -> 585-588).
  * Returns -1 if a record acks past the leader's log (index > last_index[g]),
  * which the reference treats as log corruption (log.go:239-241); else 0. */
-int orc_fixed_appresp_sequential(u32 n, u64 G, u64 M, const u32* rg, const u8* rf,
-                                 const u64* ri, const u64* rt, const u64* group_term,
-                                 const u64* term_start, const u64* last_index, u64* match,
-                                 u64* next, u16* active, u64* committed, u8* stepped_down,
-                                 u64* stats /* [8] */) {
+static int appresp_range(const orc_layout* L, u64 lo, u64 hi, u64 M, const u32* rg,
+                         const u8* rf, const u64* ri, const u64* rt, const u64* group_term,
+                         const u64* term_start, const u64* last_index, u64* match, u64* next,
+                         u16* active, u64* committed, u8* stepped_down, u64* stats) {
   for (u64 i = 0; i < M; ++i) {
     u64 g = rg[i];
+    if (g >= L->G) {
+      if (lo == 0) stats[5]++; /* counted once, by the first partition */
+      continue;
+    }
+    if (g < lo || g >= hi) continue;
     u32 s = rf[i] & 0x0F;
     int reject = (rf[i] & 0x80) != 0;
-    if (g >= G) { stats[5]++; continue; }
-    if (s >= n) { stats[3]++; continue; }            /* raft.go:1100-1104 */
+    if (s >= lay_slots(L, g)) { stats[3]++; continue; } /* raft.go:1100-1104 */
     if (rt[i] < group_term[g]) { stats[2]++; continue; } /* raft.go:883-921 */
-    if (rt[i] > group_term[g]) {                      /* raft.go:852-880 */
+    if (rt[i] > group_term[g]) {                          /* raft.go:852-880 */
       stats[4]++;
       if (!stepped_down[g]) stepped_down[g] = 1;
       continue;
     }
     if (stepped_down[g]) { stats[6]++; continue; }
-    active[g] |= (u16)(1u << s);                      /* raft.go:1107 */
+    active[g] |= (u16)(1u << s);                          /* raft.go:1107 */
     if (reject) { stats[1]++; continue; }
     stats[0]++;
     if (last_index && ri[i] > last_index[g]) return -1;
-    u64* pm = match + (u64)s * G + g;
+    u64 at = lay_at(L, g, s);
     int updated = 0;
-    if (*pm < ri[i]) { *pm = ri[i]; updated = 1; }    /* progress.go:146-150 */
-    if (next) {
-      u64* pn = next + (u64)s * G + g;
-      if (*pn < ri[i] + 1) *pn = ri[i] + 1;           /* progress.go:151 */
-    }
-    if (updated) {                                    /* raft.go:1259 -> 585-588 */
-      u64 vals[16];
-      for (u32 k = 0; k < n; ++k) vals[k] = match[(u64)k * G + g];
-      u64 ci = majority_ci(vals, (int)n);
-      if (ci > committed[g] && ci >= term_start[g]) committed[g] = ci; /* log.go:328-334 */
+    if (match[at] < ri[i]) { match[at] = ri[i]; updated = 1; } /* progress.go:146-150 */
+    if (next && next[at] < ri[i] + 1) next[at] = ri[i] + 1;    /* progress.go:151 */
+    if (updated) {
+      u64 ci = lay_ci(L, match, g);
+      if (commit_gate(ci, committed[g], term_start[g])) committed[g] = ci;
     }
   }
   return 0;
+}
+
+typedef struct {
+  const orc_layout* L;
+  u64 lo, hi, M;
+  const u32* rg;
+  const u8* rf;
+  const u64 *ri, *rt, *gt, *ts, *last;
+  u64 *match, *next, *committed;
+  u16* active;
+  u8* sd;
+  u64 stats[8];
+  int rc;
+} orc_seq_job;
+
+static void* orc_seq_worker(void* p) {
+  orc_seq_job* j = (orc_seq_job*)p;
+  j->rc = appresp_range(j->L, j->lo, j->hi, j->M, j->rg, j->rf, j->ri, j->rt, j->gt, j->ts,
+                        j->last, j->match, j->next, j->active, j->committed, j->sd, j->stats);
+  return 0;
+}
+
+static int appresp_run(const orc_layout* L, u64 M, const u32* rg, const u8* rf, const u64* ri,
+                       const u64* rt, const u64* group_term, const u64* term_start,
+                       const u64* last_index, u64* match, u64* next, u16* active,
+                       u64* committed, u8* stepped_down, u64* stats, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  orc_seq_job* jobs = (orc_seq_job*)calloc((size_t)threads, sizeof(orc_seq_job));
+  if (!jobs) return -2;
+  for (int t = 0; t < threads; ++t) {
+    orc_seq_job* j = &jobs[t];
+    memset(j, 0, sizeof *j);
+    j->L = L;
+    j->lo = L->G * (u64)t / (u64)threads;
+    j->hi = L->G * (u64)(t + 1) / (u64)threads;
+    j->M = M;
+    j->rg = rg, j->rf = rf, j->ri = ri, j->rt = rt, j->gt = group_term, j->ts = term_start;
+    j->last = last_index, j->match = match, j->next = next, j->active = active;
+    j->committed = committed, j->sd = stepped_down;
+    if (threads == 1) orc_seq_worker(j);
+    else pthread_create(&tid[t], 0, orc_seq_worker, j);
+  }
+  int rc = 0;
+  for (int t = 0; t < threads; ++t) {
+    if (threads > 1) pthread_join(tid[t], 0);
+    for (int k = 0; k < 8; ++k) stats[k] += jobs[t].stats[k];
+    if (jobs[t].rc) rc = jobs[t].rc;
+  }
+  free(jobs);
+  return rc;
+}
+
+/* FIXED layout (n voters, slot s <-> the s-th smallest voter ID). */
+int orc_fixed_appresp_sequential(u32 n, u64 G, u64 M, const u32* rg, const u8* rf,
+                                 const u64* ri, const u64* rt, const u64* group_term,
+                                 const u64* term_start, const u64* last_index, u64* match,
+                                 u64* next, u16* active, u64* committed, u8* stepped_down,
+                                 u64* stats /* [8] */) {
+  orc_layout L = {n, G, 0, 0};
+  return appresp_run(&L, M, rg, rf, ri, rt, group_term, term_start, last_index, match, next,
+                     active, committed, stepped_down, stats, 1);
+}
+
+int orc_fixed_appresp_sequential_mt(u32 n, u64 G, u64 M, const u32* rg, const u8* rf,
+                                    const u64* ri, const u64* rt, const u64* group_term,
+                                    const u64* term_start, const u64* last_index, u64* match,
+                                    u64* next, u16* active, u64* committed, u8* stepped_down,
+                                    u64* stats, int threads) {
+  orc_layout L = {n, G, 0, 0};
+  return appresp_run(&L, M, rg, rf, ri, rt, group_term, term_start, last_index, match, next,
+                     active, committed, stepped_down, stats, threads);
+}
+
+/* CSR layout (ragged voters + learners, joint configs). */
+int orc_csr_appresp_sequential(u64 G, const u32* off, const u32* cfg, u64 M, const u32* rg,
+                               const u8* rf, const u64* ri, const u64* rt, const u64* group_term,
+                               const u64* term_start, const u64* last_index, u64* match,
+                               u64* next, u16* active, u64* committed, u8* stepped_down,
+                               u64* stats, int threads) {
+  orc_layout L = {0, G, off, cfg};
+  return appresp_run(&L, M, rg, rf, ri, rt, group_term, term_start, last_index, match, next,
+                     active, committed, stepped_down, stats, threads);
+}
+
+/* maybeCommit for every CSR group (initial invariant / empty batch). */
+void orc_csr_commit_all(u64 G, const u32* off, const u32* cfg, const u64* match,
+                        const u64* term_start, u64* committed, u8* advanced) {
+  orc_layout L = {0, G, off, cfg};
+  for (u64 g = 0; g < G; ++g) {
+    u64 ci = lay_ci(&L, match, g);
+    int adv = commit_gate(ci, committed[g], term_start[g]);
+    if (adv) committed[g] = ci;
+    if (advanced) advanced[g] = (u8)adv;
+  }
 }
 
 /* maybeCommit for every group (used to establish the initial invariant). */

@@ -349,27 +349,58 @@ def datadriven_inputs(case):
 STAT_RECORDED, STAT_DUPLICATE, STAT_STALE, STAT_HIGHER, STAT_AFTER, STAT_BAD = range(6)
 
 
-def vote_response_sequential(prevote: bool, group_term: int, stepped_down: bool,
-                             votes: dict, slot: int, reject: bool, term: int):
-    """One MsgVoteResp / MsgPreVoteResp reaching a (pre-)candidate whose
-    Votes map is ``votes`` (slot -> granted).  Returns (stat, stepped_down).
+STAT_AFTER_DECISION = 6
 
-    raft.go:847-921 — Step's term handling: a lower term is ignored; a higher
-    term makes the node becomeFollower, except a granted MsgPreVoteResp
-    (raft.go:866-871); after stepping down the node is a follower and no later
-    response reaches poll.  raft.go:1391-1400 — stepCandidate polls
-    myVoteRespType; poll (raft.go:837-845) -> RecordVote, first vote wins
-    (tracker.go:258-263)."""
-    if term < group_term:
-        return STAT_STALE, stepped_down
-    if term > group_term and (reject or not prevote):
-        return STAT_HIGHER, True
-    if stepped_down:
-        return STAT_AFTER, stepped_down
-    if slot in votes:
-        return STAT_DUPLICATE, stepped_down
-    votes[slot] = not reject
-    return STAT_RECORDED, stepped_down
+
+class Candidate:
+    """The quorum-facing state of a (pre-)candidate taking its vote responses
+    one at a time, in batch order (raft.go:847-921 Step's term handling,
+    raft.go:1383-1414 stepCandidate, raft.go:837-845 poll, tracker.go:258-288
+    RecordVote / TallyVotes).  ``votes`` maps slot -> granted; c0 / c1 are the
+    slot sets of JointConfig halves Voters[0] / Voters[1].
+
+    At VoteWon / VoteLost the node changes state (raft.go:1402-1414): a
+    pre-candidate campaigns (becomeCandidate: term + 1, raft.go:1403), a
+    candidate becomes leader, a loser becomes follower at its term.  None of
+    them polls another response of this kind (a candidate's myVoteRespType is
+    MsgVoteResp, raft.go:1385-1390; leaders and followers do not handle vote
+    responses); a response above the node's current term still makes it
+    becomeFollower — except a granted MsgPreVoteResp, which never changes the
+    term (raft.go:866-871).  The new election's ResetVotes and self vote
+    (campaign) are not modelled: the votes stay as they stood at the decision."""
+
+    def __init__(self, prevote: bool, term: int, c0, c1, votes: dict):
+        self.prevote, self.term = prevote, term
+        self.c0, self.c1, self.votes = set(c0), set(c1), votes
+        self.state = "PreCandidate" if prevote else "Candidate"
+        self.down = False
+        self.decided = False
+
+    def step(self, slot: int, reject: bool, term: int) -> int:
+        if self.down:
+            return STAT_AFTER
+        if term > self.term and not (self.prevote and not reject):
+            self.term, self.state, self.down = term, "Follower", True  # becomeFollower
+            return STAT_HIGHER
+        mine = self.state == ("PreCandidate" if self.prevote else "Candidate")
+        if not mine:
+            return STAT_AFTER_DECISION
+        if term < self.term:
+            return STAT_STALE
+        # poll -> RecordVote (first vote wins) -> TallyVotes
+        stat = STAT_DUPLICATE if slot in self.votes else STAT_RECORDED
+        self.votes.setdefault(slot, not reject)
+        res = joint_vote_result(self.c0, self.c1, self.votes)
+        if res == VOTE_WON:
+            self.decided = True
+            if self.prevote:
+                self.term, self.state = self.term + 1, "Candidate"  # campaign(campaignElection)
+            else:
+                self.state = "Leader"
+        elif res == VOTE_LOST:
+            self.decided = True
+            self.state = "Follower"
+        return stat
 
 
 def tally_votes_slots(mask_in: int, mask_out: int, votes: dict):

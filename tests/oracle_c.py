@@ -32,7 +32,12 @@ SIG = {
     "orc_csr_eval_mt": (None, [_u64, _p, _p, _p, _p, _p, _p, _i32]),
     "orc_fixed_appresp_sequential": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                             _p, _p, _p, _p, _p]),
+    "orc_fixed_appresp_sequential_mt": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p,
+                                               _p, _p, _p, _p, _p, _p, _i32]),
+    "orc_csr_appresp_sequential": (_i32, [_u64, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                          _p, _p, _p, _p, _p, _i32]),
     "orc_fixed_commit_all": (None, [_u32, _u64, _p, _p, _p, _p]),
+    "orc_csr_commit_all": (None, [_u64, _p, _p, _p, _p, _p, _p]),
     "orc_bench_plumbing": (_u64, [_u32, _u64, _u64]),
     "orc_leader_step": (_u64, [_p, _p, _p, _u64, _p, _p, _p, _i32]),
     "orc_ingest": (None, [_u64, _p, _u64, _p, _p, _u64, _p, _p] + [_p] * 7 + [_i32]),
@@ -151,19 +156,48 @@ def faithful_eval(maps, G, threads=1):
     return commit, vote
 
 
-def appresp_sequential(n, G, rec, state):
+def appresp_sequential(n, G, rec, state, threads=1):
     """Sequential reference semantics; ``state`` (dict of numpy arrays) is
-    updated in place.  Returns the stats array."""
+    updated in place.  Returns the stats array.  threads > 1 partitions the
+    groups (each thread scans the batch for its own groups: the same result)."""
     lib = load()
     stats = np.zeros(8, np.uint64)
     group, flags, index, term = rec
-    rc = lib.orc_fixed_appresp_sequential(
+    rc = lib.orc_fixed_appresp_sequential_mt(
         n, G, len(group), ptr(group), ptr(flags), ptr(index), ptr(term), ptr(state["term"]),
         ptr(state["term_start"]), ptr(state.get("last_index")), ptr(state["match"]),
         ptr(state.get("next")), ptr(state["active"]), ptr(state["committed"]),
-        ptr(state["stepped_down"]), ptr(stats))
+        ptr(state["stepped_down"]), ptr(stats), threads)
     assert rc == 0, "a record acked past the leader's last index"
     return stats
+
+
+def csr_appresp_sequential(off, cfg, rec, state, threads=1):
+    """Sequential MsgAppResp semantics over the CSR layout (learners have a
+    Progress, joint CommittedIndex); ``state`` updated in place."""
+    lib = load()
+    stats = np.zeros(8, np.uint64)
+    group, flags, index, term = rec
+    G = len(cfg)
+    m = state["match"] if state["match"].size else np.zeros(1, np.uint64)
+    nx = state.get("next")
+    rc = lib.orc_csr_appresp_sequential(
+        G, ptr(off), ptr(cfg), len(group), ptr(group), ptr(flags), ptr(index), ptr(term),
+        ptr(state["term"]), ptr(state["term_start"]), ptr(state.get("last_index")), ptr(m),
+        ptr(nx if nx is None or nx.size else np.zeros(1, np.uint64)), ptr(state["active"]),
+        ptr(state["committed"]), ptr(state["stepped_down"]), ptr(stats), threads)
+    assert rc == 0, "a record acked past the leader's last index"
+    return stats
+
+
+def csr_commit_all(off, cfg, match, term_start, committed):
+    lib = load()
+    G = len(committed)
+    adv = np.empty(G, np.uint8)
+    m = match if match.size else np.zeros(1, np.uint64)
+    lib.orc_csr_commit_all(G, ptr(off), ptr(cfg), ptr(m), ptr(term_start), ptr(committed),
+                           ptr(adv))
+    return adv
 
 
 def commit_all(n, match, term_start, committed):

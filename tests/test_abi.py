@@ -90,3 +90,69 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.QuorumBatchError, match="no CPU fallback"):
         _lib.load()
+
+
+def _py_compile(vi, vo, lr):
+    """tracker.Config -> slots/masks restated in Python (tracker.go:27-78,
+    majority.go:106-113)."""
+    slot = sorted(set(vi) | set(vo) | set(lr))
+    m_in = sum(1 << j for j, i in enumerate(slot) if i in set(vi))
+    m_out = sum(1 << j for j, i in enumerate(slot) if i in set(vo))
+    return slot, m_in | (m_out << 16)
+
+
+def test_host_compile_configs_random_vs_python():
+    """qb_host_compile_configs (the C ABI config compile a cgo embedder calls)
+    equals the Python restatement on random joint configs with learners and
+    duplicate IDs, across the multi-thread threshold (65536 groups)."""
+    rng = np.random.default_rng(11)
+    G = 70000
+    vi, vo, lr = [], [], []
+    for g in range(G):
+        ids = rng.choice(np.arange(1, 40), size=12, replace=False).tolist()
+        a = int(rng.integers(0, 6))
+        b = int(rng.integers(0, 6)) if rng.random() < 0.3 else 0
+        c = int(rng.integers(0, 3))
+        inc = ids[:a] + ids[:a][:1]              # a duplicate ID in the list
+        out = ids[max(0, a - 2):max(0, a - 2) + b]
+        vi.append(inc)
+        vo.append(out)
+        lr.append(ids[8:8 + c])
+    cc = batch.compile_configs(vi, vo, lr)
+    for g in rng.integers(0, G, size=3000).tolist() + [0, G - 1]:
+        slot, cfg = _py_compile(vi[g], vo[g], lr[g])
+        assert cc.slots(g).tolist() == slot and int(cc.cfg[g]) == cfg
+
+
+def test_host_compile_configs_errors_name_the_reference_invariant():
+    with pytest.raises(ValueError, match=r"group 1: 3 is in Learners and Voters\[0\]"):
+        batch.compile_configs([{1}, {2, 3}], [set(), set()], [set(), {3, 9}])
+    with pytest.raises(ValueError, match=r"group 0: 4 is in Learners and Voters\[1\]"):
+        batch.compile_configs([{1, 4}], [{4, 5}], [{4}])
+    with pytest.raises(ValueError, match=r"more than 16 members"):
+        batch.compile_configs([set(range(1, 10))], [set(range(10, 18))])
+    lib = _lib.load()
+    off = np.array([0, 1], np.uint32)
+    ids = np.array([7], np.uint64)
+    o = np.zeros(2, np.uint32)
+    c = np.zeros(1, np.uint32)
+    out = np.zeros(1, np.uint64)
+    # slot_cap too small is an error, a sizing call (slot_ids NULL) is not
+    assert lib.qb_host_compile_configs(1, off.ctypes.data, ids.ctypes.data, None, None, None,
+                                       None, o.ctypes.data, c.ctypes.data, None, 0, None) == 0
+    assert o.tolist() == [0, 1] and c.tolist() == [1]
+    assert lib.qb_host_compile_configs(1, off.ctypes.data, ids.ctypes.data, None, None, None,
+                                       None, o.ctypes.data, c.ctypes.data, out.ctypes.data, 0,
+                                       None) == _lib.QB_EINVAL
+
+
+def test_shard_range_matches_python():
+    """qb_shard_range (C ABI) == etcd_amd.shard.shard_range for every rank."""
+    from etcd_amd.shard import shard_range
+    lib = _lib.load()
+    b, e = C.c_uint64(), C.c_uint64()
+    for total, world in ((0, 1), (7, 3), (1 << 27, 8), (1000003, 8), (5, 8)):
+        for r in range(world):
+            assert lib.qb_shard_range(total, world, r, C.byref(b), C.byref(e)) == 0
+            assert (b.value, e.value) == shard_range(total, world, r)
+    assert lib.qb_shard_range(10, 2, 2, C.byref(b), C.byref(e)) == _lib.QB_EINVAL

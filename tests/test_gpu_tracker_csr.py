@@ -1,0 +1,243 @@
+"""GPU parity for the CSR tracker step (qb_dev_csr_tracker_step): MsgAppResp
+batches over ragged voter counts, learners and joint configs — MaybeUpdate
+on the slot's Progress (learners included), the non-member drop before the
+term filter (node.go:356-360), step-down ordering, and maybeCommit with
+JointConfig.CommittedIndex (tracker.go:162-179, joint.go:49-56) — against the
+sequential one-record-at-a-time C oracle (oracle/quorum_oracle.c
+appresp_range over the CSR layout)."""
+import numpy as np
+import pytest
+import torch
+
+from etcd_amd.quorum import batch
+from tests import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MAX = (1 << 64) - 1
+
+
+def _state(rng, kind, G, term_base=0, seed=0x5EED0003):
+    off, match, cfg, _ = oc.gen_csr(seed, kind, G)
+    sizes = np.diff(off.astype(np.int64))
+    last = np.zeros(G, np.uint64)
+    nz = sizes > 0
+    last[nz] = np.maximum.reduceat(match, off[:-1][nz].astype(np.int64)) if match.size else 0
+    term = rng.integers(2, 9, size=G).astype(np.uint64) + np.uint64(term_base)
+    ts = last - rng.integers(0, 128, size=G).astype(np.uint64)
+    st = {"match": match.copy(), "next": (match + np.uint64(1)).copy(),
+          "active": np.zeros(G, np.uint16), "term": term, "term_start": ts, "last_index": last,
+          "committed": np.zeros(G, np.uint64), "stepped_down": np.zeros(G, np.uint8)}
+    oc.csr_commit_all(off, cfg, st["match"], ts, st["committed"])
+    return off, cfg, sizes, st
+
+
+def _tracker(off, cfg, st, track_next=True, max_slots=None):
+    G = len(cfg)
+    tr = batch.CsrTracker(torch.from_numpy(off.view(np.int32).copy()).to(DEV),
+                          torch.from_numpy(cfg.view(np.int32).copy()).to(DEV),
+                          max_slots=max_slots, device=DEV, track_next=track_next)
+    if st["match"].size:
+        tr.match[: st["match"].size].copy_(batch.from_u64(st["match"], DEV))
+        if track_next:
+            tr.next[: st["match"].size].copy_(batch.from_u64(st["next"], DEV))
+    act = np.zeros(G + (G & 1), np.uint16)
+    act[:G] = st["active"]
+    tr.active.copy_(torch.from_numpy(act.view(np.int16)))
+    tr.term.copy_(batch.from_u64(st["term"], DEV))
+    tr.term_start.copy_(batch.from_u64(st["term_start"], DEV))
+    tr.committed.copy_(batch.from_u64(st["committed"], DEV))
+    return tr
+
+
+def _batch(rng, G, M, sizes, st, stale=0.01, higher=0.0, reject=0.02, nonmember=0.0, bad=0.0):
+    group = rng.integers(0, G, size=M).astype(np.uint32)
+    s_g = sizes[group]
+    slot = (rng.integers(0, 1 << 30, size=M) % np.maximum(s_g, 1)).astype(np.uint8)
+    # a group with no slots only ever gets non-member records
+    slot = np.where(s_g == 0, np.uint8(0), slot).astype(np.uint8)
+    if nonmember:
+        past = (s_g + rng.integers(0, 3, size=M)).clip(max=15).astype(np.uint8)
+        slot = np.where(rng.random(M) < nonmember, past, slot).astype(np.uint8)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 96, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    term = st["term"][group].copy()
+    u = rng.random(M)
+    term = np.where(u < stale, term - np.uint64(1), term)
+    term = np.where((u >= stale) & (u < stale + higher), term + np.uint64(1), term)
+    rej = rng.random(M) < reject
+    if bad:
+        group = np.where(rng.random(M) < bad, np.uint32(G + 3), group).astype(np.uint32)
+    flags = (slot | (rej.astype(np.uint8) << 7)).astype(np.uint8)
+    return group, slot, index, term.astype(np.uint64), rej, flags
+
+
+def _compare(tr, st, G):
+    S = st["match"].size
+    assert np.array_equal(batch.as_u64(tr.match)[:S], st["match"])
+    if tr.next is not None:
+        assert np.array_equal(batch.as_u64(tr.next)[:S], st["next"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+
+
+CASES = [
+    ("ragged", 4096, 8192, {}),
+    ("ragged", 1000, 20000, {"higher": 0.002, "nonmember": 0.02, "bad": 0.01}),  # duplicates
+    ("joint", 3000, 6000, {"reject": 0.2, "stale": 0.1}),
+    ("joint", 5000, 30000, {"higher": 0.01, "nonmember": 0.01}),
+    ("ragged", 70001, 70001, {"higher": 0.001}),                     # > 1 super-bucket
+    ("joint", 1, 50, {"higher": 0.1}),
+]
+
+
+@pytest.mark.parametrize("kind,G,M,kw", CASES)
+def test_csr_step_vs_sequential(kind, G, M, kw):
+    rng = np.random.default_rng(G * 31 + M)
+    off, cfg, sizes, st = _state(rng, kind, G)
+    tr = _tracker(off, cfg, st)
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(3):
+        group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, seq, **kw)
+        stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, G)
+        got = tr.stats_dict()
+        want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                         "bad_group", "after_stepdown"), stats.tolist()))
+        assert got == want
+        tr.stepdown_at.fill_(-1)   # caller re-arms the stepped-down groups
+        seq["stepped_down"][:] = 0
+
+
+@pytest.mark.parametrize("term_base", [0xFFFFFFFF - 5, (1 << 64) - 16])
+def test_csr_step_wide_terms(term_base):
+    """Group terms straddling the u32 escape (qb_bucket.h term_to32)."""
+    G = M = 20000
+    rng = np.random.default_rng(term_base % 99991)
+    off, cfg, sizes, st = _state(rng, "joint", G, term_base)
+    tr = _tracker(off, cfg, st, track_next=False)
+    st.pop("next")
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(2):
+        group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, seq, stale=0.05,
+                                                      higher=0.01)
+        stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, G)
+        assert tr.stats_dict()["higher_term"] == stats[4]
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
+
+
+def test_csr_step_learners_ack_but_never_count():
+    """A learner's Progress takes the ack (MaybeUpdate, RecentActive) but the
+    commit index stays the voters' quorum (tracker.go:162-179)."""
+    # group 0: voters {1,2,3} + learner 4; group 1: joint {1,2,3} x {3,4,5}
+    cc = batch.compile_configs([{1, 2, 3}, {1, 2, 3}], [set(), {3, 4, 5}], [{4}, set()])
+    off, cfg = cc.off, cc.cfg
+    st = {"match": np.array([10, 0, 0, 0, 10, 0, 0, 0, 0], np.uint64),
+          "active": np.zeros(2, np.uint16), "term": np.array([5, 5], np.uint64),
+          "term_start": np.array([1, 1], np.uint64), "last_index": np.array([10, 10], np.uint64),
+          "committed": np.zeros(2, np.uint64), "stepped_down": np.zeros(2, np.uint8)}
+    tr = _tracker(off, cfg, st, track_next=False)
+    # learner (slot 3 of group 0) acks 10, voter slot 1 acks 7: commit = 7
+    # group 1: slots 1, 2 ack (incoming quorum 2 of 3 at >= 8), outgoing {3,4,5}
+    # (slots 2,3,4) has only slot 2 -> outgoing commit stays 0
+    recs = ([0, 0, 1, 1], [3, 1, 1, 2], [10, 7, 9, 8], [5, 5, 5, 5])
+    seq = {k: v.copy() for k, v in st.items()}
+    flags = np.array(recs[1], np.uint8)
+    oc.csr_appresp_sequential(off, cfg, (np.array(recs[0], np.uint32), flags,
+                                         np.array(recs[2], np.uint64),
+                                         np.array(recs[3], np.uint64)), seq)
+    tr.step(batch.AppRespBatch.from_numpy(*recs, device=DEV))
+    _compare(tr, seq, 2)
+    assert batch.as_u64(tr.committed).tolist() == [7, 0] == seq["committed"].tolist()
+    assert tr.active.cpu().numpy().view(np.uint16)[:2].tolist() == [0b1010, 0b0110]
+
+
+def test_csr_empty_config_never_commits():
+    """An empty config's CommittedIndex is MaxUint64 (majority.go:128-133),
+    past lastIndex: raftLog.maybeCommit never commits it (log.go:328-334)."""
+    off = np.array([0, 0, 2], np.uint32)
+    cfg = np.array([0, 0], np.uint32)          # group 1: two learners, no voters
+    st = {"match": np.array([3, 4], np.uint64), "active": np.zeros(2, np.uint16),
+          "term": np.array([2, 2], np.uint64), "term_start": np.array([0, 0], np.uint64),
+          "last_index": np.array([9, 9], np.uint64), "committed": np.zeros(2, np.uint64),
+          "stepped_down": np.zeros(2, np.uint8)}
+    tr = _tracker(off, cfg, st, track_next=False)
+    adv = torch.zeros(2, dtype=torch.uint8, device=DEV)
+    recs = ([0, 1, 1], [0, 1, 0], [5, 6, 7], [2, 2, 2])
+    tr.step(batch.AppRespBatch.from_numpy(*recs, device=DEV), adv)
+    assert batch.as_u64(tr.committed).tolist() == [0, 0]
+    assert adv.cpu().tolist() == [0, 0]
+    assert batch.as_u64(tr.match)[:2].tolist() == [7, 6]
+    assert tr.stats_dict()["non_member"] == 1    # group 0 has no Progress at all
+
+
+def test_csr_commit_table(tables):
+    """TestCommit (raft/raft_test.go:1127-1174) through the CSR step with an
+    empty batch, each case's voters followed by two learners holding the
+    largest matches (which must not move the commit)."""
+    cases = tables["TestCommit"]["cases"]
+    off, match, cfg, ts = [0], [], [], []
+    for c in cases:
+        n = len(c["matches"])
+        match += list(c["matches"]) + [1 << 40, 1 << 41]
+        off.append(off[-1] + n + 2)
+        cfg.append((1 << n) - 1)
+        same = [i for i, t in c["log"] if t == c["term"]]
+        ts.append(min(same) if same else MAX)
+    G = len(cases)
+    off, cfg = np.array(off, np.uint32), np.array(cfg, np.uint32)
+    st = {"match": np.array(match, np.uint64), "active": np.zeros(G, np.uint16),
+          "term": np.ones(G, np.uint64), "term_start": np.array(ts, np.uint64),
+          "committed": np.zeros(G, np.uint64), "stepped_down": np.zeros(G, np.uint8)}
+    tr = _tracker(off, cfg, st, track_next=False)
+    adv = torch.zeros(G, dtype=torch.uint8, device=DEV)
+    tr.commit_advance(adv)
+    assert batch.as_u64(tr.committed).tolist() == [c["want"] for c in cases]
+    assert adv.cpu().tolist() == [int(c["want"] > 0) for c in cases]
+
+
+def test_csr_stepdown_untouched_outside_flagged_chunks():
+    """stepdown_at is written only for the groups of chunks holding a
+    higher-term record (quorum_batch.h): other entries keep what the caller
+    left there."""
+    G = M = 70001
+    rng = np.random.default_rng(8)
+    off, cfg, sizes, st = _state(rng, "ragged", G)
+    tr = _tracker(off, cfg, st, track_next=False)
+    group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, stale=0.0)
+    hi = 12345                              # one higher-term record, group 12345
+    group[7], slot[7], term[7] = hi, 0, st["term"][hi] + np.uint64(3)
+    tr.stepdown_at.fill_(777)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    sd = tr.stepdown_at.cpu().numpy().view(np.uint32)
+    CH = 256 if tr.max_slots > 8 else 512
+    lo, hi_end = (hi // CH) * CH, min(G, (hi // CH + 1) * CH)
+    assert sd[hi] == 7
+    inside = np.arange(lo, hi_end)
+    assert np.all(sd[inside[inside != hi]] == 0xFFFFFFFF)
+    outside = np.ones(G, bool)
+    outside[lo:hi_end] = False
+    assert np.all(sd[outside] == 777)
+
+
+@pytest.mark.timeout(300)
+def test_csr_step_full_size_16m_ragged():
+    """16M ragged groups (configs[2] shape) with one MsgAppResp per group."""
+    G = 1 << 24
+    rng = np.random.default_rng(57)
+    off, cfg, sizes, st = _state(rng, "ragged", G)
+    st.pop("next")
+    tr = _tracker(off, cfg, st, track_next=False)
+    group, slot, index, term, rej, flags = _batch(rng, G, G, sizes, st, reject=0.0,
+                                                  higher=0.0001)
+    oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    assert np.array_equal(batch.as_u64(tr.match)[: st["match"].size], st["match"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))

@@ -14,6 +14,49 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+NONE = 0xFFFFFFFF
+
+
+def _slots(mask):
+    return {s for s in range(16) if (mask >> s) & 1}
+
+
+def sequential_votes(prevote, cfg, votes0, gterm, group, flags, term):
+    """The batch through one oracle Candidate per group, in batch order
+    (oracle/quorum_ref.py Candidate).  Returns (votes words, stepdown_at,
+    decided_at, stats[8]) as qb_dev_record_votes reports them."""
+    G = len(cfg)
+    cands = {}
+    sd = np.full(G, NONE, np.uint32)
+    dec = np.full(G, NONE, np.uint32)
+    stats = np.zeros(8, np.uint64)
+    for i in range(len(group)):
+        g = int(group[i])
+        if g >= G:
+            stats[q.STAT_BAD] += 1
+            continue
+        c = cands.get(g)
+        if c is None:
+            w = int(votes0[g])
+            vd, gr = w & 0xFFFF, (w >> 16) & w
+            pre = {j: bool((gr >> j) & 1) for j in range(16) if (vd >> j) & 1}
+            c = cands[g] = q.Candidate(prevote, int(gterm[g]), _slots(int(cfg[g]) & 0xFFFF),
+                                       _slots(int(cfg[g]) >> 16), pre)
+        was = c.decided
+        st = c.step(int(flags[i]) & 0x0F, bool(flags[i] & 0x80), int(term[i]))
+        stats[st] += 1
+        if st == q.STAT_HIGHER:
+            sd[g] = i
+        if c.decided and not was:
+            dec[g] = i
+    out = np.asarray(votes0, np.uint32).copy()
+    for g, c in cands.items():
+        vd = sum(1 << j for j in c.votes)
+        gr = sum(1 << j for j, v in c.votes.items() if v)
+        out[g] = vd | (gr << 16)
+    return out, sd, dec, stats
+
+
 def _run(prevote, G, M, seed, p_dup=0.3):
     rng = np.random.default_rng(seed)
     grp = batch.CsrGroups.synth(0x5EED0007, "joint" if seed % 2 else "ragged", G, device=DEV)
@@ -21,16 +64,14 @@ def _run(prevote, G, M, seed, p_dup=0.3):
     cfg = grp.cfg.cpu().numpy().view(np.uint32)
     # pre-batch votes: a few slots already voted
     votes0 = np.zeros(G, np.uint32)
-    pre = {}
     for g in range(G):
         s = int(off[g + 1] - off[g])
-        d = {}
+        vd = gr = 0
         for j in range(s):
             if rng.random() < 0.1:
-                d[j] = bool(rng.random() < 0.5)
-        pre[g] = d
-        vd = sum(1 << j for j in d)
-        gr = sum(1 << j for j, v in d.items() if v)
+                vd |= 1 << j
+                if rng.random() < 0.5:
+                    gr |= 1 << j
         votes0[g] = vd | (gr << 16)
     grp.votes.copy_(torch.from_numpy(votes0.view(np.int32)))
     gterm = rng.integers(3, 9, size=G).astype(np.uint64)
@@ -44,41 +85,26 @@ def _run(prevote, G, M, seed, p_dup=0.3):
             j = rng.integers(0, i)
             group[i], slot[i] = group[j], slot[j]
     reject = rng.random(M) < 0.4
-    dt = rng.choice([-1, 0, 0, 0, 0, 0, 1], size=M)
+    dt = rng.choice([-1, 0, 0, 0, 0, 0, 1, 2], size=M)
     term = np.where(group < G, gterm[gg].astype(np.int64) + dt, 5).astype(np.uint64)
     flags = (slot | (reject.astype(np.uint8) << 7)).astype(np.uint8)
 
-    # oracle
-    stats = np.zeros(6, np.int64)
-    down = np.zeros(G, bool)
-    first_down = np.full(G, 0xFFFFFFFF, np.uint32)
-    for i in range(M):
-        g = int(group[i])
-        if g >= G:
-            stats[q.STAT_BAD] += 1
-            continue
-        st, d = q.vote_response_sequential(prevote, int(gterm[g]), bool(down[g]), pre[g],
-                                           int(slot[i]), bool(reject[i]), int(term[i]))
-        if st == q.STAT_HIGHER and first_down[g] == 0xFFFFFFFF:
-            first_down[g] = i
-        down[g] = d
-        stats[st] += 1
-
+    want_votes, want_sd, want_dec, want_stats = sequential_votes(prevote, cfg, votes0, gterm,
+                                                                 group, flags, term)
     b = batch.AppRespBatch.from_numpy(group, slot, np.zeros(M, np.uint64), term, reject,
                                       device=DEV)
-    sd, gst = grp.record_votes(b, batch.from_u64(gterm, DEV), prevote=prevote)
-    got_votes = grp.votes.cpu().numpy().view(np.uint32)
-    for g in range(G):
-        d = pre[g]
-        vd = sum(1 << j for j in d)
-        gr = sum(1 << j for j, v in d.items() if v)
-        assert got_votes[g] == (vd | (gr << 16)), g
-    assert np.array_equal(sd.cpu().numpy().view(np.uint32), first_down)
-    assert gst.cpu().numpy()[:6].tolist() == stats.tolist()
+    sd, dec, gst = grp.record_votes(b, batch.from_u64(gterm, DEV), prevote=prevote)
+    assert np.array_equal(grp.votes.cpu().numpy().view(np.uint32), want_votes)
+    assert np.array_equal(sd.cpu().numpy().view(np.uint32), want_sd)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint32), want_dec)
+    assert gst.cpu().numpy().view(np.uint64).tolist() == want_stats.tolist()
+    assert int(want_stats[q.STAT_AFTER_DECISION]) > 0   # the workload decides mid-batch
     gr_, rj_, res = grp.tally_votes()
     gr_, rj_, res = gr_.cpu().numpy(), rj_.cpu().numpy(), res.cpu().numpy()
     for g in range(G):
-        eg, er, eres = q.tally_votes_slots(int(cfg[g]) & 0xFFFF, int(cfg[g]) >> 16, pre[g])
+        w = int(want_votes[g])
+        pre = {j: bool((w >> (16 + j)) & 1) for j in range(16) if (w >> j) & 1}
+        eg, er, eres = q.tally_votes_slots(int(cfg[g]) & 0xFFFF, int(cfg[g]) >> 16, pre)
         assert (gr_[g], rj_[g], res[g]) == (eg, er, eres), g
 
 
@@ -86,6 +112,63 @@ def _run(prevote, G, M, seed, p_dup=0.3):
 @pytest.mark.parametrize("G,M,seed", [(500, 3000, 1), (4000, 20000, 2), (50, 5000, 3)])
 def test_record_votes_vs_sequential(prevote, G, M, seed):
     _run(prevote, G, M, seed)
+
+
+def _one_group(prevote, recs, cfg=0b111, votes0=0b1 | (0b1 << 16), gterm=5):
+    """One 3-voter group (slot 0 = the candidate's own granted vote) and the
+    given (slot, reject, term) responses; device vs oracle."""
+    cfg_a = np.array([cfg], np.uint32)
+    cc = batch.compile_configs([{1, 2, 3}])
+    grp = batch.CsrGroups.from_compiled(cc, np.zeros(3, np.uint64), votes_u32=[votes0],
+                                        device=DEV)
+    grp.cfg.copy_(torch.from_numpy(cfg_a.view(np.int32)))
+    M = len(recs)
+    group = np.zeros(M, np.uint32)
+    flags = np.array([s | (0x80 if r else 0) for s, r, _ in recs], np.uint8)
+    term = np.array([t for _, _, t in recs], np.uint64)
+    want = sequential_votes(prevote, cfg_a, np.array([votes0], np.uint32),
+                            np.array([gterm], np.uint64), group, flags, term)
+    b = batch.AppRespBatch.from_numpy(group, flags & 0x0F, np.zeros(M, np.uint64), term,
+                                      flags >> 7, device=DEV)
+    sd, dec, st = grp.record_votes(b, batch.from_u64([gterm], DEV), prevote=prevote)
+    got = (grp.votes.cpu().numpy().view(np.uint32), sd.cpu().numpy().view(np.uint32),
+           dec.cpu().numpy().view(np.uint32), st.cpu().numpy().view(np.uint64))
+    for a, b_ in zip(got, want):
+        assert np.array_equal(a, b_)
+    return want
+
+
+def test_prevote_won_mid_batch_then_responses_follow():
+    """a pre-candidate wins at the first response and campaigns at
+    term + 1; a later rejection at term + 1 is stale for the new candidate
+    (ignored, no step-down), a later granted response is not recorded, and
+    only a rejection above term + 1 makes it step down."""
+    votes, sd, dec, st = _one_group(True, [(1, False, 6), (2, True, 6), (2, False, 6),
+                                           (1, True, 7)])
+    assert dec[0] == 0 and sd[0] == 3
+    assert votes[0] == 0b011 | (0b011 << 16)   # slot 2's responses came after the decision
+    assert st[q.STAT_AFTER_DECISION] == 2 and st[q.STAT_HIGHER] == 1
+    # the same batch with the last rejection at term + 1 only: no step-down
+    _, sd, dec, _ = _one_group(True, [(1, False, 6), (2, True, 6), (1, True, 6)])
+    assert dec[0] == 0 and sd[0] == NONE
+
+
+def test_vote_lost_mid_batch_then_same_term_ignored():
+    """A candidate that loses becomes a follower at its term: later responses
+    at the term are ignored; one above it still changes the term."""
+    votes, sd, dec, st = _one_group(False, [(1, True, 5), (2, True, 5), (1, False, 5),
+                                            (2, False, 6)], votes0=0)
+    assert dec[0] == 1 and sd[0] == 3
+    assert votes[0] == 0b110                    # slots 1 and 2 rejected, slot 0 never voted
+    assert st[q.STAT_AFTER_DECISION] == 1
+
+
+def test_already_decided_before_batch():
+    """Votes that already decide (a Won tally before the batch): the first
+    polled response, even a duplicate, is the decision (poll -> TallyVotes)."""
+    votes, sd, dec, st = _one_group(False, [(0, False, 5), (1, False, 5)],
+                                    votes0=0b011 | (0b011 << 16))
+    assert dec[0] == 0 and st[q.STAT_DUPLICATE] == 1 and st[q.STAT_AFTER_DECISION] == 1
 
 
 def test_election_table_through_record_votes(tables):
