@@ -310,3 +310,42 @@ def test_full_size_fixed_1m_and_ragged_16m():
     assert np.array_equal(batch.as_u64(c), ec)
     vv = v.cpu().numpy()
     assert np.array_equal(vv, ev) and set(np.unique(vv)) <= {1, 2, 3}
+
+
+@pytest.mark.timeout(300)
+def test_full_size_joint_8m():
+    """BASELINE configs[3] at its full per-GPU size: 8M JointConfig 5+5
+    groups (overlap 0-5; 64M over 8 GPUs) vs the multithreaded C oracle, plus
+    the joint identities of joint.go:49-75 checked size-independently:
+    CommittedIndex of the joint config <= either half's alone."""
+    G = 1 << 23
+    grp = batch.CsrGroups.synth(0x5EED0004, "joint", G)
+    c, v = grp.committed_vote()
+    off, m, cfg, votes = oc.gen_csr(0x5EED0004, "joint", G)
+    ec, ev = oc.csr_eval(off, m, cfg, votes, threads=16)
+    cu = batch.as_u64(c)
+    assert np.array_equal(cu, ec) and np.array_equal(v.cpu().numpy(), ev)
+    # the incoming half alone (mask_out cleared) never commits less
+    inc = batch.CsrGroups(grp.off, grp.cfg & 0xFFFF, grp.match, grp.votes, max_slots=grp.max_slots)
+    ci, _ = inc.committed_vote()
+    assert (batch.as_u64(ci) >= cu).all()
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 7, 9, 11])
+def test_bench_test_go_distribution(n):
+    """BASELINE configs[0]'s inputs (raft/quorum/bench_test.go:24-40): voter
+    IDs 1..n, Match = rand.Int63n(MaxInt64) — uniform over [0, 2^63 - 1) —
+    through the FIXED kernel (slot j = ID j+1, MajorityConfig.Slice order) for
+    1M groups, vs the C oracle; and the single config the Go benchmark loops
+    over, through the Go-API mirror (MajorityConfig + mapAckIndexer)."""
+    G = 1 << 20
+    rng = np.random.default_rng(n)
+    match = rng.integers(0, (1 << 63) - 1, size=(n, G), dtype=np.uint64)
+    fg = batch.FixedGroups(n, G, DEV, match=batch.from_u64(match, DEV).view(n, G))
+    c, _ = fg.committed_vote(want_vote=False)
+    ec, _ = oc.fixed_eval(n, match, np.zeros(G, np.uint8 if n <= 8 else np.uint16),
+                          np.zeros(G, np.uint8 if n <= 8 else np.uint16))
+    assert np.array_equal(batch.as_u64(c), ec)
+    cfg = quorum.MajorityConfig(range(1, n + 1))
+    acked = {i + 1: int(match[i, 0]) for i in range(n)}
+    assert cfg.CommittedIndex(quorum.MapAckIndexer(acked)) == int(ec[0])

@@ -1,0 +1,146 @@
+"""The N > 1 path with the HIP kernels in the loop: two gloo ranks (both on
+cuda:0 — the box has one GPU) each evaluate their shard_range of the
+counter-generated groups with the device kernels, then assemble the node-wide
+result (etcd_amd.shard.allgather_results) or deliver a record batch to the
+owning shard (route_records) before the device tracker step; rank 0 compares
+with the single-process C oracle over all groups, bit for bit.  gloo moves
+host tensors, so the collectives run on the .cpu() copies (the driver's
+multi-GPU bench runs the same calls over RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from etcd_amd.shard import shard_range
+
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED0003
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    return out
+
+
+def _eval_worker(rank, world, port, q, total, kind):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.quorum import batch
+        from etcd_amd.shard import allgather_results
+        dev = torch.device("cuda", 0)
+        b, e = shard_range(total, world, rank)
+        if kind == "fixed":
+            grp = batch.FixedGroups.synth(SEED, 5, e - b, g_begin=b, device=dev)
+        else:
+            grp = batch.CsrGroups.synth(SEED, kind, e - b, g_begin=b, device=dev)
+        c, v = grp.committed_vote()
+        gc, gv = allgather_results(c.cpu(), v.cpu(), total)
+        if rank == 0:
+            q.put((gc.numpy().view(np.uint64).copy(), gv.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,total,kind", [(2, 100003, "fixed"), (2, 50001, "ragged"),
+                                              (3, 30000, "joint")])
+def test_sharded_device_eval_allgather(world, total, kind):
+    from tests import oracle_c as oc
+    gc, gv = _spawn(_eval_worker, world, total, kind)
+    if kind == "fixed":
+        match, vd, gr, _ = oc.gen_fixed(SEED, 5, total)
+        ec, ev = oc.fixed_eval(5, match, vd, gr)
+    else:
+        off, m, cfg, votes = oc.gen_csr(SEED, kind, total)
+        ec, ev = oc.csr_eval(off, m, cfg, votes)
+    assert np.array_equal(gc, ec) and np.array_equal(gv, ev)
+
+
+def _batch_of(rank, total, M, last):
+    """Records arriving at ``rank``: global group numbers over every shard."""
+    rng = np.random.default_rng(500 + rank)
+    grp = rng.integers(0, total, M).astype(np.uint32)
+    slot = rng.integers(1, 5, M).astype(np.uint8)
+    idx = last[grp] - rng.integers(0, 64, M).astype(np.uint64)
+    term = np.where(rng.random(M) < 0.02, 6, np.where(rng.random(M) < 0.002, 8, 7))
+    return grp, slot, idx, term.astype(np.uint64)
+
+
+def _tracker_worker(rank, world, port, q, total, M):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.quorum import batch
+        from etcd_amd.shard import allgather_results, route_records
+        from tests import oracle_c as oc
+        dev = torch.device("cuda", 0)
+        b, e = shard_range(total, world, rank)
+        full, _, _, ts_full = oc.gen_fixed(SEED, 5, total)
+        grp, slot, idx, term = _batch_of(rank, total, M, full[0])
+        out = route_records({"group": torch.from_numpy(grp.view(np.int32)),
+                             "flags": torch.from_numpy(slot),
+                             "index": torch.from_numpy(idx.view(np.int64)),
+                             "term": torch.from_numpy(term.view(np.int64))}, total)
+        # this shard's leader state, regenerated from the counter-based spec
+        match, _, _, ts = oc.gen_fixed(SEED, 5, e - b, g_begin=b)
+        tr = batch.FixedTracker(5, e - b, dev)
+        tr.match.copy_(batch.from_u64(match, dev))
+        tr.term_start.copy_(batch.from_u64(ts, dev))
+        tr.term.fill_(7)
+        tr.commit_advance()
+        tr.step(batch.AppRespBatch(out["group"].to(dev), out["flags"].to(dev),
+                                   out["index"].to(dev), out["term"].to(dev)))
+        rows = [allgather_results(tr.match[s].cpu(), tr.active[: e - b].to(torch.uint8).cpu(),
+                                  total)[0] for s in range(5)]
+        cm, sd = allgather_results(tr.committed.cpu(),
+                                   tr.stepped_down().to(torch.uint8).cpu(), total)
+        if rank == 0:
+            q.put((np.stack([r.numpy().view(np.uint64) for r in rows]).copy(),
+                   cm.numpy().view(np.uint64).copy(), sd.numpy().astype(bool)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_routed_records_device_tracker_step(world):
+    """Batches arriving at every rank are routed to the owning shards
+    (route_records, stable in (source rank, position) order) and applied by
+    the bucketed device step there; the node-wide state equals the
+    sequential oracle over the concatenated batches on all groups."""
+    from tests import oracle_c as oc
+    total, M = 60001, 50000
+    match, cm, sd = _spawn(_tracker_worker, world, total, M)
+    full, _, _, ts = oc.gen_fixed(SEED, 5, total)
+    st = {"match": full.copy(), "active": np.zeros(total, np.uint16),
+          "term": np.full(total, 7, np.uint64), "term_start": ts,
+          "committed": np.zeros(total, np.uint64), "stepped_down": np.zeros(total, np.uint8)}
+    oc.commit_all(5, st["match"], ts, st["committed"])
+    for r in range(world):   # the global batch order route_records preserves per group
+        grp, slot, idx, term = _batch_of(r, total, M, full[0])
+        oc.appresp_sequential(5, total, (grp, slot, idx, term), st)
+    assert np.array_equal(match, st["match"])
+    assert np.array_equal(cm, st["committed"])
+    assert np.array_equal(sd, st["stepped_down"].astype(bool))

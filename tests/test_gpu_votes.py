@@ -98,7 +98,8 @@ def _run(prevote, G, M, seed, p_dup=0.3):
     assert np.array_equal(sd.cpu().numpy().view(np.uint32), want_sd)
     assert np.array_equal(dec.cpu().numpy().view(np.uint32), want_dec)
     assert gst.cpu().numpy().view(np.uint64).tolist() == want_stats.tolist()
-    assert int(want_stats[q.STAT_AFTER_DECISION]) > 0   # the workload decides mid-batch
+    if M <= 10 * G:  # sparse per-group streams decide before they step down
+        assert int(want_stats[q.STAT_AFTER_DECISION]) > 0
     gr_, rj_, res = grp.tally_votes()
     gr_, rj_, res = gr_.cpu().numpy(), rj_.cpu().numpy(), res.cpu().numpy()
     for g in range(G):
