@@ -286,6 +286,8 @@ def tracker_main(args, world, rank, dev):
             r = torch.randint(0, 1 << 30, group.shape, generator=g_, device=dev)
             return 1 + r % (s_g - 1)
         slots_mean = float(sizes.float().mean())
+        vm = (tr.cfg & 0xFFFF) | ((tr.cfg >> 16) & 0xFFFF)
+        voters_mean = float(sum(((vm >> b) & 1).sum().item() for b in range(16))) / G
     else:
         tr = batch.FixedTracker(n, G, dev)
         fg = batch.FixedGroups.synth(TRACKER_SEED, n, G, g_begin=rank * G, device=dev,
@@ -297,7 +299,7 @@ def tracker_main(args, world, rank, dev):
 
         def slots(group, g_):
             return torch.randint(1, n, group.shape, generator=g_, device=dev)
-        slots_mean = float(n)
+        slots_mean = voters_mean = float(n)
     tr.term.fill_(7)
     tr.commit_advance()
     batches = tracker_batches(G, nb, last, slots, gen, dev)
@@ -370,11 +372,12 @@ def tracker_main(args, world, rank, dev):
         route_ms = (time.perf_counter() - tr_) / 5 * 1e3
     if rank != 0:
         return
-    bpg = TRACKER_BYTES if not csr else None
+    bpg = TRACKER_BYTES
     if csr:
-        # record 21 + match RMW 16 + commit advance: off 8, cfg 4, match 8 s,
-        # term_start 8, committed 8 read + committed 8 written
-        bpg = 21 + 16 + 8 + 4 + 8 * slots_mean + 8 + 8 + 8
+        # record 21 + match RMW 16 + commit advance: off 4, cfg 4, the voters'
+        # match 8 each (learners ack but do not count), term_start 8,
+        # committed 8 read + 8 written
+        bpg = 21 + 16 + 4 + 4 + 8 * voters_mean + 8 + 8 + 8
     key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
     achieved = bpg * G / step_s / 1e9
     kern = ("k_bk_hist, k_scan_local, k_bk_sums_parts, k_bk_scatter, k_bk_split, "
@@ -393,6 +396,7 @@ def tracker_main(args, world, rank, dev):
                                    else ", 5 voters")),
                    "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
                    "stale_term_fraction": 0.01, "mean_slots": slots_mean,
+                   "mean_voters": voters_mean,
                    "parallelism": f"groups sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key),

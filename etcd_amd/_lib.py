@@ -56,6 +56,7 @@ SIGNATURES = {
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_validate": (_i32, [_u64, _u32, _p, _p, _p]),
+    "qb_dev_csr_committed_vote_checked": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_wide_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p]),
     "qb_dev_wide_validate": (_i32, [_u64, _u32, _p, _p, _p]),
     "qb_dev_csr_quorum_active": (_i32, [_u64, _p, _p, _p, _p]),
@@ -105,7 +106,10 @@ def load() -> C.CDLL:
                 f"{LIB_PATH} not built: run `make -C etcd_amd/csrc` (or "
                 "__graft_entry__.build()); there is no CPU fallback")
         lib = C.CDLL(LIB_PATH)
+        lab = bool(os.environ.get("QB_LIB_PATH"))  # an A/B build may predate newer symbols
         for name, (res, args) in SIGNATURES.items():
+            if lab and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -39,7 +39,18 @@ __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
 
-__host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
+// Groups per K5 chunk (one workgroup; its LDS holds n accumulators per group).
+#ifndef QB_CH_NARROW
+#define QB_CH_NARROW 512
+#endif
+#ifndef QB_CH_WIDE
+#define QB_CH_WIDE 256
+#endif
+__host__ __device__ constexpr u32 chunk_groups(u32 n) {
+  return n <= 8 ? u32(QB_CH_NARROW) : u32(QB_CH_WIDE);
+}
+// CSR chunks: the LDS run buffer holds CH * WMAX slots.
+__host__ __device__ constexpr u32 csr_chunk_groups(u32 wmax) { return wmax <= 8 ? 512u : 256u; }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
 // with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles
@@ -60,17 +71,26 @@ struct Geometry {
   u64 G, M;
   u32 n, CH, NC, NSB, NT;
   u32 xcd;  // tiles of K1/K3 mapped XCD-major (see xcd_major)
+  // CH and CH * kChunksPerSb are powers of two: group -> chunk / super-bucket
+  // by shifts (a runtime u32 division is ~30 VALU instructions per record)
+  u32 ch_shift, sb_shift;
+  __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
+  __host__ __device__ u32 sb_of(u32 g) const { return g >> sb_shift; }
   __host__ __device__ u64 nbins() const { return u64(NSB) * NT; }
   u32 tile_grid() const { return xcd ? (NT + kXcds - 1) / kXcds * kXcds : NT; }
   __device__ __forceinline__ u32 tile() const { return xcd ? xcd_major() : blockIdx.x; }
 };
 
-inline Geometry geometry(u32 n, u64 G, u64 M) {
+inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0) {
   Geometry g{};
   g.G = G;
   g.M = M;
   g.n = n;
-  g.CH = chunk_groups(n);
+  g.CH = ch ? ch : chunk_groups(n);
+  g.ch_shift = 0;
+  while ((1u << g.ch_shift) < g.CH) ++g.ch_shift;
+  g.sb_shift = g.ch_shift + 7;
+  static_assert(kChunksPerSb == 128, "sb_shift = ch_shift + log2(kChunksPerSb)");
   g.NC = u32((G + g.CH - 1) / g.CH);
   g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
   g.NT = u32((M + kTile - 1) / kTile);

@@ -29,7 +29,7 @@ namespace qb {
 namespace cc {
 
 constexpr int kBlk = 128;
-constexpr int kTab = 24;  // working table: 16 old slots + up to 8 new IDs
+constexpr int kTab = 24;  // working table: old slots + new IDs alive at once
 
 // A thread's working table, column-major in the workgroup's LDS block
 // (entry k of thread t at [k][t]): the lanes of a wave touch consecutive
@@ -161,8 +161,20 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
     if (typ == QB_CC_ADD_NODE || typ == QB_CC_ADD_LEARNER) {
       if (!has_pr) {  // initProgress
         if (x < 0) {
-          if (r.n >= kTab) return QB_CCERR_TOO_MANY_SLOTS;
-          x = r.n++;
+          if (r.n < kTab) {
+            x = r.n++;
+          } else {
+            // Reuse an entry this change list freed (an ID it added and then
+            // removed: no Progress, no role left).  Entries below n_old keep
+            // their index (the carry of old slots maps by it), so only new
+            // ones are candidates; the engine limit is then 24 IDs alive at
+            // once within the list, not 24 seen over the whole list.
+            for (int k = *n_old; k < r.n && x < 0; ++k)
+              if (!((r.prs >> k) & 1u)) x = k;
+            if (x < 0) return QB_CCERR_TOO_MANY_SLOTS;
+            const u32 b = ~(1u << x);
+            r.in &= b, r.out &= b, r.lnext &= b, r.lrn &= b, r.islrn &= b, r.fresh &= b;
+          }
           t.id(x) = id;
         }
         const u32 b = 1u << x;

@@ -1133,10 +1133,9 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   hipError_t e = hipMemsetAsync(pool, 0, c.shards - c.pool + sizeof(u64) * QB_LSTAT_COUNT * 64, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
   u64* bshards = nullptr;
-  // QB_LEADER_GROUPING=atomic selects the per-record-atomic grouping even
-  // when the bucket geometry fits (test knob: both paths are checked).
-  const char* grouping = getenv("QB_LEADER_GROUPING");
-  const bool force_atomic = grouping && grouping[0] == 'a';
+  // QB_LEADER_OPT_ATOMIC_GROUPING selects the per-record-atomic grouping
+  // even when the bucket geometry fits (both paths are tested).
+  const bool force_atomic = (lg->options & QB_LEADER_OPT_ATOMIC_GROUPING) != 0;
   if (c.bucketed && !force_atomic) {
     char* bws = ws + c.bkt;
     bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);

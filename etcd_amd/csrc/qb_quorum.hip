@@ -350,3 +350,27 @@ extern "C" int qb_dev_csr_validate(uint64_t G, uint32_t max_slots, const uint32_
   QB_CHECK_LAUNCH("k_csr_validate");
   return QB_OK;
 }
+
+extern "C" int qb_dev_csr_committed_vote_checked(uint64_t G, uint32_t max_slots,
+                                                 const uint32_t* off, const uint64_t* match,
+                                                 const uint32_t* cfg, const uint32_t* votes,
+                                                 uint64_t* commit_out, uint8_t* vote_out,
+                                                 uint64_t* bad_scratch, void* stream) {
+  if (G == 0 || (!commit_out && !vote_out)) return QB_OK;
+  QB_REQUIRE(off && bad_scratch, "off/bad_scratch NULL");
+  hipStream_t st = as_stream(stream);
+  hipError_t e = hipMemsetAsync(bad_scratch, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bad)");
+  {
+    const int rc = qb_dev_csr_validate(G, max_slots, off, bad_scratch, stream);
+    if (rc != QB_OK) return rc;
+  }
+  uint64_t bad = 0;
+  e = hipMemcpyAsync(&bad, bad_scratch, sizeof bad, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "validate readback");
+  QB_REQUIRE(bad == 0, "%llu group(s) break the CSR bound (off[0] == 0, 0 <= s_g <= %u)",
+             (unsigned long long)bad, max_slots == 0 ? unsigned(QB_MAX_SLOTS) : max_slots);
+  return qb_dev_csr_committed_vote(G, max_slots, off, match, cfg, votes, commit_out, vote_out,
+                                   stream);
+}

@@ -30,6 +30,7 @@
 #include "qb_bucket.h"
 #include "qb_tracker_slow.h"
 
+
 namespace qb {
 namespace bk {
 
@@ -48,7 +49,6 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
   for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) lh[b] = 0;
   __syncthreads();
   const u64 t0 = u64(tile) * kTile;
-  const u32 sbgroups = geo.CH * kChunksPerSb;
   // The tile's group / flag loads are all issued before the first LDS
   // atomic (a load -> use loop waited one HBM round trip per iteration).
   constexpr int kHistPer = kTile / kBlock;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __r
     const u32 g = gg[k];
     const bool in = (valid >> k) & 1u, bad = in && g >= geo.G;
     const bool non = in && !bad && (ff[k] & 0x0Fu) >= geo.n;
-    if (in && !bad && !non) atomicAdd(&lh[g / sbgroups], 1u);
+    if (in && !bad && !non) atomicAdd(&lh[geo.sb_of(g)], 1u);
     nbad += wave_popc(bad);
     nnon += wave_popc(non);
   }
@@ -254,14 +254,13 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
     gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
   }
   __syncthreads();
-  const u32 sbgroups = geo.CH * kChunksPerSb;
   if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
     u64 bins = 0, ranks = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       u32 b = kNoBin, r = 0;
       if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
-        b = g[j] / sbgroups;
+        b = geo.sb_of(g[j]);
         r = atomicAdd(&start[b], 1u);
       }
       bins |= u64(b) << (16 * j);
@@ -276,7 +275,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
       if (k >= nrec) continue;
       u16 b = kNoBin;
       if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
-        b = u16(g[j] / sbgroups);
+        b = u16(geo.sb_of(g[j]));
         L.rank[k] = u16(atomicAdd(&start[b], 1u));
       }
       L.bin[k] = b;
@@ -298,8 +297,8 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
       } else if (col == 1) {
         v[j] = vt[j];
       } else {
-        const u32 chunk = g[j] / geo.CH;
-        const u32 meta = (g[j] - chunk * geo.CH) | ((chunk % kChunksPerSb) << 10) |
+        const u32 chunk = geo.chunk_of(g[j]);
+        const u32 meta = (g[j] & (geo.CH - 1u)) | ((chunk % kChunksPerSb) << 10) |
                          ((f[j] & 0xFFu) << 17);
         v[j] = u64(meta) | (u64(out.packed ? term_to32(vt[j]) : u32(t0 + k)) << 32);
       }

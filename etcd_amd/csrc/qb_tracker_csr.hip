@@ -39,7 +39,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
     u16* __restrict__ active, u64* __restrict__ committed, u32* __restrict__ stepdown_at,
     u8* __restrict__ advanced, u8* __restrict__ chunk_slow, u32* __restrict__ any_slow,
     u64* __restrict__ shards) {
-  constexpr u32 CH = chunk_groups(WMAX);
+  constexpr u32 CH = csr_chunk_groups(WMAX);
   constexpr u32 GPT = CH / kBlock;     // groups per thread in the commit phase
   constexpr u32 CAP = CH * WMAX;       // slot-run capacity
   constexpr u32 PER = CAP / kBlock;    // run slots per thread
@@ -241,7 +241,8 @@ u32 csr_wmax(uint32_t max_slots) {
 
 extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
   if (max_slots > QB_MAX_SLOTS) return 0;
-  return bk::carve(bk::geometry(csr_wmax(max_slots), G, M), 2).total;
+  const u32 w = csr_wmax(max_slots);
+  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w)), 2).total;
 }
 
 extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
@@ -265,7 +266,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const u32 wmax = csr_wmax(max_slots);
   // the bucketing filters slot >= the table bound (geo.n) as non-member; the
   // chunk size follows the LDS run capacity (chunk_groups(wmax))
-  bk::Geometry geo = bk::geometry(wmax, G, M);
+  bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax));
   geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
   const bk::Carve cv = bk::carve(geo, 2);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,

@@ -60,7 +60,7 @@ constexpr unsigned kSlowBlockMax = 256;
 
 __device__ __forceinline__ bool in_slow_chunk(const Geometry& geo, u32 g, u32 f,
                                               const u8* __restrict__ chunk_slow) {
-  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[g / geo.CH];
+  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[geo.chunk_of(g)];
 }
 
 // Tracker state layouts.  FIXED: n voters, slot-major rows of G (every slot
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
   // whole waves iterate together (CsrLay::ci is wave-cooperative)
   for (u64 g0 = u64(blockIdx.x) * kBlock; g0 < geo.G; g0 += stride) {
     const u64 g = g0 + threadIdx.x;
-    const bool mine = g < geo.G && chunk_slow[g / geo.CH];
+    const bool mine = g < geo.G && chunk_slow[geo.chunk_of(u32(g))];
     if (__ballot(mine) == 0) continue;
     const u64 ci = lay.ci(match, mine ? u32(g) : u32(g0));
     if (!mine) continue;

@@ -317,15 +317,23 @@ class CsrGroups:
         smax = int(np.diff(off_h.astype(np.int64)).max()) if G else 0
         return cls(off, cfg, match, votes, max_slots=smax)
 
-    def committed_vote(self, commit_out=None, vote_out=None, want_commit=True, want_vote=True):
+    def committed_vote(self, commit_out=None, vote_out=None, want_commit=True, want_vote=True,
+                       validate: bool = False):
+        """JointConfig.CommittedIndex / VoteResult for every group.  validate:
+        check the table first (qb_dev_csr_committed_vote_checked; synchronises)
+        and raise QuorumBatchError on a table breaking its max_slots bound."""
         if want_commit and commit_out is None:
             commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
         if want_vote and vote_out is None:
             vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
-        _lib.call("qb_dev_csr_committed_vote", self.G, self.max_slots, _ptr(self.off),
-                  _ptr(self.match),
-                  _ptr(self.cfg), _ptr(self.votes), _ptr(commit_out if want_commit else None),
-                  _ptr(vote_out if want_vote else None), _stream(self.device))
+        args = (self.G, self.max_slots, _ptr(self.off), _ptr(self.match), _ptr(self.cfg),
+                _ptr(self.votes), _ptr(commit_out if want_commit else None),
+                _ptr(vote_out if want_vote else None))
+        if validate:
+            bad = torch.empty(1, dtype=torch.int64, device=self.device)
+            _lib.call("qb_dev_csr_committed_vote_checked", *args, _ptr(bad), _stream(self.device))
+        else:
+            _lib.call("qb_dev_csr_committed_vote", *args, _stream(self.device))
         return (commit_out if want_commit else None), (vote_out if want_vote else None)
 
     def committed_index(self) -> torch.Tensor:

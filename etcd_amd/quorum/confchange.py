@@ -28,7 +28,7 @@ ERR_MESSAGES = {
     10: "{} is in LearnersNext, but is already marked as learner",
     11: "{} is in Learners and Voters[1]", 12: "{} is in Learners and Voters[0]",
     13: "{} is in Learners, but is not marked as learner",
-    14: "AutoLeave must be false when not joint", 15: "more than 16 members (engine limit)",
+    14: "AutoLeave must be false when not joint", 15: "more than 16 members, or 24 alive within one change (engine limit)",
     16: "bad operation",
 }
 

@@ -47,7 +47,7 @@ _P = C.c_void_p
 class LeaderGroupsC(C.Structure):
     """struct qb_leader_groups (include/quorum_batch.h)."""
     _fields_ = [("G", C.c_uint64), ("inflight_cap", C.c_uint32), ("readq_cap", C.c_uint32),
-                ("read_only", C.c_uint32), ("reserved", C.c_uint32)] + [
+                ("read_only", C.c_uint32), ("options", C.c_uint32)] + [
         (n, _P) for n in ("off", "cfg", "meta", "term", "committed", "first_index", "last_index",
                           "snap_index", "snap_term", "max_ents", "run_start", "run_term", "match",
                           "next", "pending_snapshot", "pstate", "infl_pos", "infl_buf", "rq_ctx",
@@ -141,6 +141,7 @@ class LeaderGroups:
         self.G = len(arrays["cfg"])
         self.S = int(arrays["off"][-1])
         self.inflight_cap, self.readq_cap, self.read_only = inflight_cap, readq_cap, read_only
+        self.options = 0  # QB_LEADER_OPT_* (diagnostic switches)
         self.t = {k: _to_dev(arrays[k], dt, self.device) for k, dt in GROUP_ARRAYS.items()}
         self._ws = None
 
@@ -157,7 +158,7 @@ class LeaderGroups:
 
     def _struct(self) -> LeaderGroupsC:
         s = LeaderGroupsC(G=self.G, inflight_cap=self.inflight_cap, readq_cap=self.readq_cap,
-                          read_only=self.read_only, reserved=0)
+                          read_only=self.read_only, options=self.options)
         for k in GROUP_ARRAYS:
             setattr(s, k, self.t[k].data_ptr())
         return s

@@ -183,7 +183,8 @@ int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_t* match,
  * max_slots bounds every s_g of the table (0 = QB_MAX_SLOTS); it sizes the
  * kernel (LDS and networks), so pass the table's true bound: a group above it
  * gives an unspecified (never out-of-bounds) result, which
- * qb_dev_csr_validate detects. */
+ * qb_dev_csr_validate detects (qb_dev_csr_committed_vote_checked: validate,
+ * then QB_EINVAL instead of a result). */
 int qb_dev_csr_committed_vote(uint64_t G, uint32_t max_slots,
                               const uint32_t* off, const uint64_t* match,
                               const uint32_t* cfg, const uint32_t* votes,
@@ -195,6 +196,17 @@ int qb_dev_csr_committed_vote(uint64_t G, uint32_t max_slots,
  * uint64). */
 int qb_dev_csr_validate(uint64_t G, uint32_t max_slots, const uint32_t* off,
                         uint64_t* bad_out, void* stream);
+
+/* qb_dev_csr_committed_vote behind an opt-in validation: the table is checked
+ * first (qb_dev_csr_validate into bad_scratch, one device uint64) and a table
+ * breaking its bound returns QB_EINVAL — with the count in qb_last_error() —
+ * and computes nothing.  It reads the verdict back, so it synchronises the
+ * stream: a debug / once-per-config-change form, not the per-tick call. */
+int qb_dev_csr_committed_vote_checked(uint64_t G, uint32_t max_slots,
+                                      const uint32_t* off, const uint64_t* match,
+                                      const uint32_t* cfg, const uint32_t* votes,
+                                      uint64_t* commit_out, uint8_t* vote_out,
+                                      uint64_t* bad_scratch, void* stream);
 
 /* CommittedIndex and/or VoteResult for G WIDE groups (JointConfig
  * semantics as qb_dev_csr_committed_vote, quorum/joint.go:49-75 over
@@ -406,6 +418,11 @@ int qb_dev_csr_tally_votes(uint64_t G, const uint32_t* cfg,
  * (raft.pendingReadIndexMessages). */
 #define QB_META_PENDING_READINDEX (1u << 25)
 
+/* Diagnostic switch: group the records with per-record global atomics (the
+ * path used beyond the bucket geometry, > 134M groups per shard) even where
+ * the LDS bucketing applies; results are identical, only slower. */
+#define QB_LEADER_OPT_ATOMIC_GROUPING 1u
+
 #define QB_READ_ONLY_SAFE 0
 #define QB_READ_ONLY_LEASE_BASED 1
 
@@ -439,7 +456,7 @@ typedef struct qb_leader_groups {
   uint32_t inflight_cap; /* MaxInflightMsgs: ring size per slot, 1..4096  */
   uint32_t readq_cap;    /* pending ReadIndex slots per group, 0..16      */
   uint32_t read_only;    /* QB_READ_ONLY_SAFE / QB_READ_ONLY_LEASE_BASED  */
-  uint32_t reserved;
+  uint32_t options;      /* QB_LEADER_OPT_* (0 = defaults)                */
   /* configuration, CSR as qb_dev_csr_committed_vote */
   const uint32_t* off;   /* [G+1] */
   const uint32_t* cfg;   /* [G] mask_in | mask_out << 16 */
@@ -581,7 +598,7 @@ enum {
   QB_CCERR_LEARNER_INCOMING = 12,   /* "%d is in Learners and Voters[0]"                */
   QB_CCERR_LEARNER_NOT_MARKED = 13, /* "%d is in Learners, but is not marked as learner" */
   QB_CCERR_AUTOLEAVE_NOT_JOINT = 14, /* "AutoLeave must be false when not joint"        */
-  QB_CCERR_TOO_MANY_SLOTS = 15,     /* engine limit: more than QB_MAX_SLOTS members     */
+  QB_CCERR_TOO_MANY_SLOTS = 15,     /* engine limit: > QB_MAX_SLOTS members, or > 24 IDs alive at once within one change list */
   QB_CCERR_BAD_OP = 16              /* op is not a QB_CC_* operation                     */
 };
 

@@ -85,7 +85,7 @@ def test_random_sequences(seed):
         for g in range(G):
             nt, e = CP.oracle_apply(orc[g], op[g], ccs[g], last[g])
             if e is None and sum(1 for _ in nt.prs) > 16:
-                e = "more than 16 members (engine limit)"
+                e = "more than 16 members, or 24 alive within one change (engine limit)"
                 nt = orc[g]
             got_e = error_text(int(err[g]), int(err_id[g])) if err[g] else None
             assert got_e == e, (seed, step, g, op[g], ccs[g], got_e, e)
@@ -103,6 +103,37 @@ def test_random_sequences(seed):
         table = ConfigTable.from_numpy(a["off"], a["ids"], a["cfg"], a["ext"],
                                        {k: a[k] for k in ("match", "next", "pending_snapshot",
                                                           "pstate", "infl_pos", "infl_buf")}, 7)
+
+
+def test_churn_within_one_change_list():
+    """a Simple change that adds and removes more than 8 learners in
+    one list (the final config keeps its 5 voters) is legal in the reference;
+    the device reuses the freed table entries instead of failing with the
+    engine's slot limit.  Voters 1..5 are added one Simple change at a time
+    first (each changes one voter)."""
+    from etcd_amd.quorum.confchange import error_text
+    G = 64
+    orc = [CC.Tracker.empty(4) for _ in range(G)]
+    table = _table(orc, K=4)
+    plans = [[(CC.ADD_NODE, v)] for v in range(1, 6)]
+    churn = []
+    for k in range(12):                       # 12 learners in and out again
+        churn += [(CC.ADD_LEARNER, 100 + k), (CC.REMOVE_NODE, 100 + k)]
+    plans.append(churn + [(CC.ADD_LEARNER, 200)])
+    # 6 members + 19 new learners alive at once: past the 24-entry table
+    plans.append([(CC.ADD_LEARNER, 300 + k) for k in range(19)])
+    for step, ccs in enumerate(plans):
+        table, err, err_id = table.change([1] * G, [ccs] * G, [50 + step] * G)
+        dev = CP.unpack(table.numpy(), 4)
+        for g in range(G):
+            nt, e = CP.oracle_apply(orc[g], 1, ccs, 50 + step)
+            got_e = error_text(int(err[g]), int(err_id[g])) if err[g] else None
+            if step < len(plans) - 1:
+                assert got_e == e is None, (step, got_e, e)
+                assert _render(dev[g]) == _render(nt), step
+                orc[g] = nt
+            else:   # the reference accepts 25 members; the engine reports its limit
+                assert e is None and got_e is not None and "engine limit" in got_e
 
 
 def test_restore_batch():

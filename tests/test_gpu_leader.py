@@ -69,13 +69,14 @@ def test_reference_scenarios_on_device(sc):
 
 
 def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_groups=0,
-          hot_frac=0.0, term_base=0):
+          hot_frac=0.0, term_base=0, options=0):
     rng = np.random.default_rng(seed)
     groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots, term_base)
     for g in groups:
         g.read_only = read_only
     recs = LP.random_records(rng, groups, M, hot_groups=hot_groups, hot_frac=hot_frac)
     eng = _engine(groups, inflight_cap, readq_cap, read_only)
+    eng.options = options
     res = eng.step(_inbox(recs))
     orc = copy.deepcopy(groups)
     for g in orc:
@@ -133,11 +134,11 @@ def test_fuzz_crowded_chunk():
     _fuzz(42, G=300, M=5000, inflight_cap=6, readq_cap=3, hot_groups=3, hot_frac=0.5)
 
 
-def test_fuzz_atomic_grouping(monkeypatch):
+def test_fuzz_atomic_grouping():
     """The grouping used beyond the bucket geometry (> 134M groups per
-    shard): per-record global atomics, then the same gather and step."""
-    monkeypatch.setenv("QB_LEADER_GROUPING", "atomic")
-    _fuzz(31, G=3000, M=9000, inflight_cap=6, readq_cap=3, max_slots=16)
+    shard): per-record global atomics, then the same gather and step
+    (QB_LEADER_OPT_ATOMIC_GROUPING)."""
+    _fuzz(31, G=3000, M=9000, inflight_cap=6, readq_cap=3, max_slots=16, options=1)
 
 
 def test_empty_batch_and_truncated_output():

@@ -149,6 +149,24 @@ def test_csr_validate_flags_bad_tables():
     assert grp.max_slots == 5 and grp.validate() == 0 and grp.validate(max_slots=4) == 1
 
 
+def test_csr_checked_call_rejects_bad_tables():
+    """The opt-in validation (qb_dev_csr_committed_vote_checked): a table
+    breaking its max_slots bound is QB_EINVAL with nothing computed; a good
+    table gives the unchecked call's results."""
+    off = np.array([0, 3, 8, 12], np.uint32)
+    cc = batch.CompiledConfigs(off, np.array([7, 31, 15], np.uint32), np.zeros(12, np.uint64))
+    vals = np.arange(1, 13, dtype=np.uint64)
+    grp = batch.CsrGroups.from_compiled(cc, vals, device=DEV)
+    c_ok, v_ok = grp.committed_vote()
+    c_chk, v_chk = grp.committed_vote(validate=True)
+    assert torch.equal(c_ok, c_chk) and torch.equal(v_ok, v_chk)
+    grp.max_slots = 4                          # group 1 has 5 slots
+    out = torch.full((3,), 7, dtype=torch.int64, device=DEV)
+    with pytest.raises(_lib.QuorumBatchError, match="1 group"):
+        grp.committed_vote(commit_out=out, want_vote=False, validate=True)
+    assert out.cpu().tolist() == [7, 7, 7]
+
+
 @pytest.mark.parametrize("max_slots", [4, 8, 12, 16])
 def test_csr_every_kernel_width_bound(max_slots):
     """Each WMAX instantiation (LDS run buffer + widest network) is exact for

@@ -197,3 +197,35 @@ def test_c_ingest_matches_python_restatement():
                int(out["index"][i]), int(out["term"][i]), int(out["hint"][i]),
                int(out["log_term"][i]))
         assert got == tuple(want[:7]), (i, b.hex())
+
+
+def _crc32c(data: bytes) -> int:
+    """CRC-32 with the Castagnoli polynomial (reflected 0x82F63B78), as Go's
+    crc32.MakeTable(crc32.Castagnoli) + crc32.Checksum."""
+    crc = 0xFFFFFFFF
+    for byte in data:
+        crc ^= byte
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def test_wire_primitives_pinned_by_reference_bytes(monkeypatch):
+    """The only protobuf-encoded bytes the reference holds as a fixture are a
+    walpb.Record (server/storage/wal/record_test.go:29-30, decoded by the
+    test to Record{Type: 1, Crc: crc32c(infoData), Data: infoData}, :43).
+    walpb is gogoproto like raftpb, so this pins the restated decoder's
+    primitives — multi-byte varints and length-delimited fields — on
+    reference-held bytes; no reference fixture holds raftpb.Message bytes, so
+    Message-level wire parity stays unpinned."""
+    from oracle import raftpb_ref as R
+    monkeypatch.setitem(R.SCHEMAS, "walpb.Record", {1: "v", 2: "v", 3: "b"})
+    info = b"\b\xef\xfd\x02"
+    record = b"\x0e\x00\x00\x00\x00\x00\x00\x00\b\x01\x10\x99\xb5\xe4\xd0\x03\x1a\x04" + info
+    body = record[8:]            # the 8-byte frame length precedes the protobuf (decoder.go)
+    got = R.unmarshal("walpb.Record", body)
+    assert got == {1: 1, 2: _crc32c(info), 3: info}
+    # truncations the reference test expects to fail with io.ErrUnexpectedEOF (:46-47)
+    for cut in (len(body) - len(info), len(body) - 1):
+        with pytest.raises(R.WireError):
+            R.unmarshal("walpb.Record", body[:cut])

@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 bash tools/lab/ab_tracker.sh 3 tracker base shift ch1024 > gpurun_out/r2_ab2.log 2>&1
+echo rc=$?

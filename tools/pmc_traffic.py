@@ -42,22 +42,30 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--kernel", default="k_fixed")
+    ap.add_argument("--kernel", default="k_fixed",
+                    help="kernel name substring; a comma-separated list sums the medians of "
+                         "every listed kernel (a multi-kernel step, one dispatch of each per step)")
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--key", required=True)
     ap.add_argument("--algo-bytes", type=float, required=True, help="algorithmic bytes/launch")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    f = per_dispatch(a.fetch, a.kernel, "FETCH_SIZE")[a.warmup:a.warmup + a.steps]
-    w = per_dispatch(a.write, a.kernel, "WRITE_SIZE")[a.warmup:a.warmup + a.steps]
-    if not f or not w:
-        raise SystemExit("no matching dispatches")
-    fk, wk = float(np.median(f)), float(np.median(w))
+    fk = wk = 0.0
+    per = {}
+    for kern in a.kernel.split(","):
+        f = per_dispatch(a.fetch, kern, "FETCH_SIZE")[a.warmup:a.warmup + a.steps]
+        w = per_dispatch(a.write, kern, "WRITE_SIZE")[a.warmup:a.warmup + a.steps]
+        if not f or not w:
+            raise SystemExit(f"no matching dispatches for {kern}")
+        per[kern] = {"read_bytes_corrected": 2.0 * float(np.median(f)) * 1024.0,
+                     "write_bytes": float(np.median(w)) * 1024.0}
+        fk += float(np.median(f))
+        wk += float(np.median(w))
     read_b = 2.0 * fk * 1024.0   # gfx950 FETCH_SIZE x2 correction
     write_b = wk * 1024.0
     rec = {
-        "kernel": a.kernel, "dispatches": len(f),
+        "kernel": a.kernel, "dispatches": len(f), "per_kernel": per,
         "fetch_size_kib_median_raw": fk, "write_size_kib_median": wk,
         "read_bytes_corrected": read_b, "write_bytes": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
