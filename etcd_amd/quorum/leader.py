@@ -133,6 +133,8 @@ class LeaderStepResult:
 class LeaderGroups:
     """Leader state of G groups resident on one device."""
 
+    options = 0  # QB_LEADER_OPT_* (diagnostic switches)
+
     def __init__(self, arrays: Dict[str, np.ndarray], inflight_cap: int, readq_cap: int = 0,
                  read_only: int = READ_ONLY_SAFE, device="cuda"):
         self.device = torch.device(device)
@@ -141,7 +143,6 @@ class LeaderGroups:
         self.G = len(arrays["cfg"])
         self.S = int(arrays["off"][-1])
         self.inflight_cap, self.readq_cap, self.read_only = inflight_cap, readq_cap, read_only
-        self.options = 0  # QB_LEADER_OPT_* (diagnostic switches)
         self.t = {k: _to_dev(arrays[k], dt, self.device) for k, dt in GROUP_ARRAYS.items()}
         self._ws = None
 
