@@ -120,14 +120,16 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   // part table: pfirst[NSB+1], part_sb[max_parts], nparts
   c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
   c.chunk_start = o;  o += up256(sizeof(u32) * max_parts(g) * (kChunksPerSb + 1));
-  c.buf1 = o;  o += ncols * up256(sizeof(u64) * g.M);
-  c.buf2 = o;  o += ncols * up256(sizeof(u64) * g.M);
+  // (columns of at least one record: K5's branch-free loads read record 0 of
+  // an empty chunk)
+  c.buf1 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
+  c.buf2 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
   c.total = o;
   return c;
 }
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
-  const size_t col = up256(sizeof(u64) * M);
+  const size_t col = up256(sizeof(u64) * (M ? M : 1));
   if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, 0};
   if (ncols == 2)
     return Cols{reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u64*>(base + col), nullptr,

@@ -520,7 +520,10 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   // The commit phase's loads (match rows, committed, term_start) are issued
   // now, so their latency overlaps the record pass instead of following it.
+  // (RecentActive's read-modify-write reads its word here too, not after
+  // the record pass)
   u64 v[GPT][N], cm[GPT], ts[GPT];
+  u32 av[GPT];
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
     const u32 lg = threadIdx.x + k * kBlock;
@@ -530,6 +533,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     for (int s = 0; s < N; ++s) v[k][s] = live ? match[u64(s) * geo.G + g] : 0ull;
     cm[k] = live ? committed[g] : 0ull;
     ts[k] = live ? term_start[g] : 0ull;
+    av[k] = live ? active[g] : 0u;
   }
   for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
     acc_m[k] = 0;
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     const bool adv = ci > cm[k] && ci >= ts[k];  // log.go:328-334
     if (adv) committed[g] = ci;
     if (advanced) advanced[g] = adv ? 1 : 0;
-    if (act[lg]) active[g] = u16(active[g] | act[lg]);
+    if (act[lg]) active[g] = u16(av[k] | act[lg]);
   }
   const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
   tally.flush(tl, shard_of(shards), slot);

@@ -55,93 +55,138 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   const u32 c = blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
-  // commit-phase inputs of this thread's groups, issued first
-  u64 cm[GPT], ts[GPT];
-  u32 cf[GPT];
+  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
+  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  // Load order as in k_bk_apply: (1) slot offsets, group terms and the run
+  // table; (2) the first record batch, then the old slot run and the commit
+  // inputs, whose latency runs under the record pass; (3) write-back.  Loads
+  // are branch-free (clamped addresses): the compiler's wait counts stay exact
+  // only in straight-line code.
+  // offsets and group terms into registers first, the run table's loads
+  // beside them: one round trip, not three
+  constexpr u32 OPT = (CH + kBlock) / kBlock;  // CH + 1 offsets
+  u32 ofr[OPT];
+  u64 gtr[GPT];
 #pragma unroll
-  for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * kBlock;
-    const bool live = lg < ng;
-    cm[k] = live ? committed[g0 + lg] : 0ull;
-    ts[k] = live ? term_start[g0 + lg] : 0ull;
-    cf[k] = live ? cfg[g0 + lg] : 0u;
+  for (u32 q = 0; q < OPT; ++q) {
+    const u32 k = threadIdx.x + q * kBlock;
+    ofr[q] = off[g0 + (k < ng ? k : ng)];
   }
-  for (u32 k = threadIdx.x; k <= CH; k += kBlock) offs[k] = off[g0 + (k < ng ? k : ng)];
-  for (u32 k = threadIdx.x; k < CH; k += kBlock) {
-    gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
-    act[k] = 0;
-  }
-  if (threadIdx.x == 0) slow = 0;
-  __syncthreads();
-  const u32 a0 = offs[0], run = offs[CH] - a0;
-  // A table breaking its max_slots bound cannot stage its run in LDS: the
-  // chunk takes the slow path (exact per-record semantics, global atomics).
-  const bool fits = run <= CAP;
-  u64 old[PER];
 #pragma unroll
-  for (u32 p = 0; p < PER; ++p) {
-    const u32 j = threadIdx.x + p * kBlock;
-    old[p] = (fits && j < run) ? match[a0 + j] : 0ull;
+  for (u32 q = 0; q < GPT; ++q) {
+    const u32 k = threadIdx.x + q * kBlock;
+    gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
   for (u32 k = threadIdx.x; k < CAP; k += kBlock) {
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
   }
-  if (!fits && threadIdx.x == 0) slow = 1;
-  // the chunk's records: one short run per part of its super-bucket
-  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
-  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  if (threadIdx.x == 0) slow = 0;
+  u32 total = rtab.build(cs, p0, p1, cl);  // synchronises
+#pragma unroll
+  for (u32 q = 0; q < OPT; ++q) {
+    const u32 k = threadIdx.x + q * kBlock;
+    if (k <= CH) offs[k] = ofr[q];
+  }
+#pragma unroll
+  for (u32 q = 0; q < GPT; ++q) {
+    gterm[threadIdx.x + q * kBlock] = gtr[q];
+    act[threadIdx.x + q * kBlock] = 0;
+  }
+  __syncthreads();
+  const u32 a0 = offs[0], run = offs[CH] - a0;
+  // A table breaking its max_slots bound cannot stage its run in LDS: the
+  // chunk takes the slow path (exact per-record semantics, global atomics).
+  const bool fits = run <= CAP;
   constexpr int kRecPer = 4;
-  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
-    const u32 total = rtab.build(cs, pb, p1, cl);  // synchronises (acc zeroed, offs ready)
-    for (u32 f0 = 0; f0 < total; f0 += kBlock * kRecPer) {
-      u64 rmr[kRecPer], rix[kRecPer];
+  u64 rmr[kRecPer], rix[kRecPer];
+  auto load = [&](u32 f0, u32 n) {
+    u32 ix[kRecPer];
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
-        rmr[r] = 0;
-        rix[r] = 0;
-        if (f < total) {
-          const u32 i = rtab.locate(f);
-          rmr[r] = recs.mr[i];
-          rix[r] = recs.index[i];
-        }
-      }
+    for (int r = 0; r < kRecPer; ++r) {
+      const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+      ix[r] = n ? rtab.locate(f < n ? f : n - 1) : 0u;
+    }
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
-        bool stale = false, applied = false, rejected = false, non = false;
-        if (f < total && fits) {
-          const u64 mr = rmr[r];
-          const u32 t32 = u32(mr >> 32), meta = u32(mr);
-          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
-          const u32 base = offs[lg] - a0, sg = offs[lg + 1] - offs[lg];
-          const u64 gt = gterm[lg];
-          if (s >= sg) {
-            non = true;                                     // no Progress: raft.go:1100-1104
-          } else if (t32 == kTermEscape || u64(t32) > gt) {
-            slow = 1;  // higher term (step-down order) or ambiguous compare
-          } else if (u64(t32) < gt) {
-            stale = true;                                   // raft.go:883-921
+    for (int r = 0; r < kRecPer; ++r) {
+      rmr[r] = recs.mr[ix[r]];
+      rix[r] = recs.index[ix[r]];
+    }
+  };
+  auto apply = [&](u32 f0, u32 n) {
+#pragma unroll
+    for (int r = 0; r < kRecPer; ++r) {
+      const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+      bool stale = false, applied = false, rejected = false, non = false;
+      if (f < n && fits) {
+        const u64 mr = rmr[r];
+        const u32 t32 = u32(mr >> 32), meta = u32(mr);
+        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+        const u32 base = offs[lg] - a0, sg = offs[lg + 1] - offs[lg];
+        const u64 gt = gterm[lg];
+        if (s >= sg) {
+          non = true;                                     // no Progress: raft.go:1100-1104
+        } else if (t32 == kTermEscape || u64(t32) > gt) {
+          slow = 1;  // higher term (step-down order) or ambiguous compare
+        } else if (u64(t32) < gt) {
+          stale = true;                                   // raft.go:883-921
+        } else {
+          atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+          if (meta & (1u << 24)) {  // QB_REC_REJECT
+            rejected = true;                              // raft.go:1109: not MaybeUpdate
           } else {
-            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-            if (meta & (1u << 24)) {  // QB_REC_REJECT
-              rejected = true;                              // raft.go:1109: not MaybeUpdate
-            } else {
-              applied = true;
-              const u64 idx = rix[r];
-              atomicMax(&acc[base + s], idx);               // progress.go:146-150
-              if constexpr (NEXT) atomicMax(&accn[base + s], idx + 1ull);  // :151
-            }
+            applied = true;
+            const u64 idx = rix[r];
+            atomicMax(&acc[base + s], idx);               // progress.go:146-150
+            if constexpr (NEXT) atomicMax(&accn[base + s], idx + 1ull);  // :151
           }
         }
-        tally.add(0, stale);
-        tally.add(1, applied);
-        tally.add(2, rejected);
-        tally.add(3, non);
       }
+      tally.add(0, stale);
+      tally.add(1, applied);
+      tally.add(2, rejected);
+      tally.add(3, non);
     }
+  };
+  load(0, total);
+  // the old slot run (slots past the run re-read its last slot) and the
+  // commit-phase inputs of this thread's groups
+  // (an oversize run stays in HBM: its lanes re-read the first slot; an
+  // empty run has no slot to read and reads the chunk's first group term
+  // instead — a select, not a branch, which would cost the exact wait counts)
+  u64 old[PER];
+  const u64* src = run ? match + a0 : group_term + g0;
+  const u32 last = run && fits ? run - 1u : 0u;
+#pragma unroll
+  for (u32 p = 0; p < PER; ++p) {
+    const u32 j = threadIdx.x + p * kBlock;
+    old[p] = src[j < last ? j : last];
   }
+  u64 cm[GPT], ts[GPT];
+  u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * kBlock;
+    const u64 g = g0 + (lg < ng ? lg : ng - 1);
+    cm[k] = committed[g];
+    ts[k] = term_start[g];
+    cf[k] = cfg[g];
+    av[k] = active[g];
+  }
+#pragma unroll
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+  apply(0, total);
+  for (u32 pb = p0, f0 = kBlock * kRecPer;;) {
+    for (; f0 < total; f0 += kBlock * kRecPer) {
+      load(f0, total);
+      apply(f0, total);
+    }
+    pb += RunTable::kRuns;
+    if (pb >= p1) break;
+    total = rtab.build(cs, pb, p1, cl);
+    f0 = 0;
+  }
+  if (!fits && threadIdx.x == 0) slow = 1;
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
     for (u32 lg = threadIdx.x; lg < ng; lg += kBlock) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
@@ -191,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
     const bool adv = ci != kInf && ci > cm[k] && ci >= ts[k];
     if (adv) committed[g] = ci;
     if (advanced) advanced[g] = adv ? 1 : 0;
-    if (act[lg]) active[g] = u16(active[g] | act[lg]);
+    if (act[lg]) active[g] = u16(av[k] | act[lg]);
   }
   const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
   tally.flush(tl, shard_of(shards), slot);
