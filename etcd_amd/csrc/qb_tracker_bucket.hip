@@ -499,15 +499,24 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 // batch in batch order (the exact two-pass form of qb_tracker.hip).
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
 // act[CH] u32.
+// K5 threads per workgroup (QB_K5_BLOCK, at most the chunk's group count).
+#ifndef QB_K5_BLOCK
+#define QB_K5_BLOCK 256
+#endif
+__host__ __device__ constexpr u32 k5_block(int n) {
+  return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
+}
+
 template <int N, bool NEXT>
-__global__ __launch_bounds__(kBlock) void k_bk_apply(
+__global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
     u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards) {
   constexpr u32 CH = chunk_groups(N);
-  constexpr u32 GPT = CH / kBlock;  // groups per thread in the commit phase
+  constexpr u32 B = k5_block(N);
+  constexpr u32 GPT = CH / B;  // groups per thread in the commit phase
   __shared__ u32 tl[3];
   BlockTally<3> tally;
   __shared__ u64 acc_m[N * CH];
@@ -526,7 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   u32 av[GPT];
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * kBlock;
+    const u32 lg = threadIdx.x + k * B;
     const u64 g = g0 + lg;
     const bool live = lg < ng;
 #pragma unroll
@@ -535,11 +544,11 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
     ts[k] = live ? term_start[g] : 0ull;
     av[k] = live ? active[g] : 0u;
   }
-  for (u32 k = threadIdx.x; k < N * CH; k += kBlock) {
+  for (u32 k = threadIdx.x; k < N * CH; k += B) {
     acc_m[k] = 0;
     if constexpr (NEXT) acc_n[k] = 0;
   }
-  for (u32 k = threadIdx.x; k < CH; k += kBlock) {
+  for (u32 k = threadIdx.x; k < CH; k += B) {
     gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
     act[k] = 0;
   }
@@ -551,14 +560,14 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
   __shared__ RunTable rt;
-  constexpr int kRecPer = 4;
+  constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
   for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
     const u32 total = rt.build(cs, pb, p1, cl);
-    for (u32 f0 = 0; f0 < total; f0 += kBlock * kRecPer) {
+    for (u32 f0 = 0; f0 < total; f0 += B * kRecPer) {
       u64 rmr[kRecPer], rix[kRecPer];
 #pragma unroll
       for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        const u32 f = f0 + u32(r) * B + threadIdx.x;
         rmr[r] = 0;
         rix[r] = 0;
         if (f < total) {
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
       }
 #pragma unroll
       for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+        const u32 f = f0 + u32(r) * B + threadIdx.x;
         bool stale = false, applied = false, rejected = false;
         if (f < total) {
           const u64 mr = rmr[r];
@@ -605,7 +614,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
 #pragma unroll
     for (u32 k = 0; k < GPT; ++k) {
-      const u32 lg = threadIdx.x + k * kBlock;
+      const u32 lg = threadIdx.x + k * B;
       if (lg < ng) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
     }
     if (threadIdx.x == 0) {
@@ -618,7 +627,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_apply(
   // maybeCommit for every group of the chunk + write-back (coalesced rows).
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * kBlock;
+    const u32 lg = threadIdx.x + k * B;
     if (lg >= ng) continue;
     const u64 g = g0 + lg;
 #pragma unroll
@@ -660,11 +669,11 @@ template <int N>
 void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                   const ApplyArgs& a, hipStream_t st) {
   if (a.next)
-    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
+    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
                        cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
   else
-    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
+    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
                        cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
 }

@@ -267,7 +267,31 @@ __device__ __forceinline__ bool fast_prefix(const Src& s, u64& i, const u64 l, F
   QB_FAST_VARINT(0x58, f.hint)
 #undef QB_FAST_VARINT
   (void)ignored;
+  // context (field 12, bytes) of the common 8-byte form: what the generic
+  // loop does for key 0x62 with a one-byte length 8 inside the message
+  if (i + 10 <= l && s.at(i) == 0x62 && s.at(i + 1) == 0x08) {
+    f.has_ctx = true;
+    f.ctx_pos = i + 2;
+    f.ctx_len = 8;
+    i += 10;
+  }
   return true;
+}
+
+// The 8 bytes at i as a big-endian u64 (the read context's request id).
+template <class Src>
+__device__ __forceinline__ u64 load_be64(const Src& s, u64 i) {
+  u64 v = 0;
+  for (u32 t = 0; t < 8; ++t) v = (v << 8) | s.at(i + t);
+  return v;
+}
+template <>
+__device__ __forceinline__ u64 load_be64<LdsSrc>(const LdsSrc& s, u64 i) {
+  const u64 off = i - s.base;
+  const u64* w = reinterpret_cast<const u64*>(s.lds) + (off >> 3);
+  const u32 sh = u32(off & 7u) * 8u;
+  const u64 lo = w[0], hi = w[1];
+  return __builtin_bswap64(sh ? (lo >> sh) | (hi << (64u - sh)) : lo);
 }
 
 template <class Src>
@@ -303,27 +327,38 @@ struct Args {
   u64* stats;
 };
 
+// The group row of one message, loaded ahead of the parse: the slot range
+// (off) and the first kIdBatch member IDs (wider configs continue one by one
+// after the parse).  Loads are branch-free — clamped rows, and an empty row
+// reads a harmless word of moff — so their wait lands where the IDs are
+// compared, after the parse, not ahead of it.
+constexpr u32 kIdBatch = 8;
+struct GroupRow {
+  u32 mg, s0, s1;
+  u64 id[kIdBatch];
+};
+
 // One message: decode, classify, map From to its slot, write the record.
 template <class Src>
-__device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u64 p0, u64 p1) {
-  // The group's slot range is loaded first: its latency (a random row of
-  // off) overlaps the parse instead of following it.
-  const u32 mg = A.mgroup[m];
-  u32 s0 = 0, s1 = 0;
-  if (mg < A.G) {
-    s0 = A.off[mg];
-    s1 = A.off[mg + 1];
-  }
+__device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u64 p0, u64 p1,
+                                          GroupRow& row) {
   Fields f;
   int st_;
   u32 group = 0xFFFFFFFFu;
   u8 flags = 0;
   u64 index = 0, term = 0, hint = 0, lterm = 0;
+#ifdef QB_WIRE_LAB_NOPARSE  // development: the kernel without the decoder
+  f = Fields{};
+  f.type = 4;
+  f.from = u64(s.at(p0 + 5)) + 16384u;
+  if (p1 < p0 || p1 > A.nbytes) {
+#else
   if (p1 < p0 || p1 > A.nbytes || !unmarshal_message(s, p0, p1, f)) {
+#endif
     st_ = QB_WIRE_UNMARSHAL;
-    if (A.mtype) A.mtype[m] = 0;
+    if (A.mtype) __builtin_nontemporal_store(u8(0), A.mtype + m);
   } else {
-    if (A.mtype) A.mtype[m] = u8(f.type);
+    if (A.mtype) __builtin_nontemporal_store(u8(f.type), A.mtype + m);
     const int kind = kind_of_type(f.type);
     if (kind < 0) {
       st_ = QB_WIRE_TYPE;
@@ -333,29 +368,21 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
       if (kind == QB_IN_HEARTBEAT_RESP) {
         index = 0;
         if (f.has_ctx && f.ctx_len != 0) {
-          u64 v = 0;
-          if (f.ctx_len == 8)
-            for (u32 t = 0; t < 8; ++t) v = (v << 8) | s.at(f.ctx_pos + t);  // big-endian id
+          const u64 v = f.ctx_len == 8 ? load_be64(s, f.ctx_pos) : 0ull;  // big-endian id
           if (f.ctx_len != 8 || v == 0) st_ = QB_WIRE_CTX;
           index = v;
         }
       }
       if (st_ == QB_WIRE_OK) {
-        group = mg;
+        group = row.mg;
         u32 slot = QB_REC_NO_PROGRESS;
         if (group < A.G) {
-          // The first kIdBatch IDs are loaded together (one round trip),
-          // wider configs continue one by one.
-          constexpr u32 kIdBatch = 8;
-          const u32 n = s1 - s0;
-          u64 id[kIdBatch];
-#pragma unroll
-          for (u32 k = 0; k < kIdBatch; ++k) id[k] = k < n ? A.ids[s0 + k] : 0ull;
+          const u32 n = row.s1 - row.s0;
 #pragma unroll
           for (u32 k = kIdBatch; k-- > 0;)
-            if (k < n && id[k] == f.from) slot = k;
-          for (u32 j = s0 + kIdBatch; j < s1 && slot == QB_REC_NO_PROGRESS; ++j)
-            if (A.ids[j] == f.from) slot = j - s0;
+            if (k < n && row.id[k] == f.from) slot = k;
+          for (u32 j = row.s0 + kIdBatch; j < row.s1 && slot == QB_REC_NO_PROGRESS; ++j)
+            if (A.ids[j] == f.from) slot = j - row.s0;
         }
         flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
         term = f.term;
@@ -366,16 +393,22 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
       }
     }
   }
-  A.rg[m] = group;
-  A.rf[m] = flags;
-  A.ri[m] = index;
-  A.rt[m] = term;
-  if (A.rh) A.rh[m] = hint;
-  if (A.rl) A.rl[m] = lterm;
-  A.status[m] = u8(st_);
+  // The record columns are written once and read by a later launch: stored
+  // nontemporal, so the stream does not evict the group rows (off, ids) that
+  // every message gathers at random from the Infinity Cache.
+  __builtin_nontemporal_store(group, A.rg + m);
+  __builtin_nontemporal_store(flags, A.rf + m);
+  __builtin_nontemporal_store(index, A.ri + m);
+  __builtin_nontemporal_store(term, A.rt + m);
+  if (A.rh) __builtin_nontemporal_store(hint, A.rh + m);
+  if (A.rl) __builtin_nontemporal_store(lterm, A.rl + m);
+  __builtin_nontemporal_store(u8(st_), A.status + m);
   return st_;
 }
 
+// Round trips per workgroup: (1) the message offsets and groups; (2) the
+// groups' slot ranges beside the LDS-DMA stage of the byte span; (3) the
+// member IDs, in flight while the messages are parsed from LDS.
 __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   __shared__ __attribute__((aligned(16))) u8 stage[kStage + 16];  // + window over-read
   __shared__ u32 lds[4];
@@ -383,8 +416,20 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   const u64 m0 = u64(blockIdx.x) * kBlock;
   const u64 m = m0 + threadIdx.x;
   const u64 mlast = (m0 + kBlock < A.M ? m0 + kBlock : A.M);
-  // Stage the block's byte span [b0, b1) when it fits (block-uniform).
+  const u64 mc = m < A.M ? m : A.M - 1;  // lanes past M re-read the last message
   const u64 b0 = A.moff[m0], b1 = A.moff[mlast];
+  const u64 p0 = __builtin_nontemporal_load(A.moff + mc);
+  const u64 p1 = __builtin_nontemporal_load(A.moff + mc + 1);
+  GroupRow row;
+  row.mg = __builtin_nontemporal_load(A.mgroup + mc);
+  {
+    // G == 0: off may be absent; read the first word of moff (>= 2 entries)
+    const u32* offp = A.G ? A.off : reinterpret_cast<const u32*>(A.moff);
+    const u32 gi = row.mg < A.G ? row.mg : 0u;
+    row.s0 = offp[gi];
+    row.s1 = offp[gi + 1];
+  }
+  // Stage the block's byte span [b0, b1) when it fits (block-uniform).
   u64 lbase = 0, lend = 0;  // staged span (empty: nothing staged)
   if (b1 > b0 && b1 - b0 <= kStage - 16) {
     const u64 a0 = b0 & ~u64(15);             // 16-byte aligned window
@@ -411,13 +456,18 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     lend = a1 < A.nbytes ? a1 : A.nbytes;
   }
   __syncthreads();
+  {
+    const u32 n = row.mg < A.G ? row.s1 - row.s0 : 0u;
+    const u64* idp = n ? A.ids + row.s0 : A.moff;
+#pragma unroll
+    for (u32 k = 0; k < kIdBatch; ++k) row.id[k] = idp[n ? (k < n ? k : n - 1) : 0u];
+  }
   int st_ = -1;
   if (m < A.M) {
-    const u64 p0 = A.moff[m], p1 = A.moff[m + 1];
     if (p0 >= lbase && p1 <= lend && p0 <= p1)
-      st_ = ingest_one(A, LdsSrc{stage, lbase}, m, p0, p1);
+      st_ = ingest_one(A, LdsSrc{stage, lbase}, m, p0, p1, row);
     else
-      st_ = ingest_one(A, GlobalSrc{A.bytes}, m, p0, p1);
+      st_ = ingest_one(A, GlobalSrc{A.bytes}, m, p0, p1, row);
   }
   tally.add(0, st_ == QB_WIRE_OK);
   tally.add(1, st_ == QB_WIRE_UNMARSHAL);

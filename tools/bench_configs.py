@@ -312,12 +312,13 @@ def leader_config(G, reps, warm=4, shuffle=True):
                                        "C restatement of stepLeader (oracle/leader_oracle.c)"}})
 
 
-def wire_config(M, reps):
+def wire_config(M, reps, G=None):
     """§8f row 3: wire ingest of M gogoproto-encoded responses (MsgAppResp +
-    10% MsgHeartbeatResp with read contexts) to M/4 5-voter leaders."""
+    10% MsgHeartbeatResp with read contexts) to M/4 5-voter leaders (G given:
+    a development variant with a small, cache-resident group table)."""
     from etcd_amd.quorum import wire
     from tests import oracle_c as oc
-    G = M // 4
+    G = G or M // 4
     buf, moff, grp, off, ids = wire.synth_response_stream(M, G)
     d_buf = torch.from_numpy(buf).to(dev)
     d_moff = torch.from_numpy(moff.view(np.int64)).to(dev)
@@ -330,6 +331,10 @@ def wire_config(M, reps):
     # slot IDs 40 (5 x u64, read once per message); written: group 4, flags
     # 1, index/term/hint/log_term 32, status 1, type 1
     algo = nb + M * (8 + 4 + 40) + M * (4 + 1 + 32 + 1 + 1)
+    if GPU_ONLY:
+        print(json.dumps({"config": "wire ingest", "per_launch_us": t * 1e6,
+                          "messages_per_s": M / t, "frac": algo / t / 8e12}), flush=True)
+        return
     import time
     Ms = 1 << 22
     cpu = {}
@@ -383,6 +388,10 @@ def confchange_config(G, reps):
     # 6 x (29 + K*8), err 1, err_id 8
     pr = 29 + 8 * K
     algo = G * (4 + 40 + 8 + 1 + 4 + 9 + 8 + 5 * pr + 4 + 48 + 8 + 6 * pr + 9)
+    if GPU_ONLY:
+        print(json.dumps({"config": "conf change", "per_launch_us": tt * 1e6,
+                          "groups_per_s": G / tt, "frac": algo / tt / 8e12}), flush=True)
+        return
     n = 20000
     trs = []
     for _ in range(n):
@@ -464,7 +473,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="3,4,5")
-    ap.add_argument("--gpu-only", action="store_true", help="leader: skip the CPU baseline (A/B)")
+    ap.add_argument("--gpu-only", action="store_true",
+                    help="leader, wire, confchange: skip the CPU baseline (A/B)")
     a = ap.parse_args()
     global GPU_ONLY
     GPU_ONLY = a.gpu_only
@@ -483,6 +493,8 @@ def main():
         leader_config(1 << 22, a.reps, shuffle=False)
     if "wire" in which:
         wire_config(1 << 24, a.reps)
+    if "wire-g4k" in which:  # development: 4096 groups (group rows cache-resident)
+        wire_config(1 << 24, a.reps, G=4096)
     if "readindex" in which:
         readindex_config(1 << 22, a.reps)
     if "confchange" in which:
