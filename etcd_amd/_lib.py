@@ -83,6 +83,10 @@ SIGNATURES = {
     "qb_comm_destroy": (_i32, [_p]),
     "qb_allgather_workspace_bytes": (C.c_size_t, [_u64, _i32]),
     "qb_dev_allgather_results": (_i32, [_p, _u64, _p, _p, _p, _p, _p, C.c_size_t, _p]),
+    "qb_route_partition_workspace_bytes": (C.c_size_t, [_i32, _u64]),
+    "qb_dev_route_partition": (_i32, [_u64, _i32, _u64] + [_p] * 13 + [C.c_size_t, _p]),
+    "qb_route_workspace_bytes": (C.c_size_t, [_i32, _u64]),
+    "qb_dev_route_records": (_i32, [_p, _u64, _u64] + [_p] * 12 + [_u64, _p, _p, C.c_size_t, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),
     "qb_host_synth_csr_offsets": (_i32, [_u64, _u64, _u64, _p]),
     "qb_host_synth_joint_offsets": (_i32, [_u64, _u64, _u64, _p]),

@@ -13,6 +13,7 @@
 
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "qb_common.h"
 
@@ -157,6 +158,126 @@ extern "C" int qb_dev_allgather_results(qb_comm* c, uint64_t total,
         h = hipMemcpyAsync(vote_all + rb, recv_v + uint64_t(r) * cap, re - rb,
                            hipMemcpyDeviceToDevice, st);
       if (h != hipSuccess) return qb::hip_fail(h, "hipMemcpyAsync(compact)");
+    }
+  }
+  return QB_OK;
+}
+
+// ------------------------------------------------------------- routing ---
+// qb_dev_route_records: the stable partition (qb_route.hip), the per-rank
+// counts all-gathered (with every rank's output capacity, so all ranks take
+// the same decision on an overflow and none is left waiting in a send), then
+// one grouped send/recv per column — RCCL point-to-point over xGMI — into the
+// caller's columns in source-rank order.  The host waits once, for the
+// counts (the receive sizes are data-dependent).
+extern "C" size_t qb_route_workspace_bytes(int world, uint64_t M) {
+  if (world < 1 || world > QB_ROUTE_MAX_WORLD) return 0;
+  // send columns (group 4, flags 1, index/term/hint/log_term 32) + the
+  // partition's workspace + send_off and the all-gathered count rows
+  return up256(4 * M) + up256(M) + 4 * up256(8 * M) + qb_route_partition_workspace_bytes(world, M) +
+         up256(sizeof(uint32_t) * (size_t(world) + 1)) +
+         2 * up256(sizeof(uint64_t) * size_t(world) * size_t(world + 1));
+}
+
+extern "C" int qb_dev_route_records(qb_comm* c, uint64_t total, uint64_t M,
+                                    const uint32_t* rec_group, const uint8_t* rec_flags,
+                                    const uint64_t* rec_index, const uint64_t* rec_term,
+                                    const uint64_t* rec_hint, const uint64_t* rec_log_term,
+                                    uint32_t* out_group, uint8_t* out_flags,
+                                    uint64_t* out_index, uint64_t* out_term,
+                                    uint64_t* out_hint, uint64_t* out_log_term,
+                                    uint64_t out_cap, uint64_t* out_count, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  QB_REQUIRE(c && out_count, "comm / out_count NULL");
+  QB_REQUIRE(!rec_hint == !out_hint && !rec_log_term == !out_log_term,
+             "hint / log_term: give both the input and the output column, or neither");
+  const int W = c->world;
+  QB_REQUIRE(W <= QB_ROUTE_MAX_WORLD, "world %d > %d", W, QB_ROUTE_MAX_WORLD);
+  QB_REQUIRE(workspace && workspace_bytes >= qb_route_workspace_bytes(W, M),
+             "workspace too small (qb_route_workspace_bytes)");
+  hipStream_t st = qb::as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    char* p = ws + o;
+    o += up256(n);
+    return p;
+  };
+  uint32_t* s_group = reinterpret_cast<uint32_t*>(take(4 * M));
+  uint8_t* s_flags = reinterpret_cast<uint8_t*>(take(M));
+  uint64_t* s_index = reinterpret_cast<uint64_t*>(take(8 * M));
+  uint64_t* s_term = reinterpret_cast<uint64_t*>(take(8 * M));
+  uint64_t* s_hint = reinterpret_cast<uint64_t*>(take(8 * M));
+  uint64_t* s_lt = reinterpret_cast<uint64_t*>(take(8 * M));
+  const size_t pws = qb_route_partition_workspace_bytes(W, M);
+  void* part_ws = take(pws);
+  uint32_t* send_off = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * (size_t(W) + 1)));
+  uint64_t* row = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * size_t(W + 1)));
+  uint64_t* rows = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * size_t(W + 1)));
+  int rc = qb_dev_route_partition(total, W, M, rec_group, rec_flags, rec_index, rec_term, rec_hint,
+                                  rec_log_term, s_group, s_flags, s_index, s_term,
+                                  rec_hint ? s_hint : nullptr, rec_log_term ? s_lt : nullptr,
+                                  send_off, part_ws, pws, stream);
+  if (rc != QB_OK) return rc;
+  // this rank's row: records for each destination, then its output capacity
+  std::vector<uint32_t> off(size_t(W) + 1);
+  hipError_t h = hipMemcpyAsync(off.data(), send_off, sizeof(uint32_t) * off.size(),
+                                hipMemcpyDeviceToHost, st);
+  if (h == hipSuccess) h = hipStreamSynchronize(st);
+  if (h != hipSuccess) return qb::hip_fail(h, "send counts to host");
+  std::vector<uint64_t> mine(size_t(W) + 1), all(size_t(W) * size_t(W + 1));
+  for (int r = 0; r < W; ++r) mine[r] = uint64_t(off[r + 1]) - off[r];
+  mine[W] = out_cap;
+  h = hipMemcpyAsync(row, mine.data(), sizeof(uint64_t) * mine.size(), hipMemcpyHostToDevice, st);
+  if (h != hipSuccess) return qb::hip_fail(h, "count row to device");
+  QB_NCCL(ncclAllGather(row, rows, size_t(W + 1), ncclUint64, c->nccl, st), "ncclAllGather(counts)");
+  h = hipMemcpyAsync(all.data(), rows, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost, st);
+  if (h == hipSuccess) h = hipStreamSynchronize(st);
+  if (h != hipSuccess) return qb::hip_fail(h, "count rows to host");
+  // every rank checks every rank's capacity: one decision everywhere
+  auto cnt = [&](int src, int dst) { return all[size_t(src) * size_t(W + 1) + size_t(dst)]; };
+  for (int d = 0; d < W; ++d) {
+    uint64_t in = 0;
+    for (int s2 = 0; s2 < W; ++s2) in += cnt(s2, d);
+    if (d == c->rank) *out_count = in;
+    QB_REQUIRE(in <= all[size_t(d) * size_t(W + 1) + size_t(W)],
+               "rank %d would receive %llu records, over its capacity %llu", d,
+               (unsigned long long)in,
+               (unsigned long long)all[size_t(d) * size_t(W + 1) + size_t(W)]);
+  }
+  QB_REQUIRE(*out_count == 0 || (out_group && out_flags && out_index && out_term),
+             "output column is NULL");
+  std::vector<uint64_t> roff(size_t(W) + 1, 0);
+  for (int s2 = 0; s2 < W; ++s2) roff[s2 + 1] = roff[s2] + cnt(s2, c->rank);
+  struct Col {
+    const void* send;
+    void* recv;
+    size_t width;
+  };
+  const Col cols[6] = {{s_group, out_group, 4}, {s_flags, out_flags, 1}, {s_index, out_index, 8},
+                       {s_term, out_term, 8},   {s_hint, out_hint, 8},   {s_lt, out_log_term, 8}};
+  auto skip = [&](int k) { return (k == 4 && !rec_hint) || (k == 5 && !rec_log_term); };
+  QB_NCCL(ncclGroupStart(), "ncclGroupStart");
+  for (int k = 0; k < 6; ++k) {
+    if (skip(k)) continue;
+    const char* sb = static_cast<const char*>(cols[k].send);
+    char* rb = static_cast<char*>(cols[k].recv);
+    for (int p = 0; p < W; ++p) {
+      const uint64_t sn = uint64_t(off[p + 1]) - off[p], rn = cnt(p, c->rank);
+      if (p == c->rank) continue;  // the local run is copied below
+      if (sn) QB_NCCL(ncclSend(sb + cols[k].width * off[p], cols[k].width * sn, ncclUint8, p, c->nccl, st), "ncclSend");
+      if (rn) QB_NCCL(ncclRecv(rb + cols[k].width * roff[p], cols[k].width * rn, ncclUint8, p, c->nccl, st), "ncclRecv");
+    }
+  }
+  QB_NCCL(ncclGroupEnd(), "ncclGroupEnd");
+  const uint64_t self = cnt(c->rank, c->rank);
+  if (self) {
+    for (int k = 0; k < 6; ++k) {
+      if (skip(k)) continue;
+      h = hipMemcpyAsync(static_cast<char*>(cols[k].recv) + cols[k].width * roff[c->rank],
+                         static_cast<const char*>(cols[k].send) + cols[k].width * off[c->rank],
+                         cols[k].width * self, hipMemcpyDeviceToDevice, st);
+      if (h != hipSuccess) return qb::hip_fail(h, "hipMemcpyAsync(local run)");
     }
   }
   return QB_OK;

@@ -77,25 +77,67 @@ def route_records(cols: Dict[str, torch.Tensor], total: int,
     One count exchange plus one all-to-all per column: RCCL over xGMI on the
     GPU path, any torch.distributed backend in tests."""
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
     dev = cols["group"].device
-    g = cols["group"].to(torch.int64) & 0xFFFFFFFF
-    bounds = torch.tensor([shard_range(total, world, r)[1] for r in range(world)],
-                          dtype=torch.int64, device=dev)
-    owner = torch.bucketize(g, bounds, right=True).clamp_(max=world - 1)
-    order = torch.argsort(owner, stable=True)
-    send_counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    if dev.type == "cuda":  # the device partition (HIP, qb_route.hip), groups rebased
+        send, sc = route_partition(cols, total, world)
+    else:                   # host tensors (gloo tests): the same partition in torch
+        send, sc = _partition_host(cols, total, world, dist.get_rank(group))
+    send_counts = torch.tensor(sc, dtype=torch.int64, device=dev)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    rc = recv_counts.tolist()
     out = {}
-    for name, col in cols.items():
-        send = col[order].contiguous()
+    for name, col in send.items():
         recv = torch.empty((sum(rc),) + tuple(col.shape[1:]), dtype=col.dtype, device=dev)
-        dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
+        dist.all_to_all_single(recv, col, output_split_sizes=rc, input_split_sizes=sc,
                                group=group)
         out[name] = recv
-    b, _ = shard_range(total, world, rank)
-    local = (out["group"].to(torch.int64) & 0xFFFFFFFF) - b
-    out["group"] = local.to(torch.int32)
     return out
+
+
+def _owner_host(g: torch.Tensor, total: int, world: int) -> torch.Tensor:
+    bounds = torch.tensor([shard_range(total, world, r)[1] for r in range(world)],
+                          dtype=torch.int64, device=g.device)
+    return torch.bucketize(g, bounds, right=True).clamp_(max=world - 1)
+
+
+def _partition_host(cols, total, world, rank):
+    g = cols["group"].to(torch.int64) & 0xFFFFFFFF
+    owner = _owner_host(g, total, world)
+    order = torch.argsort(owner, stable=True)
+    begins = torch.tensor([shard_range(total, world, r)[0] for r in range(world)],
+                          dtype=torch.int64, device=g.device)
+    send = {name: col[order].contiguous() for name, col in cols.items()}
+    send["group"] = (g - begins[owner])[order].to(torch.int32)
+    return send, torch.bincount(owner, minlength=world).tolist()
+
+
+_ROUTE_COLS = ("group", "flags", "index", "term", "hint", "log_term")
+
+
+def route_partition(cols: Dict[str, torch.Tensor], total: int, world: int):
+    """The device half of the routing (qb_dev_route_partition): ``cols``
+    (device; group, flags, index, term required, hint / log_term optional)
+    stably partitioned by owner rank, group rebased to the owner's local
+    index.  Returns (send columns, per-rank counts)."""
+    from etcd_amd import _lib
+    lib = _lib.load()
+    unknown = set(cols) - set(_ROUTE_COLS)
+    if unknown:
+        raise ValueError(f"route_partition: unknown columns {sorted(unknown)}")
+    dev = cols["group"].device
+    M = cols["group"].numel()
+    send = {name: torch.empty_like(col) for name, col in cols.items()}
+    off = torch.empty(world + 1, dtype=torch.int32, device=dev)
+    nbytes = lib.qb_route_partition_workspace_bytes(world, M)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+
+    def ptr(d, name):
+        t = d.get(name)
+        return t.data_ptr() if t is not None else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(lib.qb_dev_route_partition(
+        total, world, M, *[ptr(cols, n) for n in _ROUTE_COLS], *[ptr(send, n) for n in _ROUTE_COLS],
+        off.data_ptr(), ws.data_ptr(), nbytes, stream), "qb_dev_route_partition")
+    o = off.cpu().tolist()
+    return send, [o[r + 1] - o[r] for r in range(world)]

@@ -675,6 +675,47 @@ int qb_dev_allgather_results(qb_comm* comm, uint64_t total,
                              uint64_t* commit_all, uint8_t* vote_all,
                              void* workspace, size_t workspace_bytes, void* stream);
 
+/* Record delivery to the owning shards ("message batches are
+ * bucketed by owning shard").  A node's inbound responses arrive at any rank;
+ * each record goes to the rank owning its global group, with the group
+ * rebased to that shard's local index (a group >= total goes to the last
+ * rank as an index >= its shard size, which the steps count as a bad group).
+ * Delivery is stable: the receiver gets each source rank's records in
+ * source-rank order, each source's in their original order — the batch order
+ * the leader step's sequential semantics need (raft.go:1099-1342 is a
+ * per-message fold).  Replaces the Python etcd_amd/shard.py:route_records
+ * (torch bucketize / argsort / all_to_all_single) for a cgo embedder. */
+#define QB_ROUTE_MAX_WORLD 64
+size_t qb_route_partition_workspace_bytes(int world, uint64_t M);
+/* The device half (no communication; usable with any world for testing and
+ * by callers with their own transport): the batch's records stably
+ * partitioned by owner into the send_* columns (M entries each; hint /
+ * log_term both-or-neither with their inputs), send_off[world + 1] (device)
+ * = the first send position per destination rank, send_off[world] = M. */
+int qb_dev_route_partition(uint64_t total, int world, uint64_t M, const uint32_t* rec_group,
+                           const uint8_t* rec_flags, const uint64_t* rec_index,
+                           const uint64_t* rec_term, const uint64_t* rec_hint,
+                           const uint64_t* rec_log_term, uint32_t* send_group,
+                           uint8_t* send_flags, uint64_t* send_index, uint64_t* send_term,
+                           uint64_t* send_hint, uint64_t* send_log_term, uint32_t* send_off,
+                           void* workspace, size_t workspace_bytes, void* stream);
+size_t qb_route_workspace_bytes(int world, uint64_t M);
+/* Collective over the comm: partition, an all-gather of every rank's counts
+ * and output capacity (every rank refuses with QB_EINVAL if any rank's
+ * receive would exceed its out_cap — one decision everywhere, no rank left in
+ * a send), then RCCL point-to-point runs per column into out_* (device,
+ * out_cap entries).  *out_count (host) = records received.  The host waits on
+ * the stream twice (the receive sizes are data-dependent).  Every rank must
+ * call it with valid arguments: a rank failing a precondition before the
+ * all-gather leaves the others waiting in it. */
+int qb_dev_route_records(qb_comm* comm, uint64_t total, uint64_t M, const uint32_t* rec_group,
+                         const uint8_t* rec_flags, const uint64_t* rec_index,
+                         const uint64_t* rec_term, const uint64_t* rec_hint,
+                         const uint64_t* rec_log_term, uint32_t* out_group, uint8_t* out_flags,
+                         uint64_t* out_index, uint64_t* out_term, uint64_t* out_hint,
+                         uint64_t* out_log_term, uint64_t out_cap, uint64_t* out_count,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
 /* ----------------------------------------------------------------------- */
 /* Synthetic workload generators (bench/test inputs)        */
 /* ----------------------------------------------------------------------- */

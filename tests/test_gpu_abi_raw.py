@@ -271,3 +271,88 @@ def test_comm_allgather_world1_raw_abi():
     assert np.array_equal(s.down(o_c, c), c) and np.array_equal(s.down(o_v, v), v)
     _lib.check(lib.qb_comm_destroy(comm), "comm destroy")
     s.close()
+
+
+def _route_ref(total, world, grp, cols):
+    """Stable partition by owner (shard_range) with rebased groups: the order
+    etcd_amd/shard.py:route_records defines."""
+    from etcd_amd.shard import shard_range
+    bounds = np.array([shard_range(total, world, r)[1] for r in range(world)], np.int64)
+    begins = np.array([shard_range(total, world, r)[0] for r in range(world)], np.int64)
+    g = grp.astype(np.int64)
+    owner = np.minimum(np.searchsorted(bounds, g, side="right"), world - 1)
+    order = np.argsort(owner, kind="stable")
+    out = {k: v[order] for k, v in cols.items()}
+    out["group"] = (g - begins[owner])[order].astype(np.uint32)
+    return out, np.bincount(owner, minlength=world)
+
+
+@pytest.mark.parametrize("world,total,M,opt", [(1, 1000, 5000, True), (2, 100003, 300001, False),
+                                               (3, 7, 20000, True), (8, 1 << 20, 1 << 20, True),
+                                               (64, 100000, 70001, False), (5, 0, 1000, True)])
+def test_route_partition_raw_abi(world, total, M, opt):
+    """qb_dev_route_partition against the stable host partition: owners from
+    qb_shard_range, groups >= total to the last rank, the columns moved in
+    (owner, original position) order; send_off per destination."""
+    s = Stream()
+    lib = s.lib
+    rng = np.random.default_rng(world * 7919 + M)
+    hi = max(total + total // 50, 1) + 3
+    cols = {"group": rng.integers(0, hi, M).astype(np.uint32),
+            "flags": rng.integers(0, 256, M).astype(np.uint8),
+            "index": rng.integers(0, 1 << 62, M).astype(np.uint64),
+            "term": rng.integers(0, 1 << 62, M).astype(np.uint64)}
+    if opt:
+        cols["hint"] = rng.integers(0, 1 << 62, M).astype(np.uint64)
+        cols["log_term"] = rng.integers(0, 1 << 62, M).astype(np.uint64)
+    names = ("group", "flags", "index", "term", "hint", "log_term")
+    din = {k: s.up(v) for k, v in cols.items()}
+    dout = {k: s.zeros(v.nbytes) for k, v in cols.items()}
+    off = s.zeros(4 * (world + 1))
+    need = lib.qb_route_partition_workspace_bytes(world, M)
+    ws = s.zeros(need)
+    _lib.check(lib.qb_dev_route_partition(total, world, M, *[din.get(n) for n in names],
+                                          *[dout.get(n) for n in names], off, ws, need, s.st),
+               "route partition")
+    ref, counts = _route_ref(total, world, cols["group"], cols)
+    for k, v in cols.items():
+        assert np.array_equal(s.down(dout[k], v), ref[k]), k
+    o = s.down(off, np.empty(world + 1, np.uint32))
+    assert np.array_equal(np.diff(o.astype(np.int64)), counts) and o[0] == 0 and o[-1] == M
+    s.close()
+
+
+def test_route_records_world1_raw_abi():
+    """qb_dev_route_records on a single-rank communicator: every record stays,
+    groups rebased (rank 0 begins at 0), order kept; an output capacity below
+    the receive count is refused (QB_EINVAL) before anything moves."""
+    s = Stream()
+    lib = s.lib
+    uid = (C.c_char * 128)()
+    _lib.check(lib.qb_comm_get_unique_id(uid), "unique id")
+    comm = C.c_void_p()
+    _lib.check(lib.qb_comm_init(C.byref(comm), 1, 0, uid), "comm init")
+    M, total = 200003, 50000
+    rng = np.random.default_rng(5)
+    cols = {"group": rng.integers(0, total + 100, M).astype(np.uint32),
+            "flags": rng.integers(0, 256, M).astype(np.uint8),
+            "index": rng.integers(0, 1 << 62, M).astype(np.uint64),
+            "term": rng.integers(0, 1 << 62, M).astype(np.uint64)}
+    names = ("group", "flags", "index", "term")
+    din = {k: s.up(v) for k, v in cols.items()}
+    dout = {k: s.zeros(v.nbytes) for k, v in cols.items()}
+    need = lib.qb_route_workspace_bytes(1, M)
+    ws = s.zeros(need)
+    cnt = C.c_uint64(0)
+    rc = lib.qb_dev_route_records(comm, total, M, *[din[n] for n in names], None, None,
+                                  *[dout[n] for n in names], None, None, M - 1, C.byref(cnt),
+                                  ws, need, s.st)
+    assert rc == _lib.QB_EINVAL and b"capacity" in lib.qb_last_error()
+    _lib.check(lib.qb_dev_route_records(comm, total, M, *[din[n] for n in names], None, None,
+                                        *[dout[n] for n in names], None, None, M, C.byref(cnt),
+                                        ws, need, s.st), "route records")
+    assert cnt.value == M
+    for k, v in cols.items():
+        assert np.array_equal(s.down(dout[k], v), v), k
+    _lib.check(lib.qb_comm_destroy(comm), "comm destroy")
+    s.close()

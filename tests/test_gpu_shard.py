@@ -144,3 +144,22 @@ def test_routed_records_device_tracker_step(world):
     assert np.array_equal(match, st["match"])
     assert np.array_equal(cm, st["committed"])
     assert np.array_equal(sd, st["stepped_down"].astype(bool))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_route_partition_device_matches_host(world):
+    """shard.route_records' device partition (qb_dev_route_partition) equals
+    its host twin on the same columns: the RCCL path and the gloo tests send
+    identical runs."""
+    from etcd_amd.shard import _partition_host, route_partition
+    total, M = 60001, 100000
+    rng = np.random.default_rng(world)
+    cols = {"group": torch.from_numpy(rng.integers(0, total + 10, M).astype(np.int32)),
+            "flags": torch.from_numpy(rng.integers(0, 256, M).astype(np.uint8)),
+            "index": torch.from_numpy(rng.integers(0, 1 << 62, M)),
+            "term": torch.from_numpy(rng.integers(0, 1 << 62, M))}
+    hs, hc = _partition_host(cols, total, world, 0)
+    ds, dc = route_partition({k: v.cuda() for k, v in cols.items()}, total, world)
+    assert hc == dc
+    for k in cols:
+        assert torch.equal(hs[k], ds[k].cpu()), k
