@@ -50,7 +50,12 @@ __host__ __device__ constexpr u32 chunk_groups(u32 n) {
   return n <= 8 ? u32(QB_CH_NARROW) : u32(QB_CH_WIDE);
 }
 // CSR chunks: the LDS run buffer holds CH * WMAX slots.
-__host__ __device__ constexpr u32 csr_chunk_groups(u32 wmax) { return wmax <= 8 ? 512u : 256u; }
+#ifndef QB_CSR_CH_WIDE
+#define QB_CSR_CH_WIDE 512
+#endif
+__host__ __device__ constexpr u32 csr_chunk_groups(u32 wmax) {
+  return wmax <= 8 ? 512u : u32(QB_CSR_CH_WIDE);
+}
 
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
 // with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles

@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 // act[CH] u32.
 // K5 threads per workgroup (QB_K5_BLOCK, at most the chunk's group count).
 #ifndef QB_K5_BLOCK
-#define QB_K5_BLOCK 256
+#define QB_K5_BLOCK 512
 #endif
 __host__ __device__ constexpr u32 k5_block(int n) {
   return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);

@@ -18,31 +18,60 @@
 // Pipeline: K1-K4 are the FIXED step's bucketing (qb_bucket.h, records cut
 // into chunks of CH consecutive groups, one run per part of the chunk's
 // super-bucket).  K5 = k_csr_apply: one workgroup per chunk.  The chunk's
-// groups own one contiguous slot run match[off[g0] .. off[g0 + CH]), at most
-// CH * WMAX slots; an LDS accumulator per slot of the run takes the records'
-// MaybeUpdate (ds_max_u64), the old run is streamed into registers meanwhile,
-// then one coalesced pass writes the raised slots and leaves max(old, acc) in
-// LDS, and each thread evaluates its group's JointConfig.CommittedIndex from
-// LDS (compacted half sorts, qb_csr.h) and the maybeCommit gate.  Chunks with
-// a higher-term record (batch order matters) go to the slow path
-// (qb_tracker_slow.h) exactly as in the FIXED step.
+// groups own one contiguous slot run match[off[g0] .. off[g0 + CH]); an LDS
+// accumulator per slot of the run takes the records' MaybeUpdate
+// (ds_max_u64), the old run is streamed into registers meanwhile, then one
+// coalesced pass writes the raised slots and leaves max(old, acc) in LDS, and
+// each thread evaluates its group's JointConfig.CommittedIndex from LDS
+// (compacted half sorts, qb_csr.h) and the maybeCommit gate.
+//
+// Two launches of K5: the first with an LDS run buffer of 8 slots per group
+// (the workgroup's LDS sets the occupancy: 512 groups x 8 slots measured 847
+// us per 16M-group step against 887 for 256 groups x 12), deferring a chunk
+// whose run is longer; the second, with the table's max_slots per group,
+// applies only the deferred chunks (a workgroup per chunk that returns at
+// once otherwise, ~5 us).  Chunks with a higher-term record (batch order
+// matters) go to the slow path (qb_tracker_slow.h) exactly as in the FIXED
+// step.
 #include "qb_tracker_slow.h"
 
 namespace qb {
 namespace bk {
 
-template <int WMAX, bool NEXT>
-__global__ __launch_bounds__(kBlock) void k_csr_apply(
-    Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
-    const u32* __restrict__ off, const u32* __restrict__ cfg, const u64* __restrict__ group_term,
-    const u64* __restrict__ term_start, u64* __restrict__ match, u64* __restrict__ next,
-    u16* __restrict__ active, u64* __restrict__ committed, u32* __restrict__ stepdown_at,
-    u8* __restrict__ advanced, u8* __restrict__ chunk_slow, u32* __restrict__ any_slow,
-    u64* __restrict__ shards) {
+// Threads per workgroup, and LDS slots per group of the first launch's run
+// buffer; compile-time knobs for A/B builds, the defaults are the measured
+// choice.
+#ifndef QB_CSR_BLOCK
+#define QB_CSR_BLOCK 512
+#endif
+#ifndef QB_CSR_CAPW
+#define QB_CSR_CAPW 8
+#endif
+__host__ __device__ constexpr u32 csr_block() {
+  return csr_chunk_groups(16) < u32(QB_CSR_BLOCK) ? csr_chunk_groups(16) : u32(QB_CSR_BLOCK);
+}
+constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the first launch
+
+// CAPW: LDS slots per group; SECOND: the launch for the deferred chunks.
+#define QB_CSR_APPLY_PARAMS                                                                      \
+  Geometry geo, Cols recs, const u32 *__restrict__ pt, const u32 *__restrict__ cs,                \
+      const u32 *__restrict__ off, const u32 *__restrict__ cfg,                                   \
+      const u64 *__restrict__ group_term, const u64 *__restrict__ term_start,                     \
+      u64 *__restrict__ match, u64 *__restrict__ next, u16 *__restrict__ active,                  \
+      u64 *__restrict__ committed, u32 *__restrict__ stepdown_at, u8 *__restrict__ advanced,      \
+      u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards
+#define QB_CSR_APPLY_ARGS                                                                      \
+  geo, recs, pt, cs, off, cfg, group_term, term_start, match, next, active, committed,          \
+      stepdown_at, advanced, chunk_slow, any_slow, shards
+
+// One chunk c (the whole workgroup).
+template <int WMAX, int CAPW, bool NEXT, bool SECOND>
+__device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS) {
   constexpr u32 CH = csr_chunk_groups(WMAX);
-  constexpr u32 GPT = CH / kBlock;     // groups per thread in the commit phase
-  constexpr u32 CAP = CH * WMAX;       // slot-run capacity
-  constexpr u32 PER = CAP / kBlock;    // run slots per thread
+  constexpr u32 B = csr_block();
+  constexpr u32 GPT = CH / B;          // groups per thread in the commit phase
+  constexpr u32 CAP = CH * u32(CAPW);  // slot-run capacity
+  constexpr u32 PER = (CAP + B - 1) / B;  // run slots per thread
   __shared__ u64 acc[CAP];
   __shared__ u64 accn[NEXT ? CAP : 1];
   __shared__ u32 offs[CH + 1];
@@ -52,7 +81,6 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   __shared__ u32 tl[4];
   __shared__ RunTable rtab;
   BlockTally<4> tally;  // stale, applied, rejected, non-member
-  const u32 c = blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
@@ -64,20 +92,20 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   // only in straight-line code.
   // offsets and group terms into registers first, the run table's loads
   // beside them: one round trip, not three
-  constexpr u32 OPT = (CH + kBlock) / kBlock;  // CH + 1 offsets
+  constexpr u32 OPT = (CH + B) / B;  // CH + 1 offsets
   u32 ofr[OPT];
   u64 gtr[GPT];
 #pragma unroll
   for (u32 q = 0; q < OPT; ++q) {
-    const u32 k = threadIdx.x + q * kBlock;
+    const u32 k = threadIdx.x + q * B;
     ofr[q] = off[g0 + (k < ng ? k : ng)];
   }
 #pragma unroll
   for (u32 q = 0; q < GPT; ++q) {
-    const u32 k = threadIdx.x + q * kBlock;
+    const u32 k = threadIdx.x + q * B;
     gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
-  for (u32 k = threadIdx.x; k < CAP; k += kBlock) {
+  for (u32 k = threadIdx.x; k < CAP; k += B) {
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
   }
@@ -85,26 +113,34 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   u32 total = rtab.build(cs, p0, p1, cl);  // synchronises
 #pragma unroll
   for (u32 q = 0; q < OPT; ++q) {
-    const u32 k = threadIdx.x + q * kBlock;
+    const u32 k = threadIdx.x + q * B;
     if (k <= CH) offs[k] = ofr[q];
   }
 #pragma unroll
   for (u32 q = 0; q < GPT; ++q) {
-    gterm[threadIdx.x + q * kBlock] = gtr[q];
-    act[threadIdx.x + q * kBlock] = 0;
+    gterm[threadIdx.x + q * B] = gtr[q];
+    act[threadIdx.x + q * B] = 0;
   }
   __syncthreads();
   const u32 a0 = offs[0], run = offs[CH] - a0;
-  // A table breaking its max_slots bound cannot stage its run in LDS: the
-  // chunk takes the slow path (exact per-record semantics, global atomics).
+  // A run longer than the buffer: the first launch defers the chunk to the
+  // second; in the second, only a table breaking its max_slots bound gets
+  // here, and the chunk takes the slow path (exact per-record semantics,
+  // global atomics).
   const bool fits = run <= CAP;
-  constexpr int kRecPer = 4;
+  if constexpr (!SECOND) {
+    if (!fits) {  // block-uniform, before anything is written
+      if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
+      return;
+    }
+  }
+  constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
   u64 rmr[kRecPer], rix[kRecPer];
   auto load = [&](u32 f0, u32 n) {
     u32 ix[kRecPer];
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
-      const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+      const u32 f = f0 + u32(r) * B + threadIdx.x;
       ix[r] = n ? rtab.locate(f < n ? f : n - 1) : 0u;
     }
 #pragma unroll
@@ -116,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   auto apply = [&](u32 f0, u32 n) {
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
-      const u32 f = f0 + u32(r) * kBlock + threadIdx.x;
+      const u32 f = f0 + u32(r) * B + threadIdx.x;
       bool stale = false, applied = false, rejected = false, non = false;
       if (f < n && fits) {
         const u64 mr = rmr[r];
@@ -159,14 +195,14 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   const u32 last = run && fits ? run - 1u : 0u;
 #pragma unroll
   for (u32 p = 0; p < PER; ++p) {
-    const u32 j = threadIdx.x + p * kBlock;
+    const u32 j = threadIdx.x + p * B;
     old[p] = src[j < last ? j : last];
   }
   u64 cm[GPT], ts[GPT];
   u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * kBlock;
+    const u32 lg = threadIdx.x + k * B;
     const u64 g = g0 + (lg < ng ? lg : ng - 1);
     cm[k] = committed[g];
     ts[k] = term_start[g];
@@ -176,8 +212,8 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
 #pragma unroll
   for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
   apply(0, total);
-  for (u32 pb = p0, f0 = kBlock * kRecPer;;) {
-    for (; f0 < total; f0 += kBlock * kRecPer) {
+  for (u32 pb = p0, f0 = B * kRecPer;;) {
+    for (; f0 < total; f0 += B * kRecPer) {
       load(f0, total);
       apply(f0, total);
     }
@@ -189,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   if (!fits && threadIdx.x == 0) slow = 1;
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
-    for (u32 lg = threadIdx.x; lg < ng; lg += kBlock) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
+    for (u32 lg = threadIdx.x; lg < ng; lg += B) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
     if (threadIdx.x == 0) {
       chunk_slow[c] = 1;
       atomicOr(any_slow, 1u);
@@ -201,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   // in LDS for the CommittedIndex of every group
 #pragma unroll
   for (u32 p = 0; p < PER; ++p) {
-    const u32 j = threadIdx.x + p * kBlock;
+    const u32 j = threadIdx.x + p * B;
     if (j < run) {
       const u64 a = acc[j];
       if (a > old[p]) {
@@ -223,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   // wave-uniform)
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * kBlock;
+    const u32 lg = threadIdx.x + k * B;
     const bool live = lg < ng;
     const u32 base = live ? offs[lg] - a0 : 0u;
     u32 sg = live ? offs[lg + 1] - offs[lg] : 0u;
@@ -242,6 +278,32 @@ __global__ __launch_bounds__(kBlock) void k_csr_apply(
   tally.flush(tl, shard_of(shards), slot);
 }
 
+template <int WMAX, int CAPW, bool NEXT>
+__global__ __launch_bounds__(csr_block()) void k_csr_apply(QB_CSR_APPLY_PARAMS) {
+  csr_apply_chunk<WMAX, CAPW, NEXT, false>(blockIdx.x, QB_CSR_APPLY_ARGS);
+}
+
+// The deferred chunks: a workgroup per kDeferSpan consecutive chunks reads
+// their flags at once and applies its deferred ones in turn (a workgroup per
+// chunk cost ~25 us even with nothing deferred: every one of them reserved
+// the big buffer's LDS).
+constexpr u32 kDeferSpan = 64;
+template <int WMAX, int CAPW, bool NEXT>
+__global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY_PARAMS) {
+  __shared__ u64 mask;
+  const u32 c0 = blockIdx.x * kDeferSpan;
+  if (threadIdx.x < 64) {
+    const u32 c = c0 + threadIdx.x;
+    const u64 m = __ballot(c < geo.NC && threadIdx.x < kDeferSpan && chunk_slow[c] == kChunkDeferred);
+    if (threadIdx.x == 0) mask = m;
+  }
+  __syncthreads();
+  for (u64 m = mask; m; m &= m - 1) {  // block-uniform
+    __syncthreads();  // the previous chunk's readers of the LDS state are done
+    csr_apply_chunk<WMAX, CAPW, NEXT, true>(c0 + u32(__builtin_ctzll(m)), QB_CSR_APPLY_ARGS);
+  }
+}
+
 struct CsrStepArgs {
   const u32 *off, *cfg;
   const u64 *gt, *ts;
@@ -255,17 +317,26 @@ struct CsrStepArgs {
   u64* shards;
 };
 
+template <int WMAX, bool SECOND>
+void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+                  const CsrStepArgs& a, hipStream_t st) {
+  constexpr int CAPW = SECOND ? WMAX : (WMAX < QB_CSR_CAPW ? WMAX : QB_CSR_CAPW);
+  const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
+#define QB_CSR_LAUNCH(NX)                                                                       \
+  hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX> : k_csr_apply<WMAX, CAPW, NX>), \
+                     grid, dim3(csr_block()), 0, st, geo, recs, pt, cs, a.off, a.cfg, a.gt, a.ts,  \
+                     a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
+                     a.any_slow, a.shards)
+  if (a.next) QB_CSR_LAUNCH(true);
+  else QB_CSR_LAUNCH(false);
+#undef QB_CSR_LAUNCH
+}
+
 template <int WMAX>
 void launch_csr_step(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                      const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
-  if (a.next)
-    hipLaunchKernelGGL((k_csr_apply<WMAX, true>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs, pt,
-                       cs, a.off, a.cfg, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.shards);
-  else
-    hipLaunchKernelGGL((k_csr_apply<WMAX, false>), dim3(geo.NC), dim3(kBlock), 0, st, geo, recs,
-                       pt, cs, a.off, a.cfg, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.shards);
+  launch_apply<WMAX, false>(geo, recs, pt, cs, a, st);
+  if constexpr (WMAX > QB_CSR_CAPW) launch_apply<WMAX, true>(geo, recs, pt, cs, a, st);
   hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
                      CsrLay<WMAX>{a.off, a.cfg}, sa.rg, sa.rf, sa.ri, sa.rt, a.gt, a.ts,
                      a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,

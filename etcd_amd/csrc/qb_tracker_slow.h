@@ -60,7 +60,7 @@ constexpr unsigned kSlowBlockMax = 256;
 
 __device__ __forceinline__ bool in_slow_chunk(const Geometry& geo, u32 g, u32 f,
                                               const u8* __restrict__ chunk_slow) {
-  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[geo.chunk_of(g)];
+  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[geo.chunk_of(g)] == 1;
 }
 
 // Tracker state layouts.  FIXED: n voters, slot-major rows of G (every slot

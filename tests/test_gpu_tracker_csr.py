@@ -216,7 +216,7 @@ def test_csr_stepdown_untouched_outside_flagged_chunks():
     tr.stepdown_at.fill_(777)
     tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
     sd = tr.stepdown_at.cpu().numpy().view(np.uint32)
-    CH = 256 if tr.max_slots > 8 else 512
+    CH = 512  # groups per K5 chunk (qb_bucket.h csr_chunk_groups)
     lo, hi_end = (hi // CH) * CH, min(G, (hi // CH + 1) * CH)
     assert sd[hi] == 7
     inside = np.arange(lo, hi_end)
@@ -224,6 +224,51 @@ def test_csr_stepdown_untouched_outside_flagged_chunks():
     outside = np.ones(G, bool)
     outside[lo:hi_end] = False
     assert np.all(sd[outside] == 777)
+
+
+@pytest.mark.parametrize("lo_slots,track_next", [(9, True), (14, False), (1, True)])
+def test_csr_step_deferred_chunks(lo_slots, track_next):
+    """Wide groups (lo_slots..16 slots, joint configs and learners): a chunk
+    whose slot run is longer than the first launch's LDS buffer (8 slots per
+    group) is deferred to the second launch (the table's max_slots per
+    group); a higher-term record in such a chunk still sends it to the slow
+    path.  Mixed widths exercise both launches in one step."""
+    G, M = 5000, 20000
+    rng = np.random.default_rng(lo_slots * 101 + track_next)
+    sizes = rng.integers(lo_slots, 17, size=G).astype(np.int64)
+    off = np.zeros(G + 1, np.uint32)
+    off[1:] = np.cumsum(sizes).astype(np.uint32)
+    cfg = np.zeros(G, np.uint32)
+    for g in range(G):
+        s = int(sizes[g])
+        vin = rng.integers(1, 1 << s) & ((1 << s) - 1)
+        vout = (rng.integers(1, 1 << s) & ((1 << s) - 1)) if rng.random() < 0.3 else 0
+        cfg[g] = np.uint32(int(vin) | (int(vout) << 16))
+    S = int(off[-1])
+    last = rng.integers(1 << 20, 1 << 40, size=G).astype(np.uint64)
+    match = (np.repeat(last, sizes) - rng.integers(0, 200, size=S).astype(np.uint64))
+    st = {"match": match, "next": match + np.uint64(1), "active": np.zeros(G, np.uint16),
+          "term": rng.integers(2, 9, size=G).astype(np.uint64),
+          "term_start": last - rng.integers(0, 300, size=G).astype(np.uint64),
+          "last_index": last, "committed": np.zeros(G, np.uint64),
+          "stepped_down": np.zeros(G, np.uint8)}
+    oc.csr_commit_all(off, cfg, st["match"], st["term_start"], st["committed"])
+    if not track_next:
+        st.pop("next")
+    tr = _tracker(off, cfg, st, track_next=track_next)
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(2):
+        group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, seq, stale=0.02,
+                                                      higher=0.0005, nonmember=0.01)
+        stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, G)
+        got = tr.stats_dict()
+        want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                         "bad_group", "after_stepdown"), stats.tolist()))
+        assert got == want
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
 
 
 @pytest.mark.timeout(300)
