@@ -381,7 +381,7 @@ def tracker_main(args, world, rank, dev):
     key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
     achieved = bpg * G / step_s / 1e9
     kern = ("k_bk_hist, k_scan_local, k_bk_sums_parts, k_bk_scatter, k_bk_split, "
-            + ("k_csr_apply<WMAX,false>, k_bk_slow<CsrLay<WMAX>>" if csr
+            + ("k_csr_apply<WMAX,8,false>, k_csr_apply_deferred, k_bk_slow<CsrLay<WMAX>>" if csr
                else "k_bk_apply<5,false>, k_bk_slow<FixedLay<5>>"))
     out = {
         "metric": METRIC + " — configs[4] streaming tracker: group-steps/s",
