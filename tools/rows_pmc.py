@@ -25,7 +25,7 @@ def main():
             per[key] += float(r["Counter_Value"])
         for (_, k), v in per.items():
             acc[k].append(v * 1024 * (2 if kind == "fetch" else 1))
-    print(f"{'kernel':60s} {'n':>5s} {'med us':>9s} {'read MB':>9s} {'write MB':>9s} {'GB/s':>7s}")
+    print(f"{'kernel':60s} {'n':>5s} {'med us':>9s} {'read MB':>9s} {'write MB':>9s} {'TB/s':>7s}")
     tot = [0.0, 0.0, 0.0]
     for k, v in sorted(dur.items(), key=lambda kv: -statistics.median(kv[1]) * len(kv[1])):
         if not k.startswith("qb::"):
@@ -33,7 +33,7 @@ def main():
         m = statistics.median(v) / 1e3
         r = statistics.median(rd[k]) / 1e6 if rd[k] else float("nan")
         w = statistics.median(wr[k]) / 1e6 if wr[k] else float("nan")
-        print(f"{k:60s} {len(v):5d} {m:9.1f} {r:9.1f} {w:9.1f} {(r + w) / m * 1e-3 * 1e3:7.0f}")
+        print(f"{k:60s} {len(v):5d} {m:9.1f} {r:9.1f} {w:9.1f} {(r + w) / m:7.2f}")
     return 0
 
 
