@@ -75,6 +75,10 @@ SIGNATURES = {
     "qb_dev_leader_step": (_i32, [_p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_dev_ingest_messages": (_i32, [_u64, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p,
                                       _p, _p, _p, _p, _p]),
+    "qb_wire_group_rows_bytes": (C.c_size_t, [_u64]),
+    "qb_dev_wire_group_rows": (_i32, [_u64, _p, _p, _p, _p]),
+    "qb_dev_ingest_messages_rows": (_i32, [_u64, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p,
+                                           _p, _p, _p, _p, _p, _p, _p]),
     "qb_conf_change_workspace_bytes": (C.c_size_t, [_u64]),
     "qb_dev_conf_change": (_i32, [_p, _p, _p, C.c_size_t, _p]),
     "qb_shard_range": (_i32, [_u64, _i32, _i32, _p, _p]),

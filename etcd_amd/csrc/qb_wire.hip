@@ -319,6 +319,7 @@ struct Args {
   const u32* mgroup;
   const u32* off;
   const u64* ids;
+  const u64* rows;  // nullable: the 64-byte group rows (qb_dev_wire_group_rows)
   u32* rg;
   u8* rf;
   u64 *ri, *rt, *rh, *rl;
@@ -333,6 +334,7 @@ struct Args {
 // reads a harmless word of moff — so their wait lands where the IDs are
 // compared, after the parse, not ahead of it.
 constexpr u32 kIdBatch = 8;
+constexpr u32 kRowIds = 7;  // member IDs held in a 64-byte group row
 struct GroupRow {
   u32 mg, s0, s1;
   u64 id[kIdBatch];
@@ -378,10 +380,11 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
         u32 slot = QB_REC_NO_PROGRESS;
         if (group < A.G) {
           const u32 n = row.s1 - row.s0;
+          const u32 held = A.rows ? kRowIds : kIdBatch;  // IDs already in registers
 #pragma unroll
           for (u32 k = kIdBatch; k-- > 0;)
-            if (k < n && row.id[k] == f.from) slot = k;
-          for (u32 j = row.s0 + kIdBatch; j < row.s1 && slot == QB_REC_NO_PROGRESS; ++j)
+            if (k < n && k < held && row.id[k] == f.from) slot = k;
+          for (u32 j = row.s0 + held; j < row.s1 && slot == QB_REC_NO_PROGRESS; ++j)
             if (A.ids[j] == f.from) slot = j - row.s0;
         }
         flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
@@ -422,7 +425,23 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   const u64 p1 = __builtin_nontemporal_load(A.moff + mc + 1);
   GroupRow row;
   row.mg = __builtin_nontemporal_load(A.mgroup + mc);
-  {
+  if (A.rows) {
+    // the group's 64-byte row: one aligned line segment per message instead
+    // of a row of off and then one or two lines of ids
+    const u32 gi = row.mg < A.G ? row.mg : 0u;
+    const ulonglong2* rw = reinterpret_cast<const ulonglong2*>(A.rows + 8ull * gi);
+    const ulonglong2 a = rw[0], b = rw[1], c = rw[2], d = rw[3];
+    row.s0 = u32(a.x >> 32);
+    row.s1 = row.s0 + u32(a.x);  // n: the member count
+    row.id[0] = a.y;
+    row.id[1] = b.x;
+    row.id[2] = b.y;
+    row.id[3] = c.x;
+    row.id[4] = c.y;
+    row.id[5] = d.x;
+    row.id[6] = d.y;
+    row.id[7] = 0;  // (member 8 and up: ids[s0 + k], after the parse)
+  } else {
     // G == 0: off may be absent; read the first word of moff (>= 2 entries)
     const u32* offp = A.G ? A.off : reinterpret_cast<const u32*>(A.moff);
     const u32 gi = row.mg < A.G ? row.mg : 0u;
@@ -456,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     lend = a1 < A.nbytes ? a1 : A.nbytes;
   }
   __syncthreads();
-  {
+  if (!A.rows) {
     const u32 n = row.mg < A.G ? row.s1 - row.s0 : 0u;
     const u64* idp = n ? A.ids + row.s0 : A.moff;
 #pragma unroll
@@ -480,7 +499,48 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
 }  // namespace wire
 }  // namespace qb
 
+namespace qb {
+namespace wire {
+// Group rows: row g = { n | s0 << 32, the first kRowIds member IDs }, 64 B.
+__global__ __launch_bounds__(kBlock) void k_group_rows(u64 G, const u32* __restrict__ off,
+                                                       const u64* __restrict__ ids,
+                                                       u64* __restrict__ rows) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const u32 s0 = off[g], n = off[g + 1] - s0;
+  u64 w[8];
+  w[0] = u64(n) | (u64(s0) << 32);
+#pragma unroll
+  for (u32 k = 0; k < kRowIds; ++k) w[1 + k] = k < n ? ids[s0 + k] : 0ull;
+  ulonglong2* dst = reinterpret_cast<ulonglong2*>(rows + 8 * g);
+#pragma unroll
+  for (u32 q = 0; q < 4; ++q) dst[q] = ulonglong2{w[2 * q], w[2 * q + 1]};
+}
+}  // namespace wire
+}  // namespace qb
+
 using namespace qb;
+
+extern "C" size_t qb_wire_group_rows_bytes(uint64_t G) { return size_t(G) * 64; }
+
+extern "C" int qb_dev_wire_group_rows(uint64_t G, const uint32_t* off, const uint64_t* ids,
+                                      uint64_t* rows, void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(off && ids && rows, "qb_dev_wire_group_rows: off, ids and rows are required");
+  QB_REQUIRE((reinterpret_cast<uintptr_t>(rows) & 15u) == 0,
+             "qb_dev_wire_group_rows: rows must be 16-byte aligned");
+  hipLaunchKernelGGL(wire::k_group_rows, dim3(grid_for(G)), dim3(kBlock), 0, as_stream(stream), G,
+                     off, reinterpret_cast<const u64*>(ids), reinterpret_cast<u64*>(rows));
+  QB_CHECK_LAUNCH("k_group_rows");
+  return QB_OK;
+}
+
+extern "C" int qb_dev_ingest_messages_rows(
+    uint64_t M, const uint8_t* bytes, uint64_t nbytes, const uint64_t* msg_off,
+    const uint32_t* msg_group, uint64_t G, const uint64_t* rows, const uint64_t* ids,
+    uint32_t* rec_group, uint8_t* rec_flags, uint64_t* rec_index, uint64_t* rec_term,
+    uint64_t* rec_hint, uint64_t* rec_log_term, uint8_t* status, uint8_t* msg_type,
+    uint64_t* stats, void* stream);
 
 extern "C" int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
                                       const uint64_t* msg_off, const uint32_t* msg_group,
@@ -496,8 +556,32 @@ extern "C" int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t
   QB_REQUIRE(nbytes == 0 || bytes, "qb_dev_ingest_messages: bytes is NULL");
   QB_REQUIRE(G == 0 || (off && ids), "qb_dev_ingest_messages: off and ids are required");
   wire::Args A{M, nbytes, G, bytes, reinterpret_cast<const u64*>(msg_off), msg_group, off,
-               reinterpret_cast<const u64*>(ids), rec_group, rec_flags,
+               reinterpret_cast<const u64*>(ids), nullptr, rec_group, rec_flags,
                reinterpret_cast<u64*>(rec_index), reinterpret_cast<u64*>(rec_term),
+               reinterpret_cast<u64*>(rec_hint), reinterpret_cast<u64*>(rec_log_term), status,
+               msg_type, reinterpret_cast<u64*>(stats)};
+  hipLaunchKernelGGL(wire::k_ingest, dim3(grid_for(M)), dim3(kBlock), 0, as_stream(stream), A);
+  QB_CHECK_LAUNCH("k_ingest");
+  return QB_OK;
+}
+
+extern "C" int qb_dev_ingest_messages_rows(
+    uint64_t M, const uint8_t* bytes, uint64_t nbytes, const uint64_t* msg_off,
+    const uint32_t* msg_group, uint64_t G, const uint64_t* rows, const uint64_t* ids,
+    uint32_t* rec_group, uint8_t* rec_flags, uint64_t* rec_index, uint64_t* rec_term,
+    uint64_t* rec_hint, uint64_t* rec_log_term, uint8_t* status, uint8_t* msg_type,
+    uint64_t* stats, void* stream) {
+  if (M == 0) return QB_OK;
+  QB_REQUIRE(msg_off && msg_group && rec_group && rec_flags && rec_index && rec_term && status,
+             "qb_dev_ingest_messages_rows: msg_off, msg_group, rec_* and status are required");
+  QB_REQUIRE(nbytes == 0 || bytes, "qb_dev_ingest_messages_rows: bytes is NULL");
+  QB_REQUIRE(G == 0 || (rows && ids), "qb_dev_ingest_messages_rows: rows and ids are required");
+  QB_REQUIRE((reinterpret_cast<uintptr_t>(rows) & 15u) == 0,
+             "qb_dev_ingest_messages_rows: rows must be 16-byte aligned");
+  wire::Args A{M, nbytes, G, bytes, reinterpret_cast<const u64*>(msg_off), msg_group, nullptr,
+               reinterpret_cast<const u64*>(ids), G ? reinterpret_cast<const u64*>(rows) : nullptr,
+               rec_group,
+               rec_flags, reinterpret_cast<u64*>(rec_index), reinterpret_cast<u64*>(rec_term),
                reinterpret_cast<u64*>(rec_hint), reinterpret_cast<u64*>(rec_log_term), status,
                msg_type, reinterpret_cast<u64*>(stats)};
   hipLaunchKernelGGL(wire::k_ingest, dim3(grid_for(M)), dim3(kBlock), 0, as_stream(stream), A);

@@ -26,10 +26,23 @@ def pack_messages(msgs, groups, device="cuda"):
             torch.from_numpy(np.asarray(groups, np.uint32).view(np.int32).copy()).to(dev))
 
 
+def group_rows(off: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """The 64-byte group-row table of a CSR slot-ID config
+    (qb_dev_wire_group_rows): build once per config, pass to ``ingest(rows=)``."""
+    G = off.numel() - 1
+    rows = torch.empty(max(G, 1) * 8, dtype=torch.int64, device=off.device)
+    _lib.call("qb_dev_wire_group_rows", G, off.data_ptr(), ids.data_ptr(), rows.data_ptr(),
+              torch.cuda.current_stream(off.device).cuda_stream)
+    return rows
+
+
 def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: torch.Tensor,
-           off: torch.Tensor, ids: torch.Tensor, stats: torch.Tensor = None):
+           off: torch.Tensor, ids: torch.Tensor, stats: torch.Tensor = None,
+           rows: torch.Tensor = None):
     """Decode M = len(msg_group) messages.  ``off`` [G+1] int32 and ``ids``
-    [off[G]] int64 are the groups' CSR slot IDs (ascending per group).
+    [off[G]] int64 are the groups' CSR slot IDs (ascending per group); with
+    ``rows`` (``group_rows(off, ids)``) each message gathers one 64-byte row
+    instead (qb_dev_ingest_messages_rows).
     Returns (LeaderInbox, status u8 tensor, msg_type u8 tensor)."""
     for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
         if not t.is_cuda:
@@ -43,11 +56,20 @@ def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: tor
     ri, rt, rh, rl = (torch.empty(n, dtype=torch.int64, device=dev) for _ in range(4))
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     mtype = torch.empty(n, dtype=torch.uint8, device=dev)
-    _lib.call("qb_dev_ingest_messages", M, buf.data_ptr(), nbytes, msg_off.data_ptr(),
-              msg_group.data_ptr(), G, off.data_ptr(), ids.data_ptr(), rg.data_ptr(),
-              rf.data_ptr(), ri.data_ptr(), rt.data_ptr(), rh.data_ptr(), rl.data_ptr(),
-              status.data_ptr(), mtype.data_ptr(), None if stats is None else stats.data_ptr(),
-              torch.cuda.current_stream(dev).cuda_stream)
+    if rows is None:
+        _lib.call("qb_dev_ingest_messages", M, buf.data_ptr(), nbytes, msg_off.data_ptr(),
+                  msg_group.data_ptr(), G, off.data_ptr(), ids.data_ptr(), rg.data_ptr(),
+                  rf.data_ptr(), ri.data_ptr(), rt.data_ptr(), rh.data_ptr(), rl.data_ptr(),
+                  status.data_ptr(), mtype.data_ptr(),
+                  None if stats is None else stats.data_ptr(),
+                  torch.cuda.current_stream(dev).cuda_stream)
+    else:
+        _lib.call("qb_dev_ingest_messages_rows", M, buf.data_ptr(), nbytes, msg_off.data_ptr(),
+                  msg_group.data_ptr(), G, rows.data_ptr(), ids.data_ptr(), rg.data_ptr(),
+                  rf.data_ptr(), ri.data_ptr(), rt.data_ptr(), rh.data_ptr(), rl.data_ptr(),
+                  status.data_ptr(), mtype.data_ptr(),
+                  None if stats is None else stats.data_ptr(),
+                  torch.cuda.current_stream(dev).cuda_stream)
     ib = LeaderInbox(rg, rf, ri, rt, rh, rl)
     ib._m = M
     return ib, status[:M], mtype[:M]

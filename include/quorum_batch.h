@@ -549,6 +549,23 @@ int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
                            uint64_t* rec_hint, uint64_t* rec_log_term,
                            uint8_t* status, uint8_t* msg_type, uint64_t* stats,
                            void* stream);
+/* The same ingest over a 64-byte group-row table built once per config
+ * (qb_dev_wire_group_rows: row g = member count | first slot << 32, then the
+ * first 7 member IDs; 16-byte aligned, qb_wire_group_rows_bytes(G)).  Each
+ * message then gathers one row instead of a row of off and one or two lines
+ * of ids; members past the 7th are still read from ids.  Rebuild the rows
+ * whenever off / ids change. */
+size_t qb_wire_group_rows_bytes(uint64_t G);
+int qb_dev_wire_group_rows(uint64_t G, const uint32_t* off, const uint64_t* ids,
+                           uint64_t* rows, void* stream);
+int qb_dev_ingest_messages_rows(uint64_t M, const uint8_t* bytes, uint64_t nbytes,
+                                const uint64_t* msg_off, const uint32_t* msg_group,
+                                uint64_t G, const uint64_t* rows, const uint64_t* ids,
+                                uint32_t* rec_group, uint8_t* rec_flags,
+                                uint64_t* rec_index, uint64_t* rec_term,
+                                uint64_t* rec_hint, uint64_t* rec_log_term,
+                                uint8_t* status, uint8_t* msg_type, uint64_t* stats,
+                                void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Configuration changes                             */

@@ -17,8 +17,8 @@ from tests.wire_gen import groups_ids as _groups_ids, random_message as _random_
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_ingest_matches_oracle(seed):
+@pytest.mark.parametrize("seed,rows", [(1, False), (2, False), (1, True), (3, True)])
+def test_ingest_matches_oracle(seed, rows):
     import torch
     from etcd_amd.quorum import wire
     r = random.Random(seed)
@@ -32,8 +32,10 @@ def test_ingest_matches_oracle(seed):
         groups.append(g)
     buf, nb, moff, mg = wire.pack_messages(msgs, groups)
     stats = torch.zeros(4, dtype=torch.int64, device="cuda")
-    ib, status, mtype = wire.ingest(buf, nb, moff, mg, torch.from_numpy(off.view(np.int32)).cuda(),
-                                    torch.from_numpy(ids.view(np.int64)).cuda(), stats)
+    d_off = torch.from_numpy(off.view(np.int32)).cuda()
+    d_ids = torch.from_numpy(ids.view(np.int64)).cuda()
+    ib, status, mtype = wire.ingest(buf, nb, moff, mg, d_off, d_ids, stats,
+                                    rows=wire.group_rows(d_off, d_ids) if rows else None)
     got = list(zip(status.cpu().numpy().tolist(), ib.group.cpu().numpy().view(np.uint32).tolist(),
                    ib.flags.cpu().numpy().tolist(),
                    ib.index.cpu().numpy().view(np.uint64).tolist(),
@@ -98,20 +100,23 @@ def test_ingest_then_leader_step_end_to_end():
     assert got == want
 
 
-def test_response_stream_full_size_vs_c_oracle():
+@pytest.mark.parametrize("rows", [False, True])
+def test_response_stream_full_size_vs_c_oracle(rows):
     """The bench workload (4M gogoproto-encoded responses to 1M leaders)
-    decoded on the device and by the C restatement: every column identical."""
+    decoded on the device (CSR slot IDs, or the 64-byte group rows) and by the
+    C restatement: every column identical."""
     import torch
     from etcd_amd.quorum import wire
     from tests import oracle_c as oc
     M, G = 1 << 22, 1 << 20
     buf, moff, grp, off, ids = wire.synth_response_stream(M, G)
     dev = "cuda"
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
     ib, status, _ = wire.ingest(torch.from_numpy(buf).to(dev), int(moff[-1]),
                                 torch.from_numpy(moff.view(np.int64)).to(dev),
-                                torch.from_numpy(grp.view(np.int32)).to(dev),
-                                torch.from_numpy(off.view(np.int32)).to(dev),
-                                torch.from_numpy(ids.view(np.int64)).to(dev))
+                                torch.from_numpy(grp.view(np.int32)).to(dev), d_off, d_ids,
+                                rows=wire.group_rows(d_off, d_ids) if rows else None)
     want = oc.ingest(buf, moff, grp, off, ids, threads=16)
     assert np.array_equal(status.cpu().numpy(), want["status"])
     assert int(want["status"].max()) == 0

@@ -1,0 +1,7 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r2l
+mkdir -p $O
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d $O/ld_sq1 -o run -- python3 tools/bench_configs.py --only leader --reps 3 --gpu-only > $O/ld_sq1.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/ld_sq2 -o run -- python3 tools/bench_configs.py --only leader --reps 3 --gpu-only > $O/ld_sq2.log 2>&1
+echo rc=$?
