@@ -286,3 +286,25 @@ def test_csr_step_full_size_16m_ragged():
     assert np.array_equal(batch.as_u64(tr.match)[: st["match"].size], st["match"])
     assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
     assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+
+
+@pytest.mark.parametrize("kind,G", [("ragged", 513), ("joint", 1537), ("ragged", 1)])
+def test_csr_step_empty_batch_is_commit_advance(kind, G):
+    """An empty batch (M = 0) through the CSR step: no record, so the state
+    is unchanged except the commit advance every group gets (the step's
+    maybeCommit equals commit_advance's) — here after the match rows were
+    raised behind the tracker's back."""
+    rng = np.random.default_rng(G)
+    off, cfg, sizes, st = _state(rng, kind, G)
+    tr = _tracker(off, cfg, st, track_next=False)
+    bump = st["match"] + rng.integers(0, 50, size=st["match"].size).astype(np.uint64)
+    tr.match[: bump.size].copy_(batch.from_u64(bump, DEV))
+    want = st["committed"].copy()
+    oc.csr_commit_all(off, cfg, bump, st["term_start"], want)
+    adv = torch.zeros(G, dtype=torch.uint8, device=DEV)
+    e = np.zeros(0)
+    tr.step(batch.AppRespBatch.from_numpy(e, e, e, e, device=DEV), adv)
+    assert np.array_equal(batch.as_u64(tr.committed), want)
+    assert np.array_equal(batch.as_u64(tr.match)[: bump.size], bump)
+    assert np.array_equal(adv.cpu().numpy().astype(bool), want != st["committed"])
+    assert all(v == 0 for v in tr.stats_dict().values())
