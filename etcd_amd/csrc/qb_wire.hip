@@ -278,6 +278,76 @@ __device__ __forceinline__ bool fast_prefix(const Src& s, u64& i, const u64 l, F
   return true;
 }
 
+// The fast prefix from the LDS stage, branch-free.  Each field is one
+// 8-byte window at a 32-bit stage offset (two aligned LDS reads): the key is
+// byte 0, the varint starts at byte 1 and ends at the lowest of bytes 1-7
+// with the high bit clear, its 7-bit groups compacted in three SWAR steps.
+// Every field is evaluated under a predicate instead of an early return (the
+// wire row is issue-bound once its group rows are one gather: the branchy
+// form spent as many scalar instructions on exec masks as vector ones): a
+// lane whose message leaves the canonical form — another key, a varint of 8+
+// bytes, a varint running past the message — simply stops consuming there,
+// and the generic loop (unmarshal<K_MESSAGE>) continues from that byte with
+// the generic decoder's result on any input.
+__device__ __forceinline__ u64 lds_win(const u8* lds, u32 o) {
+  const u64* w = reinterpret_cast<const u64*>(lds) + (o >> 3);
+  const u32 sh = (o & 7u) * 8u;
+  const u64 lo = w[0], hi = w[1];
+  return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+}
+__device__ __forceinline__ u64 varint_bits(u64 x) {  // x: the varint's bytes, higher bytes 0
+  x &= 0x7F7F7F7F7F7F7F7Full;
+  x = (x & 0x007F007F007F007Full) | ((x & 0x7F007F007F007F00ull) >> 1);
+  x = (x & 0x00003FFF00003FFFull) | ((x & 0x3FFF00003FFF0000ull) >> 2);
+  return (x & 0x000000000FFFFFFFull) | ((x & 0x0FFFFFFF00000000ull) >> 4);
+}
+// key byte `key`, then a varint: consumed into dst when the lane is still in
+// the canonical form (go) and the field is whole inside [o, e)
+__device__ __forceinline__ void fast_field(const u8* lds, u32& o, u32 e, bool& go, u32 key,
+                                           u64* dst) {
+  const u64 x = lds_win(lds, o);
+  const u64 stop = ~x & 0x8080808080808000ull;
+  const u32 t = stop ? u32(__builtin_ctzll(stop)) >> 3 : 8u;  // varint bytes (1..7; 8 = none)
+  const bool ok = go && u32(x & 0xFFu) == key && t < 8u && o + 1u + t <= e;
+  if (dst) {
+    const u64 v = varint_bits((x >> 8) & (~0ull >> (64u - 8u * (t < 8u ? t : 7u))));
+    *dst = ok ? v : *dst;
+  }
+  o = ok ? o + 1u + t : o;
+  go = ok;
+}
+
+template <>
+__device__ __forceinline__ bool fast_prefix<LdsSrc>(const LdsSrc& s, u64& i, const u64 l,
+                                                   Fields& f) {
+  u32 o = u32(i - s.base);
+  const u32 e = u32(l - s.base);
+  bool go = o < e;
+  fast_field(s.lds, o, e, go, 0x08, &f.type);
+  fast_field(s.lds, o, e, go, 0x10, nullptr);
+  fast_field(s.lds, o, e, go, 0x18, &f.from);
+  fast_field(s.lds, o, e, go, 0x20, &f.term);
+  fast_field(s.lds, o, e, go, 0x28, &f.log_term);
+  fast_field(s.lds, o, e, go, 0x30, &f.index);
+  fast_field(s.lds, o, e, go, 0x40, nullptr);
+  {  // the empty snapshot 4A 02 12 00
+    const bool ok = go && o + 4u <= e && u32(lds_win(s.lds, o)) == 0x0012024Au;
+    o = ok ? o + 4u : o;
+    go = ok;
+  }
+  fast_field(s.lds, o, e, go, 0x50, &f.reject);
+  fast_field(s.lds, o, e, go, 0x58, &f.hint);
+  {  // context (field 12, bytes) of the common 8-byte form
+    const bool ok = go && o + 10u <= e && u32(lds_win(s.lds, o) & 0xFFFFu) == 0x0862u;
+    f.has_ctx = ok;
+    f.ctx_pos = ok ? s.base + o + 2u : 0ull;
+    f.ctx_len = ok ? 8ull : 0ull;
+    o = ok ? o + 10u : o;
+  }
+  i = s.base + o;
+  return true;  // errors are the generic loop's to find
+}
+
 // The 8 bytes at i as a big-endian u64 (the read context's request id).
 template <class Src>
 __device__ __forceinline__ u64 load_be64(const Src& s, u64 i) {
