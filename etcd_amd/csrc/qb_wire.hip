@@ -330,9 +330,16 @@ __device__ __forceinline__ bool fast_prefix<LdsSrc>(const LdsSrc& s, u64& i, con
   fast_field(s.lds, o, e, go, 0x28, &f.log_term);
   fast_field(s.lds, o, e, go, 0x30, &f.index);
   fast_field(s.lds, o, e, go, 0x40, nullptr);
-  {  // the empty snapshot 4A 02 12 00
-    const bool ok = go && o + 4u <= e && u32(lds_win(s.lds, o)) == 0x0012024Au;
-    o = ok ? o + 4u : o;
+  {  // the zero Snapshot as gogoproto writes it — Metadata and its ConfState
+     // are non-nullable, AutoLeave / Index / Term always present:
+     // 4A 0A 12 08 0A 02 28 00 10 00 18 00 — or with an empty Metadata,
+     // 4A 02 12 00 (any encoding of it decodes the same)
+    const u64 x = lds_win(s.lds, o);
+    const u32 y = u32(lds_win(s.lds, o + 8u));
+    const bool full = o + 12u <= e && x == 0x0028020A08120A4Aull && y == 0x00180010u;
+    const bool brief = o + 4u <= e && u32(x) == 0x0012024Au;
+    const bool ok = go && (full || brief);
+    o = ok ? o + (full ? 12u : 4u) : o;
     go = ok;
   }
   fast_field(s.lds, o, e, go, 0x50, &f.reject);
@@ -410,23 +417,39 @@ struct GroupRow {
   u64 id[kIdBatch];
 };
 
+// A message the first launch leaves to the second (status value between the
+// launches only; never returned).
+constexpr u8 kDeferred = 0xFF;
+
 // One message: decode, classify, map From to its slot, write the record.
-template <class Src>
+// GENERIC = false (the first launch): a message the branch-free fast prefix
+// does not consume whole is deferred — status kDeferred, nothing else
+// written — to the second launch, which decodes it with the generic loop.
+// Keeping the generic decoder (every nested kind inlined) out of the first
+// launch's code is worth 22 % of the row: its mere presence cost registers
+// and instruction-cache footprint though canonical messages never enter it.
+template <class Src, bool GENERIC>
 __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u64 p0, u64 p1,
                                           GroupRow& row) {
-  Fields f;
+  Fields f = Fields{};
   int st_;
   u32 group = 0xFFFFFFFFu;
   u8 flags = 0;
   u64 index = 0, term = 0, hint = 0, lterm = 0;
-#ifdef QB_WIRE_LAB_NOPARSE  // development: the kernel without the decoder
-  f = Fields{};
-  f.type = 4;
-  f.from = u64(s.at(p0 + 5)) + 16384u;
-  if (p1 < p0 || p1 > A.nbytes) {
-#else
-  if (p1 < p0 || p1 > A.nbytes || !unmarshal_message(s, p0, p1, f)) {
-#endif
+  bool ok = p0 <= p1 && p1 <= A.nbytes;
+  if (ok) {
+    u64 i = p0;
+    ok = fast_prefix(s, i, p1, f);
+    if (ok && i < p1) {
+      if constexpr (!GENERIC) {
+        __builtin_nontemporal_store(kDeferred, A.status + m);
+        return kDeferred;
+      } else {
+        ok = unmarshal<K_MESSAGE>(s, i, p1, &f);
+      }
+    }
+  }
+  if (!ok) {
     st_ = QB_WIRE_UNMARSHAL;
     if (A.mtype) __builtin_nontemporal_store(u8(0), A.mtype + m);
   } else {
@@ -479,21 +502,9 @@ __device__ __forceinline__ int ingest_one(const Args& A, const Src& s, u64 m, u6
   return st_;
 }
 
-// Round trips per workgroup: (1) the message offsets and groups; (2) the
-// groups' slot ranges beside the LDS-DMA stage of the byte span; (3) the
-// member IDs, in flight while the messages are parsed from LDS.
-__global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
-  __shared__ __attribute__((aligned(16))) u8 stage[kStage + 16];  // + window over-read
-  __shared__ u32 lds[4];
-  BlockTally<4> tally;
-  const u64 m0 = u64(blockIdx.x) * kBlock;
-  const u64 m = m0 + threadIdx.x;
-  const u64 mlast = (m0 + kBlock < A.M ? m0 + kBlock : A.M);
-  const u64 mc = m < A.M ? m : A.M - 1;  // lanes past M re-read the last message
-  const u64 b0 = A.moff[m0], b1 = A.moff[mlast];
-  const u64 p0 = __builtin_nontemporal_load(A.moff + mc);
-  const u64 p1 = __builtin_nontemporal_load(A.moff + mc + 1);
-  GroupRow row;
+// The group row of message mc: the 64-byte row, or the slot range (off)
+// with the IDs read by load_ids after it.
+__device__ __forceinline__ void load_row(const Args& A, u64 mc, GroupRow& row) {
   row.mg = __builtin_nontemporal_load(A.mgroup + mc);
   if (A.rows) {
     // the group's 64-byte row: one aligned line segment per message instead
@@ -518,6 +529,33 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     row.s0 = offp[gi];
     row.s1 = offp[gi + 1];
   }
+}
+__device__ __forceinline__ void load_ids(const Args& A, GroupRow& row) {
+  if (!A.rows) {
+    const u32 n = row.mg < A.G ? row.s1 - row.s0 : 0u;
+    const u64* idp = n ? A.ids + row.s0 : A.moff;
+#pragma unroll
+    for (u32 k = 0; k < kIdBatch; ++k) row.id[k] = idp[n ? (k < n ? k : n - 1) : 0u];
+  }
+}
+
+// First launch.  Round trips per workgroup: (1) the message offsets and
+// groups; (2) the groups' rows beside the LDS-DMA stage of the byte span;
+// (3) (CSR IDs only) the member IDs, in flight while the messages are parsed
+// from LDS.  A message outside the staged span is deferred too.
+__global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
+  __shared__ __attribute__((aligned(16))) u8 stage[kStage + 48];  // + window over-reads (<= 24 B past a message)
+  __shared__ u32 lds[4];
+  BlockTally<4> tally;
+  const u64 m0 = u64(blockIdx.x) * kBlock;
+  const u64 m = m0 + threadIdx.x;
+  const u64 mlast = (m0 + kBlock < A.M ? m0 + kBlock : A.M);
+  const u64 mc = m < A.M ? m : A.M - 1;  // lanes past M re-read the last message
+  const u64 b0 = A.moff[m0], b1 = A.moff[mlast];
+  const u64 p0 = __builtin_nontemporal_load(A.moff + mc);
+  const u64 p1 = __builtin_nontemporal_load(A.moff + mc + 1);
+  GroupRow row;
+  load_row(A, mc, row);
   // Stage the block's byte span [b0, b1) when it fits (block-uniform).
   u64 lbase = 0, lend = 0;  // staged span (empty: nothing staged)
   if (b1 > b0 && b1 - b0 <= kStage - 16) {
@@ -545,18 +583,14 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     lend = a1 < A.nbytes ? a1 : A.nbytes;
   }
   __syncthreads();
-  if (!A.rows) {
-    const u32 n = row.mg < A.G ? row.s1 - row.s0 : 0u;
-    const u64* idp = n ? A.ids + row.s0 : A.moff;
-#pragma unroll
-    for (u32 k = 0; k < kIdBatch; ++k) row.id[k] = idp[n ? (k < n ? k : n - 1) : 0u];
-  }
+  load_ids(A, row);
   int st_ = -1;
   if (m < A.M) {
-    if (p0 >= lbase && p1 <= lend && p0 <= p1)
-      st_ = ingest_one(A, LdsSrc{stage, lbase}, m, p0, p1, row);
-    else
-      st_ = ingest_one(A, GlobalSrc{A.bytes}, m, p0, p1, row);
+    if (p0 >= lbase && p1 <= lend && p0 <= p1) {
+      st_ = ingest_one<LdsSrc, false>(A, LdsSrc{stage, lbase}, m, p0, p1, row);
+    } else {
+      __builtin_nontemporal_store(kDeferred, A.status + m);
+    }
   }
   tally.add(0, st_ == QB_WIRE_OK);
   tally.add(1, st_ == QB_WIRE_UNMARSHAL);
@@ -564,6 +598,42 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
   tally.add(3, st_ == QB_WIRE_CTX);
   const int slot[4] = {QB_WIRE_OK, QB_WIRE_UNMARSHAL, QB_WIRE_TYPE, QB_WIRE_CTX};
   if (A.stats) tally.flush(lds, A.stats, slot);
+}
+
+// Second launch: the deferred messages, each decoded from global memory by
+// the generic loop.  A thread scans kScan consecutive statuses (loaded
+// together); with nothing deferred the launch reads the status column once.
+constexpr u32 kScan = 16;
+__global__ __launch_bounds__(kBlock) void k_ingest_deferred(Args A) {
+  __shared__ u32 lds[4];
+  const u64 m0 = (u64(blockIdx.x) * kBlock + threadIdx.x) * kScan;
+  u8 st[kScan];
+#pragma unroll
+  for (u32 k = 0; k < kScan; ++k) st[k] = m0 + k < A.M ? A.status[m0 + k] : u8(0);
+  u32 cnt[4] = {0, 0, 0, 0};
+  for (u32 k = 0; k < kScan; ++k) {
+    if (st[k] != kDeferred) continue;
+    const u64 m = m0 + k;
+    GroupRow row;
+    load_row(A, m, row);
+    load_ids(A, row);
+    const int r = ingest_one<GlobalSrc, true>(A, GlobalSrc{A.bytes}, m, A.moff[m], A.moff[m + 1],
+                                              row);
+    ++cnt[r];
+  }
+  if (!A.stats) return;
+  if (threadIdx.x < 4) lds[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    u32 v = cnt[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&lds[q], v);
+  }
+  __syncthreads();
+  // statuses 0..3 are the stat slots QB_WIRE_OK .. QB_WIRE_CTX
+  if (threadIdx.x < 4 && lds[threadIdx.x]) atomicAdd(A.stats + threadIdx.x, u64(lds[threadIdx.x]));
 }
 
 }  // namespace wire
@@ -585,6 +655,19 @@ __global__ __launch_bounds__(kBlock) void k_group_rows(u64 G, const u32* __restr
   ulonglong2* dst = reinterpret_cast<ulonglong2*>(rows + 8 * g);
 #pragma unroll
   for (u32 q = 0; q < 4; ++q) dst[q] = ulonglong2{w[2 * q], w[2 * q + 1]};
+}
+}  // namespace wire
+}  // namespace qb
+
+namespace qb {
+namespace wire {
+static int launch(const Args& A, hipStream_t st) {
+  hipLaunchKernelGGL(k_ingest, dim3(grid_for(A.M)), dim3(kBlock), 0, st, A);
+  QB_CHECK_LAUNCH("k_ingest");
+  hipLaunchKernelGGL(k_ingest_deferred, dim3(grid_for((A.M + kScan - 1) / kScan)), dim3(kBlock), 0,
+                     st, A);
+  QB_CHECK_LAUNCH("k_ingest_deferred");
+  return QB_OK;
 }
 }  // namespace wire
 }  // namespace qb
@@ -630,9 +713,7 @@ extern "C" int qb_dev_ingest_messages(uint64_t M, const uint8_t* bytes, uint64_t
                reinterpret_cast<u64*>(rec_index), reinterpret_cast<u64*>(rec_term),
                reinterpret_cast<u64*>(rec_hint), reinterpret_cast<u64*>(rec_log_term), status,
                msg_type, reinterpret_cast<u64*>(stats)};
-  hipLaunchKernelGGL(wire::k_ingest, dim3(grid_for(M)), dim3(kBlock), 0, as_stream(stream), A);
-  QB_CHECK_LAUNCH("k_ingest");
-  return QB_OK;
+  return wire::launch(A, as_stream(stream));
 }
 
 extern "C" int qb_dev_ingest_messages_rows(
@@ -654,7 +735,5 @@ extern "C" int qb_dev_ingest_messages_rows(
                rec_flags, reinterpret_cast<u64*>(rec_index), reinterpret_cast<u64*>(rec_term),
                reinterpret_cast<u64*>(rec_hint), reinterpret_cast<u64*>(rec_log_term), status,
                msg_type, reinterpret_cast<u64*>(stats)};
-  hipLaunchKernelGGL(wire::k_ingest, dim3(grid_for(M)), dim3(kBlock), 0, as_stream(stream), A);
-  QB_CHECK_LAUNCH("k_ingest");
-  return QB_OK;
+  return wire::launch(A, as_stream(stream));
 }
