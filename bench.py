@@ -641,7 +641,8 @@ def main():
             cfg = {"workload": "BASELINE configs[1]: 1M groups x 5 voters CommittedIndex + "
                                "VoteResult, uint64 indexes, one MI355X per shard",
                    "groups_per_gpu": G, "voters": n, "layout": "fixed slot-major SoA"}
-            kname = f"k_fixed<{n},2,true,true>"
+            kname = (f"k_fixed_lds<{n},{4 if n <= 5 else 2},true>" if n <= 8
+                     else f"k_fixed<{n},2,true,true>")
         cfg.update({"batches_resident": B, "streams": S, "graph_steps": args.graph,
                     "parallelism": f"groups sharded by id over {world} GPU(s)"})
         achieved = bpg * G / avg_kernel_s / 1e9

@@ -135,6 +135,88 @@ __global__ __launch_bounds__(kBlock) void k_fixed(const u64* __restrict__ match,
   }
 }
 
+// LDS-DMA form (CommittedIndex wanted, n <= 8, aligned operands): a
+// workgroup owns kBlock * GPT consecutive groups; each slot row's slice for
+// them (kBlock * GPT * 8 contiguous bytes) lands in LDS by
+// global_load_lds_dwordx4, all N rows issued before the one wait, and a lane
+// reads back the groups its own 16-byte pieces landed (piece k of lane t =
+// groups 2 (k kBlock + t) and +1).  Longer contiguous row slices than the
+// register form's one dwordx4 per row and lane, and no VGPRs held by the
+// loads: 1M groups 8.7-8.9 -> 8.5 us, 16M 146 -> 141 us
+// (`profiles/r02/ab_fixed_ldsdma.log`).
+template <int N, int GPT, bool VOTE>
+__global__ __launch_bounds__(kBlock) void k_fixed_lds(const u64* __restrict__ match, u64 G,
+                                                      const MaskT<N>* __restrict__ voted,
+                                                      const MaskT<N>* __restrict__ granted,
+                                                      u64* __restrict__ commit,
+                                                      u8* __restrict__ vote) {
+  using M = MaskT<N>;
+  constexpr int kPer = GPT / 2;  // 16-byte pieces per lane and row
+  constexpr u32 kSpan = u32(kBlock) * GPT;
+  __shared__ __attribute__((aligned(16))) u64 lds[N][kSpan];
+  const u64 gb = u64(blockIdx.x) * kSpan;
+  if (gb + kSpan > G) {  // the tail workgroup (block-uniform): group by group
+    const u64 g0 = gb + u64(threadIdx.x) * GPT;
+    for (u64 g = g0; g < G && g < g0 + GPT; ++g) {
+      u64 v[N];
+#pragma unroll
+      for (int s = 0; s < N; ++s) v[s] = match[u64(s) * G + g];
+      u64 ci;
+      u8 vr;
+      eval_fixed<N, true, VOTE>(v, VOTE ? u32(voted[g]) : 0u, VOTE ? u32(granted[g]) : 0u, ci, vr);
+      commit[g] = ci;
+      if constexpr (VOTE) vote[g] = vr;
+    }
+    return;
+  }
+  M vd[GPT], gr[GPT];
+  if constexpr (VOTE) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const u64 ge = gb + 2ull * (u32(k) * kBlock + threadIdx.x);
+      M a[2], b[2];
+      vload<M, 2>(voted + ge, a);
+      vload<M, 2>(granted + ge, b);
+      vd[2 * k] = a[0];
+      vd[2 * k + 1] = a[1];
+      gr[2 * k] = b[0];
+      gr[2 * k + 1] = b[1];
+    }
+  }
+  const u32 wave_base = threadIdx.x & ~63u;
+#pragma unroll
+  for (int s = 0; s < N; ++s)
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const u32 piece = u32(k) * kBlock + threadIdx.x;
+      char* dst = reinterpret_cast<char*>(&lds[s][0]) + 16u * (u32(k) * kBlock + wave_base);
+      __builtin_amdgcn_global_load_lds(
+          (gbl_cvoid_t*)(reinterpret_cast<const char*>(match + u64(s) * G + gb) + 16ull * piece),
+          (lds_void_t*)dst, 16, 0, 2);
+    }
+  __syncthreads();
+  u64 ci[GPT];
+  u8 vr[GPT];
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const u32 e = 2u * (u32(j / 2) * kBlock + threadIdx.x) + u32(j & 1);
+    u64 v[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) v[s] = lds[s][e];
+    eval_fixed<N, true, VOTE>(v, VOTE ? u32(vd[j]) : 0u, VOTE ? u32(gr[j]) : 0u, ci[j], vr[j]);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const u64 ge = gb + 2ull * (u32(k) * kBlock + threadIdx.x);
+    const u64 c2[2] = {ci[2 * k], ci[2 * k + 1]};
+    vstore<u64, 2>(commit + ge, c2);
+    if constexpr (VOTE) {
+      const u8 v2[2] = {vr[2 * k], vr[2 * k + 1]};
+      vstore<u8, 2>(vote + ge, v2);
+    }
+  }
+}
+
 // Empty config (n == 0): CommittedIndex = ∞, VoteResult = VoteWon
 // (majority.go:128-133, 179-184).
 __global__ void k_fill_empty(u64 G, u64* __restrict__ commit, u8* __restrict__ vote) {
@@ -157,6 +239,21 @@ template <int N>
 static void launch_fixed_n(u64 G, const u64* match, const void* voted, const void* granted,
                            u64* commit, u8* vote, bool vec, hipStream_t st) {
   const bool ci = commit != nullptr, vt = vote != nullptr;
+  if constexpr (N <= 8) {
+    if (vec && ci) {
+      constexpr int GPT = N <= 5 ? 4 : 2;
+      const dim3 grid(unsigned((G + u64(kBlock) * GPT - 1) / (u64(kBlock) * GPT)));
+      const auto* vd = static_cast<const MaskT<N>*>(voted);
+      const auto* gr = static_cast<const MaskT<N>*>(granted);
+      if (vt)
+        hipLaunchKernelGGL((k_fixed_lds<N, GPT, true>), grid, dim3(kBlock), 0, st, match, G, vd, gr,
+                           commit, vote);
+      else
+        hipLaunchKernelGGL((k_fixed_lds<N, GPT, false>), grid, dim3(kBlock), 0, st, match, G, vd,
+                           gr, commit, vote);
+      return;
+    }
+  }
   // GPT = 2: one dwordx4 per slot row, 2-4 byte mask/vote chunks.  Measured
   // best of {1,2,4,8} x {plain,nt} for n = 5.
   if (vec) {

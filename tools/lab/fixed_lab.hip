@@ -111,6 +111,95 @@ __global__ __launch_bounds__(BLOCK) void k_var1(const u64* __restrict__ match, u
   }
 }
 
+// LDS-DMA: each slot row's slice for the workgroup (BLOCK * GPT u64) goes
+// global -> LDS by global_load_lds_dwordx4 (AUX: cache policy bits), every
+// row issued before the one wait; each thread then reads back the GPT groups
+// its own lanes landed (LDS is only the landing buffer).
+template <int GPT, int AUX, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_ldsdma(const u64* __restrict__ match, u64 G,
+                                                  const u8* __restrict__ voted,
+                                                  const u8* __restrict__ granted,
+                                                  u64* __restrict__ commit, u8* __restrict__ vote,
+                                                  u64) {
+  using MaskV = std::conditional_t<GPT == 2, u16, std::conditional_t<GPT == 4, u32, u64>>;
+  constexpr int kPer = GPT / 2;  // 16-byte pieces per lane per row
+  __shared__ __attribute__((aligned(16))) u64 lds[N][BLOCK * GPT];
+  const u64 gb = u64(blockIdx.x) * BLOCK * GPT;
+  const u64 g0 = gb + u64(threadIdx.x) * GPT;
+  const bool full = gb + BLOCK * GPT <= G;
+  MaskV vdw = 0, grw = 0;  // bytes of the groups in this lane's pieces
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const u64 ge = gb + 2ull * (u32(k) * BLOCK + threadIdx.x);
+      vdw |= MaskV(ldT<true>(reinterpret_cast<const u16*>(voted + ge))) << (16 * k);
+      grw |= MaskV(ldT<true>(reinterpret_cast<const u16*>(granted + ge))) << (16 * k);
+    }
+  }
+  const u32 wave_base = threadIdx.x & ~63u;
+  if (full) {
+#pragma unroll
+    for (int s = 0; s < N; ++s)
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const u32 piece = u32(k) * BLOCK + threadIdx.x;  // 16-byte piece of this row slice
+        char* dst = reinterpret_cast<char*>(&lds[s][0]) + 16u * (u32(k) * BLOCK + wave_base);
+        __builtin_amdgcn_global_load_lds(
+            (gbl_cvoid_t*)(reinterpret_cast<const char*>(match + u64(s) * G + gb) + 16ull * piece),
+            (lds_void_t*)dst, 16, 0, AUX);
+      }
+  }
+  __syncthreads();
+  if (!full) {
+    for (u64 g = g0; g < G && g < g0 + GPT; ++g) {
+      u64 v[N];
+#pragma unroll
+      for (int s = 0; s < N; ++s) v[s] = match[u64(s) * G + g];
+      commit[g] = select_quorum<N>(v);
+      vote[g] = vote5(voted[g], granted[g]);
+    }
+    return;
+  }
+  u64 ci[GPT];
+  MaskV vo = 0;
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    // group g0 + j sits in piece (j / 2) * BLOCK + tid ... only when GPT == 2;
+    // for GPT == 4 the pieces of a lane are BLOCK apart.
+    const u32 e = 2u * (u32(j / 2) * BLOCK + threadIdx.x) + u32(j & 1);
+    u64 v[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) v[s] = lds[s][e];
+    ci[j] = select_quorum<N>(v);
+    const u32 vd = u32(vdw >> (8 * j)) & 0xFFu, gr = u32(grw >> (8 * j)) & 0xFFu;
+    vo |= MaskV(vote5(vd, gr)) << (8 * j);
+  }
+  // outputs in the same piece order as the loads
+  using V = u32 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    V x;
+    x.x = u32(ci[2 * k]);
+    x.y = u32(ci[2 * k] >> 32);
+    x.z = u32(ci[2 * k + 1]);
+    x.w = u32(ci[2 * k + 1] >> 32);
+    const u64 ge = gb + 2ull * (u32(k) * BLOCK + threadIdx.x);
+    stT<true>(reinterpret_cast<V*>(commit + ge), x);
+  }
+  // vote bytes of groups (2*(k*BLOCK+tid), +1), piece by piece
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    stT<true>(reinterpret_cast<u16*>(vote + gb + 2ull * (u32(k) * BLOCK + threadIdx.x)),
+              u16(vo >> (16 * k)));
+}
+
+template <int GPT, int AUX, int BLOCK>
+void launch_ldsdma(const u64* m, u64 G, const u8* vd, const u8* gr, u64* c, u8* v, hipStream_t st) {
+  const u64 blocks = (G + u64(BLOCK) * GPT - 1) / (u64(BLOCK) * GPT);
+  hipLaunchKernelGGL((k_ldsdma<GPT, AUX, BLOCK>), dim3(unsigned(blocks)), dim3(BLOCK), 0, st, m, G,
+                     vd, gr, c, v, 0ull);
+}
+
 struct Variant {
   const char* name;
   void (*launch)(const u64*, u64, const u8*, const u8*, u64*, u8*, hipStream_t);
@@ -148,6 +237,15 @@ const Variant kVariants[] = {
     {"gpt8_nt", launch_var<8, true, false, true, 256, 0>},
     {"gpt2_nt_b512", launch_var<2, true, false, true, 512, 0>},
     {"gpt2_nt_nts", launch_var<2, true, true, true, 256, 0>},
+    {"ldsdma2_nt", launch_ldsdma<2, 2, 256>},
+    {"ldsdma2", launch_ldsdma<2, 0, 256>},
+    {"ldsdma2_b512", launch_ldsdma<2, 2, 512>},
+    {"ldsdma4_nt", launch_ldsdma<4, 2, 256>},
+    {"ldsdma4_b512", launch_ldsdma<4, 2, 512>},
+    {"ldsdma4_b128", launch_ldsdma<4, 2, 128>},
+    {"ldsdma8_b128", launch_ldsdma<8, 2, 128>},
+    {"ldsdma8_nt", launch_ldsdma<8, 2, 256>},
+    {"ldsdma4_aux1", launch_ldsdma<4, 1, 256>},
     {"floor_gpt4", launch_var<4, false, false, false, 256, 0>},
     {"floor_gpt2", launch_var<2, false, false, false, 256, 0>},
     {"floor_gpt2_nt", launch_var<2, true, false, false, 256, 0>},
