@@ -39,6 +39,32 @@ __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
+// with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles
+// t, t+1, ... run on one XCD: the partial 128-byte lines that neighbouring
+// tiles write into the same bucket (K3 runs, K1 histogram columns) meet in
+// that XCD's L2 instead of reaching HBM as separate partial writes.  The grid
+// must be a multiple of kXcds (Geometry::tile_grid); logical tiles >= the real count exit.
+// Used only when a tile's mean run per super-bucket is shorter than two lines
+// (kTile / NSB < 32 u64): config 5 (NSB = 256, 16-record runs) K3 241 -> 200
+// us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
+// 41 -> 55 us with it, so it keeps the linear order.
+constexpr u32 kXcds = 8;
+// interleaved super-buckets (Geometry::il) for the tracker steps
+#ifndef QB_SB_IL
+#define QB_SB_IL 1
+#endif
+constexpr bool kSbIl = QB_SB_IL != 0;
+// K5 write-back granularity (k_bk_apply, k_csr_apply): 0 = changed values
+// only; 1 = committed / active as whole wave segments where any changed; 2 =
+// the slot rows too
+#ifndef QB_K5_FULL
+#define QB_K5_FULL 2
+#endif
+__device__ __forceinline__ u32 xcd_major() {
+  return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
+}
+
 // Groups per K5 chunk (one workgroup; its LDS holds n accumulators per group).
 #ifndef QB_CH_NARROW
 #define QB_CH_NARROW 512
@@ -57,21 +83,6 @@ __host__ __device__ constexpr u32 csr_chunk_groups(u32 wmax) {
   return wmax <= 8 ? 512u : u32(QB_CSR_CH_WIDE);
 }
 
-// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
-// with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles
-// t, t+1, ... run on one XCD: the partial 128-byte lines that neighbouring
-// tiles write into the same bucket (K3 runs, K1 histogram columns) meet in
-// that XCD's L2 instead of reaching HBM as separate partial writes.  The grid
-// must be a multiple of kXcds (Geometry::tile_grid); logical tiles >= the real count exit.
-// Used only when a tile's mean run per super-bucket is shorter than two lines
-// (kTile / NSB < 32 u64): config 5 (NSB = 256, 16-record runs) K3 241 -> 200
-// us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
-// 41 -> 55 us with it, so it keeps the linear order.
-constexpr u32 kXcds = 8;
-__device__ __forceinline__ u32 xcd_major() {
-  return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
-}
-
 struct Geometry {
   u64 G, M;
   u32 n, CH, NC, NSB, NT;
@@ -79,15 +90,26 @@ struct Geometry {
   // CH and CH * kChunksPerSb are powers of two: group -> chunk / super-bucket
   // by shifts (a runtime u32 division is ~30 VALU instructions per record)
   u32 ch_shift, sb_shift;
+  // il (interleaved super-buckets): super-bucket = the chunks of one XCD
+  // within a window of 1024 consecutive chunks, i.e. chunk c is (c & 7) |
+  // (c >> 10) << 3, chunk-low (c >> 3) & 127.  K5 dispatches chunk c as
+  // workgroup c, round-robin over the XCDs, so a super-bucket's 128 chunks
+  // run together on one XCD while K5 still walks the state in memory order.
+  u32 il;
   __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
-  __host__ __device__ u32 sb_of(u32 g) const { return g >> sb_shift; }
+  __host__ __device__ u32 sb_of_chunk(u32 c) const {
+    return il ? (c & (kXcds - 1u)) | ((c >> 10) << 3) : c >> 7;
+  }
+  __host__ __device__ u32 cl_of_chunk(u32 c) const { return il ? (c >> 3) & 127u : c & 127u; }
+  __host__ __device__ u32 sb_of(u32 g) const { return il ? sb_of_chunk(g >> ch_shift) : g >> sb_shift; }
   __host__ __device__ u64 nbins() const { return u64(NSB) * NT; }
   u32 tile_grid() const { return xcd ? (NT + kXcds - 1) / kXcds * kXcds : NT; }
   __device__ __forceinline__ u32 tile() const { return xcd ? xcd_major() : blockIdx.x; }
 };
 
-inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0) {
+inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   Geometry g{};
+  g.il = il;
   g.G = G;
   g.M = M;
   g.n = n;
@@ -97,7 +119,8 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0) {
   g.sb_shift = g.ch_shift + 7;
   static_assert(kChunksPerSb == 128, "sb_shift = ch_shift + log2(kChunksPerSb)");
   g.NC = u32((G + g.CH - 1) / g.CH);
-  g.NSB = (g.NC + kChunksPerSb - 1) / kChunksPerSb;
+  g.NSB = il ? (g.NC + 1023u) / 1024u * kXcds : (g.NC + kChunksPerSb - 1) / kChunksPerSb;
+  static_assert(kChunksPerSb * 8 == 1024, "il: 8 XCDs x 128 chunks per window");
   g.NT = u32((M + kTile - 1) / kTile);
   g.xcd = g.NSB > 0 && u32(kTile) / g.NSB < 32u;
   return g;
@@ -182,12 +205,62 @@ struct RunTable {
     __syncthreads();
     return pre[n];
   }
+  // build() in two halves, for a caller that wants the run table's loads in
+  // flight ahead of its own bulk loads (vector loads retire in order, so a
+  // wait for loads issued after the bulk would wait for the bulk too):
+  // issue() loads lane r's run (every wave, branch-free: an empty table reads
+  // row 0 and counts nothing); finish() scans the lengths and wave 0 publishes
+  // the table.  The caller synchronises before locate().
+  struct Regs {
+    u32 l, len, n;
+  };
+  __device__ __forceinline__ static Regs issue(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
+    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
+    const u32 r = threadIdx.x & 63u;
+    const u64 row0 = n ? u64(pb + (r < n ? r : 0u)) * (kChunksPerSb + 1) : 0ull;
+    const u32 l = cs[row0 + cl], h = cs[row0 + cl + 1];
+    return Regs{l, r < n ? h - l : 0u, n};
+  }
+  __device__ __forceinline__ u32 finish(const Regs& q) {
+    const u32 r = threadIdx.x & 63u;
+    u32 x = q.len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = u32(__shfl_up(int(x), o, 64));
+      if (r >= u32(o)) x += y;
+    }
+    if (threadIdx.x < 64) {
+      if (r < q.n) {
+        lo[r] = q.l;
+        pre[r + 1] = x;
+      }
+      if (r == 0) {
+        pre[0] = 0;
+        nr = q.n;
+      }
+    }
+    return u32(__shfl(int(x), 63, 64));  // lengths past n are 0
+  }
   __device__ __forceinline__ u32 locate(u32 f) const {
     u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
     while (b - a > 1) {
       const u32 m = (a + b) >> 1;
       if (pre[m] <= f) a = m;
       else b = m;
+    }
+    return lo[a] + (f - pre[a]);
+  }
+  // locate() unrolled for a caller in straight-line code (no loop: exact
+  // wait counts); nr <= kRuns = 64.
+  __device__ __forceinline__ u32 locate_fixed(u32 f) const {
+    static_assert(kRuns == 64, "six halvings");
+    const u32 n = nr;
+    u32 a = 0;
+#pragma unroll
+    for (u32 st = 32; st >= 1; st >>= 1) {
+      const u32 m = a + st;
+      const u32 pm = pre[m < n ? m : 0u];
+      a = m < n && pm <= f ? m : a;
     }
     return lo[a] + (f - pre[a]);
   }
@@ -208,6 +281,7 @@ struct RunTable {
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
                    hipStream_t st, bool term32 = false, bool packed = false);
+
 
 }  // namespace bk
 }  // namespace qb

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
         v[j] = vt[j];
       } else {
         const u32 chunk = geo.chunk_of(g[j]);
-        const u32 meta = (g[j] & (geo.CH - 1u)) | ((chunk % kChunksPerSb) << 10) |
+        const u32 meta = (g[j] & (geo.CH - 1u)) | (geo.cl_of_chunk(chunk) << 10) |
                          ((f[j] & 0xFFu) << 17);
         v[j] = u64(meta) | (u64(out.packed ? term_to32(vt[j]) : u32(t0 + k)) << 32);
       }
@@ -507,6 +507,15 @@ __host__ __device__ constexpr u32 k5_block(int n) {
   return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
 }
 
+template <typename T>
+__device__ __forceinline__ void k5_store(T* p, T v) {
+#ifdef QB_K5_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <int N, bool NEXT>
 __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
@@ -527,88 +536,125 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   const u32 c = blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
-  // The commit phase's loads (match rows, committed, term_start) are issued
-  // now, so their latency overlaps the record pass instead of following it.
-  // (RecentActive's read-modify-write reads its word here too, not after
-  // the record pass)
+  // Load order: the group terms and this chunk's run table first, then the
+  // commit phase's state (match rows, committed, term_start, RecentActive's
+  // word), so the record pass waits for its own inputs only — vector loads
+  // retire in order, and with the state issued first every wait of the
+  // record chain (run table, then records) also waited for the state.  The
+  // state's latency runs under the record pass.  Loads are branch-free
+  // (clamped to the chunk's last group): exact wait counts need straight-line
+  // code.
+  const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
+  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  u64 gtr[GPT];
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * B;
+    gtr[k] = group_term[g0 + (lg < ng ? lg : ng - 1)];
+  }
+  __shared__ RunTable rt;
+  const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
   u64 v[GPT][N], cm[GPT], ts[GPT];
   u32 av[GPT];
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
     const u32 lg = threadIdx.x + k * B;
-    const u64 g = g0 + lg;
-    const bool live = lg < ng;
+    const u64 g = g0 + (lg < ng ? lg : ng - 1);
 #pragma unroll
-    for (int s = 0; s < N; ++s) v[k][s] = live ? match[u64(s) * geo.G + g] : 0ull;
-    cm[k] = live ? committed[g] : 0ull;
-    ts[k] = live ? term_start[g] : 0ull;
-    av[k] = live ? active[g] : 0u;
+    for (int s = 0; s < N; ++s) v[k][s] = match[u64(s) * geo.G + g];
+    cm[k] = committed[g];
+    ts[k] = term_start[g];
+    av[k] = active[g];
   }
   for (u32 k = threadIdx.x; k < N * CH; k += B) {
     acc_m[k] = 0;
     if constexpr (NEXT) acc_n[k] = 0;
   }
-  for (u32 k = threadIdx.x; k < CH; k += B) {
-    gterm[k] = k < ng ? group_term[g0 + k] : 0ull;
-    act[k] = 0;
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    gterm[threadIdx.x + k * B] = gtr[k];
+    act[threadIdx.x + k * B] = 0;
   }
   if (threadIdx.x == 0) slow = 0;
   // This chunk's records: one short run per part of its super-bucket,
   // flattened into one index space (RunTable) so every thread has a record
   // in flight at once; kRecPer records per thread, both columns of each
   // loaded before the first is classified.
-  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
-  const u32 p0 = pt[sb], p1 = pt[sb + 1];
-  __shared__ RunTable rt;
+  u32 total = rt.finish(rq);
+  __syncthreads();
   constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
-  for (u32 pb = p0; pb < p1; pb += RunTable::kRuns) {
-    const u32 total = rt.build(cs, pb, p1, cl);
-    for (u32 f0 = 0; f0 < total; f0 += B * kRecPer) {
-      u64 rmr[kRecPer], rix[kRecPer];
+  u64 rmr[kRecPer], rix[kRecPer];
+  // branch-free (clamped; an empty chunk reads record 0, which exists)
+  auto fetch = [&](u32 f0, u32 tot) {
+    u32 ix[kRecPer];
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * B + threadIdx.x;
-        rmr[r] = 0;
-        rix[r] = 0;
-        if (f < total) {
-          const u32 i = rt.locate(f);
-          rmr[r] = recs.mr[i];
-          rix[r] = recs.index[i];
-        }
-      }
+    for (int r = 0; r < kRecPer; ++r) {
+      const u32 f = f0 + u32(r) * B + threadIdx.x;
+      ix[r] = tot ? rt.locate_fixed(f < tot ? f : tot - 1) : 0u;
+    }
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) {
-        const u32 f = f0 + u32(r) * B + threadIdx.x;
-        bool stale = false, applied = false, rejected = false;
-        if (f < total) {
-          const u64 mr = rmr[r];
-          const u32 t32 = u32(mr >> 32), meta = u32(mr);
-          const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
-          const u64 gt = gterm[lg];
-          // t32 == kTermEscape: term >= 2^32 - 1, higher than any smaller group
-          // term and not comparable with a group term >= 2^32 - 1
-          const bool esc = t32 == kTermEscape;
-          if (esc || u64(t32) > gt) {
-            slow = 1;  // higher term (step-down order) or ambiguous compare
-          } else if (u64(t32) < gt) {
-            stale = true;                                   // raft.go:883-921
+    for (int r = 0; r < kRecPer; ++r) {
+      rmr[r] = recs.mr[ix[r]];
+      rix[r] = recs.index[ix[r]];
+    }
+  };
+  auto apply = [&](u32 f0, u32 tot) {
+#pragma unroll
+    for (int r = 0; r < kRecPer; ++r) {
+      const u32 f = f0 + u32(r) * B + threadIdx.x;
+      bool stale = false, applied = false, rejected = false;
+      if (f < tot) {
+        const u64 mr = rmr[r];
+        const u32 t32 = u32(mr >> 32), meta = u32(mr);
+        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+        const u64 gt = gterm[lg];
+        // t32 == kTermEscape: term >= 2^32 - 1, higher than any smaller group
+        // term and not comparable with a group term >= 2^32 - 1
+        const bool esc = t32 == kTermEscape;
+        if (esc || u64(t32) > gt) {
+          slow = 1;  // higher term (step-down order) or ambiguous compare
+        } else if (u64(t32) < gt) {
+          stale = true;                                   // raft.go:883-921
+        } else {
+          atomicOr(&act[lg], 1u << s);                    // raft.go:1107
+          if (meta & (1u << 24)) {  // QB_REC_REJECT
+            rejected = true;                              // raft.go:1109: not MaybeUpdate
           } else {
-            atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-            if (meta & (1u << 24)) {  // QB_REC_REJECT
-              rejected = true;                              // raft.go:1109: not MaybeUpdate
-            } else {
-              applied = true;
-              const u64 idx = rix[r];
-              atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
-              if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
-            }
+            applied = true;
+            const u64 idx = rix[r];
+            atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
+            if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
           }
         }
-        tally.add(0, stale);
-        tally.add(1, applied);
-        tally.add(2, rejected);
       }
+      tally.add(0, stale);
+      tally.add(1, applied);
+      tally.add(2, rejected);
     }
+  };
+  // The first batch (at the bench's ~512 records per chunk, all of them) in
+  // straight-line code: its wait is for its own loads and the state issued
+  // before them, not a conservative drain at a loop head.
+#ifdef QB_LAB_K5_NORECS
+  total = 0;
+#endif
+  fetch(0, total);
+  // pinned: both columns are loaded here, not sunk into apply's branches
+  // (each a round trip of its own)
+#pragma unroll
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+  apply(0, total);
+  for (u32 pb = p0, f0 = B * kRecPer;;) {
+    for (; f0 < total; f0 += B * kRecPer) {
+      fetch(f0, total);
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+      apply(f0, total);
+    }
+    pb += RunTable::kRuns;
+    if (pb >= p1) break;
+    total = rt.build(cs, pb, p1, cl);  // more than kRuns parts (synchronises)
+    f0 = 0;
   }
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
@@ -625,29 +671,40 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   }
   if (threadIdx.x == 0) chunk_slow[c] = 0;
   // maybeCommit for every group of the chunk + write-back (coalesced rows).
+  // Write-back granularity (QB_K5_FULL): a store only where the value
+  // changed leaves partially written lines; 2 = a wave whose segment of a
+  // row (or of committed / active) changed anywhere stores the whole segment.
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
     const u32 lg = threadIdx.x + k * B;
-    if (lg >= ng) continue;
-    const u64 g = g0 + lg;
+    const bool live = lg < ng;
+    const u64 g = g0 + (live ? lg : 0u);
 #pragma unroll
     for (int s = 0; s < N; ++s) {
       const u64 a = acc_m[s * CH + lg];
-      if (a > v[k][s]) {
-        v[k][s] = a;
-        match[u64(s) * geo.G + g] = a;
-      }
+      const bool up = live && a > v[k][s];
+      if (up) v[k][s] = a;
+#ifndef QB_LAB_K5_NOSTORE
+      if (QB_K5_FULL >= 2 ? (__ballot(up) != 0 && live) : up) k5_store(match + u64(s) * geo.G + g, v[k][s]);
+#endif
       if constexpr (NEXT) {
-        u64* q = next + u64(s) * geo.G + g;
-        const u64 nn = acc_n[s * CH + lg];
-        if (nn > *q) *q = nn;
+        if (live) {
+          u64* q = next + u64(s) * geo.G + g;
+          const u64 nn = acc_n[s * CH + lg];
+          if (nn > *q) *q = nn;
+        }
       }
     }
     const u64 ci = select_quorum<N>(v[k]);
-    const bool adv = ci > cm[k] && ci >= ts[k];  // log.go:328-334
-    if (adv) committed[g] = ci;
-    if (advanced) advanced[g] = adv ? 1 : 0;
-    if (act[lg]) active[g] = u16(av[k] | act[lg]);
+    const bool adv = live && ci > cm[k] && ci >= ts[k];  // log.go:328-334
+    const u32 na = live ? act[lg] : 0u;
+#ifndef QB_LAB_K5_NOSTORE
+    if (QB_K5_FULL >= 1 ? (__ballot(adv) != 0 && live) : adv) k5_store(committed + g, adv ? ci : cm[k]);
+    if (advanced && live) advanced[g] = adv ? 1 : 0;
+    if (QB_K5_FULL >= 1 ? (__ballot(na != 0) != 0 && live) : na != 0) active[g] = u16(av[k] | na);
+#else
+    if (ci == 0x1234567ull && av[k] == 7) committed[g] = ci;  // keeps the loads live
+#endif
   }
   const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
   tally.flush(tl, shard_of(shards), slot);
@@ -748,7 +805,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
                      rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1);
   QB_CHECK_LAUNCH("k_bk_scatter");
   hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
-                     geo, hist, bsum, pt, buf1, buf2, cs);
+                       geo, hist, bsum, pt, buf1, buf2, cs);
   QB_CHECK_LAUNCH("k_bk_split");
   return QB_OK;
 }
@@ -758,7 +815,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
 
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
-  return bk::carve(bk::geometry(n, G, M), 2).total;
+  return bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 2).total;
 }
 
 extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
@@ -777,7 +834,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
              "required state pointer is NULL");
   QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
              "record pointer is NULL");
-  const bk::Geometry geo = bk::geometry(n, G, M);
+  const bk::Geometry geo = bk::geometry(n, G, M, 0, bk::kSbIl);
   const bk::Carve cv = bk::carve(geo, 2);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
              "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv.total);
@@ -787,7 +844,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M, 2);
+  const bk::Cols recs = bk::cols_at(ws + cv.buf2, M, 2);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   // the stat shards and the any_slow word start at zero (bucket_records: K1)
@@ -810,7 +867,7 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                         reinterpret_cast<u8*>(ws + cv.chunk_flags),
                         reinterpret_cast<u32*>(ws + cv.flags),
                         shards};
-  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, buf2, pt, cs, a,
+  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, pt, cs, a,
                      st);
   QB_CHECK_LAUNCH("k_bk_apply");
   // chunks flagged slow by K5 (none in the steady state: the launch folds

@@ -83,15 +83,16 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   BlockTally<4> tally;  // stale, applied, rejected, non-member
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
-  const u32 sb = c / kChunksPerSb, cl = c % kChunksPerSb;
+  const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
-  // Load order as in k_bk_apply: (1) slot offsets, group terms and the run
-  // table; (2) the first record batch, then the old slot run and the commit
-  // inputs, whose latency runs under the record pass; (3) write-back.  Loads
-  // are branch-free (clamped addresses): the compiler's wait counts stay exact
-  // only in straight-line code.
-  // offsets and group terms into registers first, the run table's loads
-  // beside them: one round trip, not three
+  // Load order: (1) slot offsets, group terms and the run table's rows (the
+  // part table by scalar load); (2) the old slot run and the commit inputs;
+  // (3) the records.  Vector loads retire in order, so each wait of the
+  // record chain (offsets, then the run table, then the records) waits only
+  // for what was issued before it: the state's latency runs under the chain
+  // and the record pass instead of in front of them.  Loads are branch-free
+  // (clamped addresses): the compiler's wait counts stay exact only in
+  // straight-line code.
   constexpr u32 OPT = (CH + B) / B;  // CH + 1 offsets
   u32 ofr[OPT];
   u64 gtr[GPT];
@@ -105,12 +106,12 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     const u32 k = threadIdx.x + q * B;
     gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
+  const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
   for (u32 k = threadIdx.x; k < CAP; k += B) {
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
   }
   if (threadIdx.x == 0) slow = 0;
-  u32 total = rtab.build(cs, p0, p1, cl);  // synchronises
 #pragma unroll
   for (u32 q = 0; q < OPT; ++q) {
     const u32 k = threadIdx.x + q * B;
@@ -119,8 +120,8 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 #pragma unroll
   for (u32 q = 0; q < GPT; ++q) {
     gterm[threadIdx.x + q * B] = gtr[q];
-    act[threadIdx.x + q * B] = 0;
   }
+  for (u32 k = threadIdx.x; k < CH; k += B) act[k] = 0;
   __syncthreads();
   const u32 a0 = offs[0], run = offs[CH] - a0;
   // A run longer than the buffer: the first launch defers the chunk to the
@@ -134,6 +135,32 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       return;
     }
   }
+  // the old slot run (slots past the run re-read its last slot) and the
+  // commit-phase inputs of this thread's groups
+  // (an oversize run stays in HBM: its lanes re-read the first slot; an
+  // empty run has no slot to read and reads the chunk's first group term
+  // instead — a select, not a branch, which would cost the exact wait counts)
+  u64 old[PER];
+  const u64* src = run ? match + a0 : group_term + g0;
+  const u32 last = run && fits ? run - 1u : 0u;
+#pragma unroll
+  for (u32 p = 0; p < PER; ++p) {
+    const u32 j = threadIdx.x + p * B;
+    old[p] = src[j < last ? j : last];
+  }
+  u64 cm[GPT], ts[GPT];
+  u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * B;
+    const u64 g = g0 + (lg < ng ? lg : ng - 1);
+    cm[k] = committed[g];
+    ts[k] = term_start[g];
+    cf[k] = cfg[g];
+    av[k] = active[g];
+  }
+  u32 total = rtab.finish(rq);
+  __syncthreads();
   constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
   u64 rmr[kRecPer], rix[kRecPer];
   auto load = [&](u32 f0, u32 n) {
@@ -141,7 +168,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
       const u32 f = f0 + u32(r) * B + threadIdx.x;
-      ix[r] = n ? rtab.locate(f < n ? f : n - 1) : 0u;
+      ix[r] = n ? rtab.locate_fixed(f < n ? f : n - 1) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
@@ -185,36 +212,14 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     }
   };
   load(0, total);
-  // the old slot run (slots past the run re-read its last slot) and the
-  // commit-phase inputs of this thread's groups
-  // (an oversize run stays in HBM: its lanes re-read the first slot; an
-  // empty run has no slot to read and reads the chunk's first group term
-  // instead — a select, not a branch, which would cost the exact wait counts)
-  u64 old[PER];
-  const u64* src = run ? match + a0 : group_term + g0;
-  const u32 last = run && fits ? run - 1u : 0u;
-#pragma unroll
-  for (u32 p = 0; p < PER; ++p) {
-    const u32 j = threadIdx.x + p * B;
-    old[p] = src[j < last ? j : last];
-  }
-  u64 cm[GPT], ts[GPT];
-  u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
-#pragma unroll
-  for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * B;
-    const u64 g = g0 + (lg < ng ? lg : ng - 1);
-    cm[k] = committed[g];
-    ts[k] = term_start[g];
-    cf[k] = cfg[g];
-    av[k] = active[g];
-  }
 #pragma unroll
   for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
   apply(0, total);
   for (u32 pb = p0, f0 = B * kRecPer;;) {
     for (; f0 < total; f0 += B * kRecPer) {
       load(f0, total);
+#pragma unroll
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
       apply(f0, total);
     }
     pb += RunTable::kRuns;
@@ -240,10 +245,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     const u32 j = threadIdx.x + p * B;
     if (j < run) {
       const u64 a = acc[j];
-      if (a > old[p]) {
-        match[a0 + j] = a;
-        old[p] = a;
-      }
+      const bool up = a > old[p];
+      if (up) old[p] = a;
+      // whole wave segments where any slot rose (k_bk_apply: QB_K5_FULL)
+      if (QB_K5_FULL >= 2 ? __ballot(up) != 0 : up) match[a0 + j] = old[p];
       acc[j] = old[p];
       if constexpr (NEXT) {
         const u64 nn = accn[j];
@@ -270,9 +275,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     // log.go:328-334; an empty config's ci = MaxUint64 is past lastIndex,
     // whose term is 0 (log.go:271-273): never committed
     const bool adv = ci != kInf && ci > cm[k] && ci >= ts[k];
-    if (adv) committed[g] = ci;
+    if (QB_K5_FULL >= 1 ? __ballot(adv) != 0 : adv) committed[g] = adv ? ci : cm[k];
     if (advanced) advanced[g] = adv ? 1 : 0;
-    if (act[lg]) active[g] = u16(av[k] | act[lg]);
+    const u32 na = act[lg];
+    if (QB_K5_FULL >= 1 ? __ballot(na != 0) != 0 : na != 0) active[g] = u16(av[k] | na);
   }
   const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
   tally.flush(tl, shard_of(shards), slot);
@@ -358,7 +364,7 @@ u32 csr_wmax(uint32_t max_slots) {
 extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
   if (max_slots > QB_MAX_SLOTS) return 0;
   const u32 w = csr_wmax(max_slots);
-  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w)), 2).total;
+  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 2).total;
 }
 
 extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
@@ -382,7 +388,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const u32 wmax = csr_wmax(max_slots);
   // the bucketing filters slot >= the table bound (geo.n) as non-member; the
   // chunk size follows the LDS run capacity (chunk_groups(wmax))
-  bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax));
+  bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax), bk::kSbIl);
   geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
   const bk::Carve cv = bk::carve(geo, 2);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
