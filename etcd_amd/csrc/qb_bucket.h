@@ -61,6 +61,9 @@ constexpr bool kSbIl = QB_SB_IL != 0;
 #ifndef QB_K5_FULL
 #define QB_K5_FULL 2
 #endif
+#ifndef QB_CSR_FULL
+#define QB_CSR_FULL 0
+#endif
 __device__ __forceinline__ u32 xcd_major() {
   return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
 }
