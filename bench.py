@@ -314,8 +314,34 @@ def tracker_main(args, world, rank, dev):
         for k in names:
             getattr(tr, k).copy_(snap[k])
 
+    pipe = args.pipeline and not csr
+    if pipe:
+        # Two ticks in flight: tick k+1's bucketing (records only) on a side
+        # stream while tick k is applied on the launch stream
+        # (qb_dev_fixed_tracker_bucket / _apply, include/quorum_batch.h).
+        # apply(k) waits for bucket(k) (and, in stream order, apply(k-1));
+        # bucket(k) waits for apply(k-2), the last reader of its workspace.
+        wss = [tr.workspace(G), tr.workspace(G)]
+        side = torch.cuda.Stream(dev)
+        main = torch.cuda.current_stream(dev)
+        ev_b = [torch.cuda.Event() for _ in range(2)]
+        ev_a = [torch.cuda.Event() for _ in range(2)]
+        for e in ev_a:
+            e.record(main)
+        nstep = [0]
+
     def step(b):
-        tr.step(b, reset_stats=False)
+        if not pipe:
+            tr.step(b, reset_stats=False)
+            return
+        j = nstep[0] & 1
+        nstep[0] += 1
+        side.wait_event(ev_a[j])
+        tr.bucket(b, wss[j], stream=side)
+        ev_b[j].record(side)
+        main.wait_event(ev_b[j])
+        tr.apply_bucketed(b, wss[j])
+        ev_a[j].record(main)
 
     def barrier():
         if world > 1:
@@ -339,6 +365,9 @@ def tracker_main(args, world, rank, dev):
     ev = HipEvents(2)
     barrier()
     ev.record(ev.ev[0], st.cuda_stream)
+    if pipe:  # the side stream's first bucketing starts inside the region
+        for e in ev_a:
+            e.record(main)
     t0 = time.perf_counter()
     for k in range(W, nb):
         step(batches[k])
@@ -398,6 +427,7 @@ def tracker_main(args, world, rank, dev):
                    "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
                    "stale_term_fraction": 0.01, "mean_slots": slots_mean,
                    "mean_voters": voters_mean,
+                   "pipelined_ticks": bool(pipe),
                    "parallelism": f"groups sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key),
@@ -405,7 +435,10 @@ def tracker_main(args, world, rank, dev):
                                f" (one step = {kern})",
                      "bytes_per_group": bpg, "avg_kernel_us": step_s * 1e6,
                      "timing": "HIP events around the K timed steps on the launch stream; "
-                               "per-step device time = region / K (every kernel of the step)"},
+                               "per-step device time = region / K (every kernel of the step)"
+                               + ("; pipelined: tick k+1's bucketing (qb_dev_fixed_tracker_bucket) "
+                                  "on a second stream while tick k is applied "
+                                  "(qb_dev_fixed_tracker_apply), two workspaces" if pipe else "")},
         "preroll_ms": preroll_ms, "preroll_steps": preroll_steps,
         "last_region_stats": {k: int(v) for k, v in stats.items()},
         "route_ms": route_ms,
@@ -426,6 +459,11 @@ def main():
                          "settle; 20 warm-up steps measured 2-3 %% slow)")
     ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
     ap.add_argument("--voters", type=int, default=5)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="tracker workload: 1 = overlap tick k+1's bucketing with tick k's apply "
+                         "on two streams (bucket / apply entry points; measured 5 %% slower: "
+                         "the concurrent kernels contend); 0 = one qb_dev_fixed_tracker_step "
+                         "per tick (default)")
     ap.add_argument("--workload", default="fixed",
                     choices=["fixed", "ragged", "joint", "tracker", "tracker-csr"],
                     help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]; "

@@ -65,6 +65,8 @@ SIGNATURES = {
     "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
     "qb_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
     "qb_dev_fixed_tracker_step": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
+    "qb_dev_fixed_tracker_bucket": (_i32, [_u32, _u64, _u64] + [_p] * 5 + [C.c_size_t, _p]),
+    "qb_dev_fixed_tracker_apply": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_csr_tracker_workspace_bytes": (C.c_size_t, [_u64, _u32, _u64]),
     "qb_dev_csr_tracker_step": (_i32, [_u64, _u32, _p, _p, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_votes_workspace_bytes": (C.c_size_t, [_u64]),

@@ -818,28 +818,62 @@ extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint6
   return bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 2).total;
 }
 
-extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
-                                         const uint32_t* rec_group, const uint8_t* rec_flags,
-                                         const uint64_t* rec_index, const uint64_t* rec_term,
-                                         const uint64_t* group_term, const uint64_t* term_start,
-                                         uint64_t* match, uint64_t* next, uint16_t* active,
-                                         uint64_t* committed, uint32_t* stepdown_at,
-                                         uint8_t* advanced_out, uint64_t* stats,
-                                         void* workspace, size_t workspace_bytes, void* stream) {
+namespace {
+// Shared checks of the tracker-step entry points; the geometry and carve of
+// (n, G, M) are the same in all three, so a workspace bucketed by
+// qb_dev_fixed_tracker_bucket is exactly what qb_dev_fixed_tracker_apply reads.
+int fixed_tracker_check(uint32_t n, uint64_t G, uint64_t M, const void* workspace,
+                        size_t workspace_bytes, bk::Geometry* geo, bk::Carve* cv) {
   QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
   QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
   QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
+  *geo = bk::geometry(n, G, M, 0, bk::kSbIl);
+  *cv = bk::carve(*geo, 2);
+  QB_REQUIRE(workspace && workspace_bytes >= cv->total,
+             "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv->total);
+  QB_REQUIRE(geo->NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
+             (unsigned long long)G);
+  return QB_OK;
+}
+}  // namespace
+
+extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
+                                           const uint32_t* rec_group, const uint8_t* rec_flags,
+                                           const uint64_t* rec_index, const uint64_t* rec_term,
+                                           void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
+             "record pointer is NULL");
+  bk::Geometry geo;
+  bk::Carve cv;
+  const int rc = fixed_tracker_check(n, G, M, workspace, workspace_bytes, &geo, &cv);
+  if (rc != QB_OK) return rc;
+  char* ws = static_cast<char*>(workspace);
+  // the stat shards and the flag words start at zero (K2 writes them)
+  return bk::bucket_records(geo, cv, ws, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
+                            reinterpret_cast<const u64*>(rec_term),
+                            reinterpret_cast<u64*>(ws + cv.shards), as_stream(stream),
+                            /*term32=*/false, /*packed=*/true);
+}
+
+extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
+                                          const uint32_t* rec_group, const uint8_t* rec_flags,
+                                          const uint64_t* rec_index, const uint64_t* rec_term,
+                                          const uint64_t* group_term, const uint64_t* term_start,
+                                          uint64_t* match, uint64_t* next, uint16_t* active,
+                                          uint64_t* committed, uint32_t* stepdown_at,
+                                          uint8_t* advanced_out, uint64_t* stats,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
   if (G == 0) return QB_OK;
   QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
              "required state pointer is NULL");
   QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
              "record pointer is NULL");
-  const bk::Geometry geo = bk::geometry(n, G, M, 0, bk::kSbIl);
-  const bk::Carve cv = bk::carve(geo, 2);
-  QB_REQUIRE(workspace && workspace_bytes >= cv.total,
-             "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv.total);
-  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
-             (unsigned long long)G);
+  bk::Geometry geo;
+  bk::Carve cv;
+  const int rc = fixed_tracker_check(n, G, M, workspace, workspace_bytes, &geo, &cv);
+  if (rc != QB_OK) return rc;
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
@@ -847,15 +881,9 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   const bk::Cols recs = bk::cols_at(ws + cv.buf2, M, 2);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
-  // the stat shards and the any_slow word start at zero (bucket_records: K1)
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
-  {
-    const int rc = bk::bucket_records(geo, cv, ws, rg, rec_flags, ri, rtm, shards, st,
-                                      /*term32=*/false, /*packed=*/true);
-    if (rc != QB_OK) return rc;
-  }
   const bk::ApplyArgs a{reinterpret_cast<const u64*>(group_term),
                         reinterpret_cast<const u64*>(term_start),
                         reinterpret_cast<u64*>(match),
@@ -877,4 +905,23 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   bk::dispatch_slow(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, sa, stt, st);
   QB_CHECK_LAUNCH("k_bk_slow");
   return QB_OK;
+}
+
+extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
+                                         const uint32_t* rec_group, const uint8_t* rec_flags,
+                                         const uint64_t* rec_index, const uint64_t* rec_term,
+                                         const uint64_t* group_term, const uint64_t* term_start,
+                                         uint64_t* match, uint64_t* next, uint16_t* active,
+                                         uint64_t* committed, uint32_t* stepdown_at,
+                                         uint8_t* advanced_out, uint64_t* stats,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
+             "required state pointer is NULL");
+  const int rc = qb_dev_fixed_tracker_bucket(n, G, M, rec_group, rec_flags, rec_index, rec_term,
+                                             workspace, workspace_bytes, stream);
+  if (rc != QB_OK) return rc;
+  return qb_dev_fixed_tracker_apply(n, G, M, rec_group, rec_flags, rec_index, rec_term, group_term,
+                                    term_start, match, next, active, committed, stepdown_at,
+                                    advanced_out, stats, workspace, workspace_bytes, stream);
 }

@@ -467,6 +467,31 @@ class FixedTracker:
                   _ptr(self.stats), _ptr(self._ws), self._ws.numel(), _stream(self.device))
         return advanced_out
 
+    def workspace(self, M: int) -> torch.Tensor:
+        """A device workspace for one batch of M records (bucket / apply_bucketed)."""
+        need = _lib.load().qb_fixed_tracker_workspace_bytes(self.n, self.G, M)
+        return torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+
+    def bucket(self, batch: AppRespBatch, ws: torch.Tensor, stream=None):
+        """First half of ``step`` (qb_dev_fixed_tracker_bucket): the batch sorted
+        by group into ``ws``; touches no tracker state, so it may run on another
+        stream while the previous batch is applied."""
+        _lib.call("qb_dev_fixed_tracker_bucket", self.n, self.G, batch.M, _ptr(batch.group),
+                  _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(ws), ws.numel(),
+                  _stream(self.device) if stream is None else stream.cuda_stream)
+
+    def apply_bucketed(self, batch: AppRespBatch, ws: torch.Tensor,
+                       advanced_out: Optional[torch.Tensor] = None, stream=None):
+        """Second half of ``step`` (qb_dev_fixed_tracker_apply) over a workspace
+        that ``bucket`` filled for the same batch."""
+        _lib.call("qb_dev_fixed_tracker_apply", self.n, self.G, batch.M, _ptr(batch.group),
+                  _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(self.term),
+                  _ptr(self.term_start), _ptr(self.match), _ptr(self.next), _ptr(self.active),
+                  _ptr(self.committed), _ptr(self.stepdown_at), _ptr(advanced_out),
+                  _ptr(self.stats), _ptr(ws), ws.numel(),
+                  _stream(self.device) if stream is None else stream.cuda_stream)
+        return advanced_out
+
     def stats_dict(self) -> dict:
         v = self.stats.cpu().tolist()
         return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}

@@ -301,6 +301,38 @@ int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                               void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* qb_dev_fixed_tracker_step in two halves, for a caller that pipelines
+ * ticks: _bucket sorts a batch by group into a workspace (reads only the
+ * batch: K1-K4, no leader state), _apply applies that workspace's batch to
+ * the state (K5 + the exact slow path; the same batch pointers, which the
+ * slow path re-reads).  step == bucket then apply on one stream.  With two
+ * workspaces on two streams, tick k+1's bucketing can run while tick k is
+ * applied: the caller orders apply(k+1) after bucket(k+1) and apply(k), and
+ * bucket(k+2) after apply(k) (workspace reuse).  Each workspace carries its
+ * own statistic shards, folded into `stats` by _apply.  (On one MI355X the
+ * overlap measured slower than back-to-back steps, 706-712 vs 672-674 us per
+ * 16M-group tick: the concurrent kernels contend for the CUs and HBM; the
+ * split is for callers that interleave other work between the halves.) */
+int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
+                                const uint32_t* rec_group,
+                                const uint8_t* rec_flags,
+                                const uint64_t* rec_index,
+                                const uint64_t* rec_term,
+                                void* workspace, size_t workspace_bytes,
+                                void* stream);
+int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
+                               const uint32_t* rec_group,
+                               const uint8_t* rec_flags,
+                               const uint64_t* rec_index,
+                               const uint64_t* rec_term,
+                               const uint64_t* group_term,
+                               const uint64_t* term_start, uint64_t* match,
+                               uint64_t* next, uint16_t* active,
+                               uint64_t* committed, uint32_t* stepdown_at,
+                               uint8_t* advanced_out, uint64_t* stats,
+                               void* workspace, size_t workspace_bytes,
+                               void* stream);
+
 /* The same leader tick over G groups of the CSR layout (ragged voter
  * counts, learners, joint configs): a MsgAppResp batch applied (MaybeUpdate on
  * the slot's Progress, learners included; a slot >= s_g has no Progress and

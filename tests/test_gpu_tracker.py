@@ -221,3 +221,58 @@ def test_appresp_full_size_16m():
     tr.commit_advance()
     assert np.array_equal(batch.as_u64(tr.match), st["match"])
     assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+
+
+@pytest.mark.gpu
+def test_pipelined_bucket_apply_equals_step():
+    """qb_dev_fixed_tracker_bucket / _apply with two workspaces on two streams
+    (tick k+1 bucketed while tick k is applied, as bench.py --pipeline 1)
+    leave exactly the state of consecutive qb_dev_fixed_tracker_step calls."""
+    import torch
+    from etcd_amd.quorum import batch as qb
+    dev = torch.device("cuda", 0)
+    n, G, M, K = 5, 300_001, 250_000, 5
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99)
+
+    def fresh():
+        tr = qb.FixedTracker(n, G, dev)
+        tr.match.copy_(torch.randint(0, 1 << 20, (n, G), generator=gen, device=dev))
+        tr.term.fill_(7)
+        tr.term_start.copy_(torch.randint(0, 1 << 19, (G,), generator=gen, device=dev))
+        tr.commit_advance()
+        return tr
+
+    a = fresh()
+    b = qb.FixedTracker(n, G, dev)
+    for name in ("match", "term", "term_start", "committed"):
+        getattr(b, name).copy_(getattr(a, name))
+    batches = []
+    for k in range(K):
+        grp = torch.randint(0, G + 50, (M,), generator=gen, device=dev, dtype=torch.int32)
+        slot = torch.randint(0, n + 1, (M,), generator=gen, device=dev, dtype=torch.int32)
+        rej = (torch.rand(M, generator=gen, device=dev) < 0.05).to(torch.int32) << 7
+        idx = torch.randint(0, 1 << 21, (M,), generator=gen, device=dev)
+        trm = torch.where(torch.rand(M, generator=gen, device=dev) < 0.02, 6,
+                          torch.where(torch.rand(M, generator=gen, device=dev) < 0.001, 8, 7))
+        batches.append(qb.AppRespBatch(grp, (slot | rej).to(torch.uint8), idx, trm.to(torch.int64)))
+    for bt in batches:
+        a.step(bt, reset_stats=False)
+    wss = [b.workspace(M), b.workspace(M)]
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    ev_b = [torch.cuda.Event() for _ in range(2)]
+    ev_a = [torch.cuda.Event() for _ in range(2)]
+    for e in ev_a:
+        e.record(main)
+    for k, bt in enumerate(batches):
+        j = k & 1
+        side.wait_event(ev_a[j])
+        b.bucket(bt, wss[j], stream=side)
+        ev_b[j].record(side)
+        main.wait_event(ev_b[j])
+        b.apply_bucketed(bt, wss[j])
+        ev_a[j].record(main)
+    torch.cuda.synchronize()
+    for name in ("match", "committed", "active", "stepdown_at", "stats"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
