@@ -507,15 +507,6 @@ __host__ __device__ constexpr u32 k5_block(int n) {
   return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
 }
 
-template <typename T>
-__device__ __forceinline__ void k5_store(T* p, T v) {
-#ifdef QB_K5_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-
 template <int N, bool NEXT>
 __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
@@ -685,7 +676,7 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
       const bool up = live && a > v[k][s];
       if (up) v[k][s] = a;
 #ifndef QB_LAB_K5_NOSTORE
-      if (QB_K5_FULL >= 2 ? (__ballot(up) != 0 && live) : up) k5_store(match + u64(s) * geo.G + g, v[k][s]);
+      if (QB_K5_FULL >= 2 ? (__ballot(up) != 0 && live) : up) match[u64(s) * geo.G + g] = v[k][s];
 #endif
       if constexpr (NEXT) {
         if (live) {
@@ -699,7 +690,7 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     const bool adv = live && ci > cm[k] && ci >= ts[k];  // log.go:328-334
     const u32 na = live ? act[lg] : 0u;
 #ifndef QB_LAB_K5_NOSTORE
-    if (QB_K5_FULL >= 1 ? (__ballot(adv) != 0 && live) : adv) k5_store(committed + g, adv ? ci : cm[k]);
+    if (QB_K5_FULL >= 1 ? (__ballot(adv) != 0 && live) : adv) committed[g] = adv ? ci : cm[k];
     if (advanced && live) advanced[g] = adv ? 1 : 0;
     if (QB_K5_FULL >= 1 ? (__ballot(na != 0) != 0 && live) : na != 0) active[g] = u16(av[k] | na);
 #else
