@@ -138,9 +138,10 @@ def _records(rng, G, M, last, slots, higher=0.002):
     return group, flags, index, term
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [True, False, "split"])
 def test_fixed_tracker_raw_abi(fused):
-    """qb_dev_fixed_tracker_step (fused) and qb_dev_fixed_apply_appresp +
+    """qb_dev_fixed_tracker_step (fused), qb_dev_fixed_tracker_bucket +
+    qb_dev_fixed_tracker_apply (split) and qb_dev_fixed_apply_appresp +
     qb_dev_fixed_commit_advance (two calls) through the raw ABI vs the
     sequential oracle; stepdown_at follows each entry point's contract."""
     s = Stream()
@@ -157,7 +158,15 @@ def test_fixed_tracker_raw_abi(fused):
                                          lambda g: rng.integers(1, n, size=g.size))
     d_g, d_f, d_i, d_t = s.up(group), s.up(flags), s.up(index), s.up(term)
     stats = oc.appresp_sequential(n, G, (group, flags, index, term), st)
-    if fused:
+    if fused == "split":
+        need = lib.qb_fixed_tracker_workspace_bytes(n, G, M)
+        ws = s.zeros(need)
+        _lib.check(lib.qb_dev_fixed_tracker_bucket(n, G, M, d_g, d_f, d_i, d_t, ws, need, s.st),
+                   "bucket")
+        _lib.check(lib.qb_dev_fixed_tracker_apply(n, G, M, d_g, d_f, d_i, d_t, d_term, d_ts,
+                                                  d_match, None, d_act, d_cm, d_sd, d_adv, d_stats,
+                                                  ws, need, s.st), "apply")
+    elif fused:
         need = lib.qb_fixed_tracker_workspace_bytes(n, G, M)
         ws = s.zeros(need)
         _lib.check(lib.qb_dev_fixed_tracker_step(n, G, M, d_g, d_f, d_i, d_t, d_term, d_ts,
