@@ -256,6 +256,14 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
 // replay kernel keeps that kernel's LDS to the working tables (occupancy) and
 // gives the byte moving a full-occupancy streaming launch of its own.
 constexpr u8 kCarried = 0xFF;
+// A fresh slot (initProgress) is marked kFresh with its group in the new
+// infl_pos; k_cc_copy materialises it.  So every new slot's row is written
+// by the copy kernel, whole lines per wave (QB_CC_FRESH_IN_COPY; 0 = the
+// write pass stores fresh rows itself, scattered partial lines).
+constexpr u8 kFresh = 0xFE;
+#ifndef QB_CC_FRESH_IN_COPY
+#define QB_CC_FRESH_IN_COPY 1
+#endif
 
 __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
   __shared__ u64 tabs[kTab][kBlk];
@@ -292,6 +300,9 @@ __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
     if (best < n_old && !(r.fresh & b)) {  // carried Progress: k_cc_copy
       A.n_pstate[d] = kCarried;
       A.n_infl_pos[d] = s0 + u32(best);
+    } else if (QB_CC_FRESH_IN_COPY) {  // initProgress (confchange.go:258-281): k_cc_copy
+      A.n_pstate[d] = kFresh;
+      A.n_infl_pos[d] = u32(g);
     } else {  // initProgress (confchange.go:258-281)
       A.n_match[d] = 0;
       A.n_next[d] = last;
@@ -370,8 +381,9 @@ __global__ __launch_bounds__(256) void k_cc_copy(Args A) {
   const u32 old_total = A.off[A.G];
   const u32 K = A.K;
   for (u64 d = u64(blockIdx.x) * 256 + threadIdx.x; d < end; d += u64(gridDim.x) * 256) {
-    const bool carried = A.n_pstate[d] == kCarried;
-    const u32 src = carried ? A.n_infl_pos[d] : 0u;
+    const u8 mk = A.n_pstate[d];
+    const bool carried = mk == kCarried, fresh = QB_CC_FRESH_IN_COPY && mk == kFresh;
+    const u32 src = carried || fresh ? A.n_infl_pos[d] : 0u;
     const bool ok = carried && src < old_total;
     if (ok) {
       const u64 m = A.match[src], nx = A.next[src], ps = A.psnap[src];
@@ -382,6 +394,12 @@ __global__ __launch_bounds__(256) void k_cc_copy(Args A) {
       A.n_psnap[d] = ps;
       A.n_infl_pos[d] = ip;
       A.n_pstate[d] = st;
+    } else if (fresh) {  // initProgress (confchange.go:258-281); src = the group
+      A.n_match[d] = 0;
+      A.n_next[d] = A.last_index[src];
+      A.n_psnap[d] = 0;
+      A.n_infl_pos[d] = 0;
+      A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
     }
     if (K) {
       const u64* sr = A.infl_buf + u64(src) * K;
