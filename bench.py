@@ -459,6 +459,9 @@ def main():
                          "settle; 20 warm-up steps measured 2-3 %% slow)")
     ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
     ap.add_argument("--voters", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=2000.0,
+                    help="configs[1]-[3]: at most this long, untimed 64-step probes before the "
+                         "timed region until one runs within 10 %% of the pre-roll's fastest")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="tracker workload: 1 = overlap tick k+1's bucketing with tick k's apply "
                          "on two streams (bucket / apply entry points; measured 5 %% slower: "
@@ -594,12 +597,31 @@ def main():
     # 9.85 us per launch against 8.6 us settled).  Then the W warm-up steps.
     preroll_steps, tp = 0, time.perf_counter()
     preroll_s = max(0.0, args.preroll_ms) / 1e3
+    best64 = float("inf")  # fastest 64-step chunk (wall, synchronised)
     while time.perf_counter() - tp < preroll_s:
+        tc = time.perf_counter()
         run_steps(64)
         preroll_steps += 64
         torch.cuda.synchronize()
+        best64 = min(best64, time.perf_counter() - tc)
     preroll_ms = (time.perf_counter() - tp) * 1e3
     run_steps(W)
+    # Settle guard (untimed): one box ran the timed region and the MALL-warm
+    # pass after it at 0.6x the pre-roll's rate (a transient slowdown that the
+    # pre-roll had not seen).  Before the region, 64-step probes are run until
+    # one is within 10 % of the pre-roll's fastest chunk (at most --settle-ms);
+    # the probes and their last ratio are reported.
+    settle_probes, settle_ratio, ts_ = 0, None, time.perf_counter()
+    if best64 < float("inf"):
+        while time.perf_counter() - ts_ < max(0.0, args.settle_ms) / 1e3:
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
+            run_steps(64)
+            torch.cuda.synchronize()
+            settle_probes += 1
+            settle_ratio = (time.perf_counter() - tc) / best64
+            if settle_ratio <= 1.10:
+                break
     # Timed region: K steps between barrier + synchronize.  Device time = from
     # the earliest start event to the latest end event, one event pair per
     # launch stream (no cross-stream hop inside the region: a fork + join
@@ -716,6 +738,8 @@ def main():
             },
             "preroll_ms": preroll_ms,
             "preroll_steps": preroll_steps,
+            "settle_probes": settle_probes,
+            "settle_last_ratio": settle_ratio,
             "value_mall_warm": world * G * K / warm_elapsed,
             "allgather_ms": allgather_ms,
         }
