@@ -524,7 +524,12 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   __shared__ u64 gterm[CH];
   __shared__ u32 act[CH];
   __shared__ u32 slow;
-  const u32 c = blockIdx.x;
+#ifndef QB_K5_REV
+#define QB_K5_REV 1
+#endif
+  // Chunks in reverse order (QB_K5_REV): K4 wrote the last super-buckets
+  // last, so their runs are the ones still in the 256 MB MALL when K5 starts.
+  const u32 c = QB_K5_REV ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   // Load order: the group terms and this chunk's run table first, then the
