@@ -38,11 +38,19 @@ def allgather_results(commit: torch.Tensor, vote: torch.Tensor, total: int,
     if commit.numel() != e - b or vote.numel() != e - b:
         raise ValueError("local vectors do not match this rank's shard")
     cap = shard_range(total, world, 0)[1]  # rank 0 holds the largest shard
+    backend = dist.get_backend(group)
+    if backend == "nccl" and total == cap * world:
+        # equal shards (the bench's weak-scaling case): gathered straight into
+        # the node-wide vectors, no padding copies and no concatenation
+        gc = torch.empty(total, dtype=commit.dtype, device=commit.device)
+        gv = torch.empty(total, dtype=vote.dtype, device=vote.device)
+        dist.all_gather_into_tensor(gc, commit.contiguous(), group=group)
+        dist.all_gather_into_tensor(gv, vote.contiguous(), group=group)
+        return gc, gv
     pc = torch.zeros(cap, dtype=commit.dtype, device=commit.device)
     pv = torch.zeros(cap, dtype=vote.dtype, device=vote.device)
     pc[: e - b] = commit
     pv[: e - b] = vote
-    backend = dist.get_backend(group)
     if backend == "nccl":
         gc = torch.empty(world * cap, dtype=commit.dtype, device=commit.device)
         gv = torch.empty(world * cap, dtype=vote.dtype, device=vote.device)

@@ -163,3 +163,29 @@ def test_route_partition_device_matches_host(world):
     assert hc == dc
     for k in cols:
         assert torch.equal(hs[k], ds[k].cpu()), k
+
+
+def _nccl_world1_worker(rank, world, port, q, total):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from etcd_amd.quorum import batch
+        from etcd_amd.shard import allgather_results
+        dev = torch.device("cuda", 0)
+        grp = batch.FixedGroups.synth(SEED, 5, total, device=dev)
+        c, v = grp.committed_vote()
+        gc, gv = allgather_results(c, v, total)   # RCCL, device tensors
+        torch.cuda.synchronize()
+        q.put((bool(torch.equal(gc, c)), bool(torch.equal(gv, v)), gc.is_cuda, gc.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_allgather_results_rccl_world1():
+    """allgather_results over RCCL (backend "nccl", device tensors) on a
+    single-rank group — the call the driver's multi-GPU bench makes, here with
+    the one GPU (RCCL refuses two ranks on one device)."""
+    ok_c, ok_v, on_dev, n = _spawn(_nccl_world1_worker, 1, 50_000)
+    assert ok_c and ok_v and on_dev and n == 50_000
