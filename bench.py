@@ -332,7 +332,7 @@ def tracker_main(args, world, rank, dev):
 
     def step(b):
         if not pipe:
-            tr.step(b, reset_stats=False)
+            tr.step(b, reset_stats=False, rearm=False)
             return
         j = nstep[0] & 1
         nstep[0] += 1

@@ -12,8 +12,12 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# QB_LIB_PATH overrides the in-tree build (A/B timing of two builds; tools/lab).
-LIB_PATH = os.environ.get("QB_LIB_PATH") or os.path.join(_HERE, "libquorumbatch.so")
+# The product library is always the in-tree build.  An A/B lab run selects
+# another build explicitly (use_lab_library, from a `--lab-lib PATH` flag of
+# bench.py / tools/bench_configs.py); no environment variable swaps it.
+LIB_PATH = os.path.join(_HERE, "libquorumbatch.so")
+_lab_path = None
+_skipped: set = set()
 
 QB_OK = 0
 QB_EINVAL = -1
@@ -63,6 +67,7 @@ SIGNATURES = {
     "qb_dev_fixed_apply_appresp": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
                                           _p, _p, _p]),
     "qb_dev_fixed_commit_advance": (_i32, [_u32, _u64, _p, _p, _p, _p, _p]),
+    "qb_dev_stepdown_check_armed": (_i32, [_u64, _p, _p, _p]),
     "qb_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
     "qb_dev_fixed_tracker_step": (_i32, [_u32, _u64, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_dev_fixed_tracker_bucket": (_i32, [_u32, _u64, _u64] + [_p] * 5 + [C.c_size_t, _p]),
@@ -103,6 +108,18 @@ _lib = None
 _lock = threading.Lock()
 
 
+def use_lab_library(path: str) -> None:
+    """Test/lab hook: bind ``path`` (an A/B build of the same ABI) instead of
+    the in-tree library.  Must run before the first ``load()``.  Symbols the
+    lab build lacks are recorded; ``call`` raises naming them."""
+    global _lab_path
+    if _lib is not None:
+        raise QuorumBatchError("use_lab_library() after the library was loaded")
+    if not os.path.exists(path):
+        raise QuorumBatchError(f"lab library {path} does not exist")
+    _lab_path = os.path.abspath(path)
+
+
 def load() -> C.CDLL:
     """Load (once) and type the library; raises QuorumBatchError if absent."""
     global _lib
@@ -111,20 +128,25 @@ def load() -> C.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
+        path = _lab_path or LIB_PATH
+        if not os.path.exists(path):
             raise QuorumBatchError(
-                f"{LIB_PATH} not built: run `make -C etcd_amd/csrc` (or "
+                f"{path} not built: run `make -C etcd_amd/csrc` (or "
                 "__graft_entry__.build()); there is no CPU fallback")
-        lib = C.CDLL(LIB_PATH)
-        lab = bool(os.environ.get("QB_LIB_PATH"))  # an A/B build may predate newer symbols
+        lib = C.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            if lab and not hasattr(lib, name):
+            if _lab_path and not hasattr(lib, name):  # an A/B build may predate newer symbols
+                _skipped.add(name)
                 continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
         if lib.qb_abi_version() != 1:
             raise QuorumBatchError("libquorumbatch ABI version mismatch")
+        if _skipped:
+            import warnings
+            warnings.warn(f"lab library {path} lacks {len(_skipped)} ABI symbol(s): "
+                          f"{', '.join(sorted(_skipped))}", stacklevel=2)
         _lib = lib
     return _lib
 
@@ -135,5 +157,16 @@ def check(rc: int, what: str) -> None:
         raise QuorumBatchError(f"{what} failed (rc={rc}): {msg}")
 
 
+def fn(name: str):
+    """The typed entry point ``name``; a symbol a lab build lacks raises here
+    (never an untyped ctypes default that would truncate 64-bit pointers)."""
+    lib = load()
+    if name in _skipped:
+        raise QuorumBatchError(f"{name} is missing from the lab library {_lab_path}")
+    if name not in SIGNATURES:
+        raise QuorumBatchError(f"{name} is not part of the ABI (include/quorum_batch.h)")
+    return getattr(lib, name)
+
+
 def call(name: str, *args) -> None:
-    check(getattr(load(), name)(*args), name)
+    check(fn(name)(*args), name)

@@ -12,7 +12,9 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <algorithm>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "qb_common.h"
@@ -173,10 +175,10 @@ extern "C" int qb_dev_allgather_results(qb_comm* c, uint64_t total,
 extern "C" size_t qb_route_workspace_bytes(int world, uint64_t M) {
   if (world < 1 || world > QB_ROUTE_MAX_WORLD) return 0;
   // send columns (group 4, flags 1, index/term/hint/log_term 32) + the
-  // partition's workspace + send_off and the all-gathered count rows
+  // partition's workspace + send_off and the all-gathered rows
   return up256(4 * M) + up256(M) + 4 * up256(8 * M) + qb_route_partition_workspace_bytes(world, M) +
          up256(sizeof(uint32_t) * (size_t(world) + 1)) +
-         2 * up256(sizeof(uint64_t) * size_t(world) * size_t(world + 1));
+         2 * up256(sizeof(uint64_t) * size_t(world) * size_t(world + 2));
 }
 
 extern "C" int qb_dev_route_records(qb_comm* c, uint64_t total, uint64_t M,
@@ -188,13 +190,16 @@ extern "C" int qb_dev_route_records(qb_comm* c, uint64_t total, uint64_t M,
                                     uint64_t* out_hint, uint64_t* out_log_term,
                                     uint64_t out_cap, uint64_t* out_count, void* workspace,
                                     size_t workspace_bytes, void* stream) {
+  // Only the checks that leave no workspace to gather through return before
+  // the collectives; every other local failure (the inputs, the partition,
+  // NULL outputs) is carried in this rank's row, so all ranks see it and
+  // return together instead of some waiting in a send for a rank that left.
   QB_REQUIRE(c && out_count, "comm / out_count NULL");
-  QB_REQUIRE(!rec_hint == !out_hint && !rec_log_term == !out_log_term,
-             "hint / log_term: give both the input and the output column, or neither");
   const int W = c->world;
   QB_REQUIRE(W <= QB_ROUTE_MAX_WORLD, "world %d > %d", W, QB_ROUTE_MAX_WORLD);
   QB_REQUIRE(workspace && workspace_bytes >= qb_route_workspace_bytes(W, M),
              "workspace too small (qb_route_workspace_bytes)");
+  *out_count = 0;
   hipStream_t st = qb::as_stream(stream);
   char* ws = static_cast<char*>(workspace);
   size_t o = 0;
@@ -212,41 +217,66 @@ extern "C" int qb_dev_route_records(qb_comm* c, uint64_t total, uint64_t M,
   const size_t pws = qb_route_partition_workspace_bytes(W, M);
   void* part_ws = take(pws);
   uint32_t* send_off = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * (size_t(W) + 1)));
-  uint64_t* row = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * size_t(W + 1)));
-  uint64_t* rows = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * size_t(W + 1)));
-  int rc = qb_dev_route_partition(total, W, M, rec_group, rec_flags, rec_index, rec_term, rec_hint,
-                                  rec_log_term, s_group, s_flags, s_index, s_term,
-                                  rec_hint ? s_hint : nullptr, rec_log_term ? s_lt : nullptr,
-                                  send_off, part_ws, pws, stream);
-  if (rc != QB_OK) return rc;
-  // this rank's row: records for each destination, then its output capacity
-  std::vector<uint32_t> off(size_t(W) + 1);
-  hipError_t h = hipMemcpyAsync(off.data(), send_off, sizeof(uint32_t) * off.size(),
-                                hipMemcpyDeviceToHost, st);
-  if (h == hipSuccess) h = hipStreamSynchronize(st);
-  if (h != hipSuccess) return qb::hip_fail(h, "send counts to host");
-  std::vector<uint64_t> mine(size_t(W) + 1), all(size_t(W) * size_t(W + 1));
+  const size_t RW = size_t(W) + 2;  // a row: W counts, output capacity, ok flag
+  uint64_t* row = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * RW));
+  uint64_t* rows = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W) * RW));
+  std::string local_err;
+  int local_rc = QB_OK;
+  if (!rec_hint != !out_hint || !rec_log_term != !out_log_term) {
+    local_rc = QB_EINVAL;
+    local_err = "hint / log_term: give both the input and the output column, or neither";
+  } else {
+    local_rc = qb_dev_route_partition(total, W, M, rec_group, rec_flags, rec_index, rec_term,
+                                      rec_hint, rec_log_term, s_group, s_flags, s_index, s_term,
+                                      rec_hint ? s_hint : nullptr, rec_log_term ? s_lt : nullptr,
+                                      send_off, part_ws, pws, stream);
+    if (local_rc != QB_OK) local_err = qb_last_error();
+  }
+  // this rank's row: records for each destination, its output capacity (0
+  // when an output column is NULL: it can take no record), and ok
+  std::vector<uint32_t> off(size_t(W) + 1, 0);
+  hipError_t h = hipSuccess;
+  if (local_rc == QB_OK) {
+    h = hipMemcpyAsync(off.data(), send_off, sizeof(uint32_t) * off.size(), hipMemcpyDeviceToHost,
+                       st);
+    if (h == hipSuccess) h = hipStreamSynchronize(st);
+    if (h != hipSuccess) {
+      local_rc = qb::hip_fail(h, "send counts to host");
+      local_err = qb_last_error();
+      std::fill(off.begin(), off.end(), 0u);
+    }
+  }
+  const bool outputs = out_group && out_flags && out_index && out_term;
+  std::vector<uint64_t> mine(RW), all(size_t(W) * RW);
   for (int r = 0; r < W; ++r) mine[r] = uint64_t(off[r + 1]) - off[r];
-  mine[W] = out_cap;
+  mine[W] = outputs ? out_cap : 0;
+  mine[W + 1] = local_rc == QB_OK ? 1 : 0;
   h = hipMemcpyAsync(row, mine.data(), sizeof(uint64_t) * mine.size(), hipMemcpyHostToDevice, st);
   if (h != hipSuccess) return qb::hip_fail(h, "count row to device");
-  QB_NCCL(ncclAllGather(row, rows, size_t(W + 1), ncclUint64, c->nccl, st), "ncclAllGather(counts)");
+  QB_NCCL(ncclAllGather(row, rows, RW, ncclUint64, c->nccl, st), "ncclAllGather(counts)");
   h = hipMemcpyAsync(all.data(), rows, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost, st);
   if (h == hipSuccess) h = hipStreamSynchronize(st);
   if (h != hipSuccess) return qb::hip_fail(h, "count rows to host");
+  if (local_rc != QB_OK) {
+    qb::set_error("%s", local_err.c_str());
+    return local_rc;
+  }
+  for (int r = 0; r < W; ++r)
+    QB_REQUIRE(all[size_t(r) * RW + size_t(W) + 1] == 1,
+               "rank %d failed before the exchange (its qb_last_error has the reason)", r);
   // every rank checks every rank's capacity: one decision everywhere
-  auto cnt = [&](int src, int dst) { return all[size_t(src) * size_t(W + 1) + size_t(dst)]; };
+  auto cnt = [&](int src, int dst) { return all[size_t(src) * RW + size_t(dst)]; };
+  uint64_t mine_in = 0;
   for (int d = 0; d < W; ++d) {
     uint64_t in = 0;
     for (int s2 = 0; s2 < W; ++s2) in += cnt(s2, d);
-    if (d == c->rank) *out_count = in;
-    QB_REQUIRE(in <= all[size_t(d) * size_t(W + 1) + size_t(W)],
-               "rank %d would receive %llu records, over its capacity %llu", d,
-               (unsigned long long)in,
-               (unsigned long long)all[size_t(d) * size_t(W + 1) + size_t(W)]);
+    if (d == c->rank) mine_in = in;
+    const uint64_t cap = all[size_t(d) * RW + size_t(W)];
+    QB_REQUIRE(in <= cap, "rank %d would receive %llu records, over its capacity %llu%s", d,
+               (unsigned long long)in, (unsigned long long)cap,
+               cap == 0 ? " (or an output column of it is NULL)" : "");
   }
-  QB_REQUIRE(*out_count == 0 || (out_group && out_flags && out_index && out_term),
-             "output column is NULL");
+  *out_count = mine_in;
   std::vector<uint64_t> roff(size_t(W) + 1, 0);
   for (int s2 = 0; s2 < W; ++s2) roff[s2 + 1] = roff[s2] + cnt(s2, c->rank);
   struct Col {

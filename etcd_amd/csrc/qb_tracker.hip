@@ -298,3 +298,35 @@ extern "C" int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_
   QB_CHECK_LAUNCH("k_commit_advance");
   return QB_OK;
 }
+
+namespace qb {
+// Entries of stepdown_at that are not UINT32_MAX: a ballot per wave, one
+// atomic per wave with any (the check is for a caller's debug builds and
+// its once-per-config-change paths, not the tick).
+__global__ void k_stepdown_unarmed(u64 G, const u32* __restrict__ sd, u64* __restrict__ bad) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  const u64 m = __ballot(g < G && sd[g] != 0xFFFFFFFFu);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, u64(__popcll(m)));
+}
+}  // namespace qb
+
+extern "C" int qb_dev_stepdown_check_armed(uint64_t G, const uint32_t* stepdown_at,
+                                           uint64_t* bad_scratch, void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(stepdown_at && bad_scratch, "stepdown_at/bad_scratch NULL");
+  hipStream_t st = as_stream(stream);
+  hipError_t e = hipMemsetAsync(bad_scratch, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(bad)");
+  hipLaunchKernelGGL(k_stepdown_unarmed, dim3(grid_for(G)), dim3(kBlock), 0, st, G, stepdown_at,
+                     reinterpret_cast<u64*>(bad_scratch));
+  QB_CHECK_LAUNCH("k_stepdown_unarmed");
+  uint64_t bad = 0;
+  e = hipMemcpyAsync(&bad, bad_scratch, sizeof bad, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "stepdown check readback");
+  QB_REQUIRE(bad == 0,
+             "%llu group(s) enter the bucketed tracker step with stepdown_at != UINT32_MAX "
+             "(re-arm the groups that stepped down)",
+             (unsigned long long)bad);
+  return QB_OK;
+}

@@ -124,12 +124,13 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   for (u32 k = threadIdx.x; k < CH; k += B) act[k] = 0;
   __syncthreads();
   const u32 a0 = offs[0], run = offs[CH] - a0;
-  // A run longer than the buffer: the first launch defers the chunk to the
-  // second; in the second, only a table breaking its max_slots bound gets
-  // here, and the chunk takes the slow path (exact per-record semantics,
-  // global atomics).
+  // A run longer than the buffer: when a second launch exists (CAPW < WMAX)
+  // the first defers the chunk to it; otherwise (CAPW == WMAX, and in the
+  // second launch) only a table breaking its max_slots bound gets here, and
+  // the chunk takes the slow path (exact per-record semantics, global
+  // atomics) — no chunk is left deferred without a launch to apply it.
   const bool fits = run <= CAP;
-  if constexpr (!SECOND) {
+  if constexpr (!SECOND && CAPW < WMAX) {
     if (!fits) {  // block-uniform, before anything is written
       if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
       return;

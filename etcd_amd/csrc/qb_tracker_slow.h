@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
   // whole waves iterate together (CsrLay::ci is wave-cooperative)
   for (u64 g0 = u64(blockIdx.x) * kBlock; g0 < geo.G; g0 += stride) {
     const u64 g = g0 + threadIdx.x;
-    const bool mine = g < geo.G && chunk_slow[geo.chunk_of(u32(g))];
+    const bool mine = g < geo.G && chunk_slow[geo.chunk_of(u32(g))] == 1;
     if (__ballot(mine) == 0) continue;
     const u64 ci = lay.ci(match, mine ? u32(g) : u32(g0));
     if (!mine) continue;

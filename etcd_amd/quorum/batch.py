@@ -452,11 +452,20 @@ class FixedTracker:
         return advanced_out
 
     def step(self, batch: AppRespBatch, advanced_out: Optional[torch.Tensor] = None,
-             reset_stats: bool = True) -> Optional[torch.Tensor]:
+             reset_stats: bool = True, rearm: bool = True) -> Optional[torch.Tensor]:
         """One leader tick: apply the batch and run maybeCommit for every group
-        (qb_dev_fixed_tracker_step: records bucketed by group, LDS atomics)."""
+        (qb_dev_fixed_tracker_step: records bucketed by group, LDS atomics).
+
+        The C step requires ``stepdown_at`` to hold UINT32_MAX on entry and
+        writes it only for chunks holding a higher-term record
+        (include/quorum_batch.h).  ``rearm=True`` (default) refills it first,
+        so ``stepped_down()`` always describes this batch alone, as after
+        ``apply_appresp``; ``rearm=False`` is the Go caller's protocol (it
+        re-arms only the groups it stepped down; no per-group write per tick)."""
         if reset_stats:
             self.stats.zero_()
+        if rearm:
+            self.stepdown_at.fill_(-1)
         need = _lib.load().qb_fixed_tracker_workspace_bytes(self.n, self.G, batch.M)
         if getattr(self, "_ws", None) is None or self._ws.numel() < need:
             self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
@@ -497,7 +506,17 @@ class FixedTracker:
         return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}
 
     def stepped_down(self) -> torch.Tensor:
+        """Groups whose leader stepped down in the last batch (a higher-term
+        response, raft.go:875-879).  After ``step(..., rearm=False)`` a marker
+        from an earlier batch stays until the caller re-arms that group."""
         return self.stepdown_at != -1
+
+    def check_armed(self) -> None:
+        """Opt-in check of the bucketed step's entry rule (every stepdown_at
+        entry UINT32_MAX): qb_dev_stepdown_check_armed, synchronising."""
+        scratch = torch.empty(1, dtype=torch.int64, device=self.device)
+        _lib.call("qb_dev_stepdown_check_armed", self.G, _ptr(self.stepdown_at), _ptr(scratch),
+                  _stream(self.device))
 
 
 class CsrTracker:
@@ -546,9 +565,13 @@ class CsrTracker:
         return self.step(empty, advanced_out, reset_stats=False)
 
     def step(self, batch: AppRespBatch, advanced_out: Optional[torch.Tensor] = None,
-             reset_stats: bool = True) -> Optional[torch.Tensor]:
+             reset_stats: bool = True, rearm: bool = True) -> Optional[torch.Tensor]:
+        """One leader tick (qb_dev_csr_tracker_step); ``rearm`` as
+        FixedTracker.step."""
         if reset_stats:
             self.stats.zero_()
+        if rearm:
+            self.stepdown_at.fill_(-1)
         need = _lib.load().qb_csr_tracker_workspace_bytes(self.G, self.max_slots, batch.M)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
@@ -565,4 +588,14 @@ class CsrTracker:
         return {k: v[i] for i, k in enumerate(_lib.QB_STAT_NAMES)}
 
     def stepped_down(self) -> torch.Tensor:
+        """Groups whose leader stepped down in the last batch (a higher-term
+        response, raft.go:875-879).  After ``step(..., rearm=False)`` a marker
+        from an earlier batch stays until the caller re-arms that group."""
         return self.stepdown_at != -1
+
+    def check_armed(self) -> None:
+        """Opt-in check of the bucketed step's entry rule (every stepdown_at
+        entry UINT32_MAX): qb_dev_stepdown_check_armed, synchronising."""
+        scratch = torch.empty(1, dtype=torch.int64, device=self.device)
+        _lib.call("qb_dev_stepdown_check_armed", self.G, _ptr(self.stepdown_at), _ptr(scratch),
+                  _stream(self.device))

@@ -121,6 +121,37 @@ def _partition_host(cols, total, world, rank):
 
 
 _ROUTE_COLS = ("group", "flags", "index", "term", "hint", "log_term")
+_WIDE = (torch.int64, torch.uint64) if hasattr(torch, "uint64") else (torch.int64,)
+_INTS = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64) + _WIDE[1:]
+
+
+def _device_columns(cols: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """The column layout qb_dev_route_partition reads, whatever the caller
+    passed — as the host path accepts: group as int32 (any integer dtype,
+    masked to uint32 like the host path), flags uint8, the 8-byte columns
+    int64/uint64, every column contiguous and of one length.  An unsupported
+    dtype raises ValueError instead of being read as the wrong bytes."""
+    for need in ("group", "flags", "index", "term"):
+        if need not in cols:
+            raise ValueError(f"route_partition: column {need!r} is required")
+    M = cols["group"].numel()
+    out = {}
+    for name, col in cols.items():
+        if col.dim() != 1 or col.numel() != M:
+            raise ValueError(f"route_partition: column {name!r} must be 1-D of length {M}")
+        if name == "group":
+            if col.dtype not in _INTS:
+                raise ValueError(f"route_partition: group must be an integer tensor, not {col.dtype}")
+            if col.dtype != torch.int32:
+                col = (col.to(torch.int64) & 0xFFFFFFFF).to(torch.int32)  # wraps: uint32 bits
+        elif name == "flags":
+            if col.dtype not in (torch.uint8, torch.int8):
+                raise ValueError(f"route_partition: flags must be uint8, not {col.dtype}")
+            col = col.view(torch.uint8)
+        elif col.dtype not in _WIDE:
+            raise ValueError(f"route_partition: {name} must be int64/uint64, not {col.dtype}")
+        out[name] = col.contiguous()
+    return out
 
 
 def route_partition(cols: Dict[str, torch.Tensor], total: int, world: int):
@@ -133,6 +164,7 @@ def route_partition(cols: Dict[str, torch.Tensor], total: int, world: int):
     unknown = set(cols) - set(_ROUTE_COLS)
     if unknown:
         raise ValueError(f"route_partition: unknown columns {sorted(unknown)}")
+    cols = _device_columns(cols)
     dev = cols["group"].device
     M = cols["group"].numel()
     send = {name: torch.empty_like(col) for name, col in cols.items()}

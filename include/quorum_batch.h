@@ -286,7 +286,13 @@ int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
  *   - workspace: device scratch of qb_fixed_tracker_workspace_bytes(n, G, M)
  *     bytes (caller-owned, reusable across calls of the same or smaller
  *     size; no allocation inside, so the call can be graph-captured).
- * Requires G, M < 2^32. */
+ * Requires G, M < 2^32.
+ * qb_dev_stepdown_check_armed is the opt-in check of that entry rule (for a
+ * caller's debug builds): it counts the entries != UINT32_MAX on the device,
+ * synchronises the stream and returns QB_EINVAL naming the count if any
+ * (bad_scratch: one device uint64). */
+int qb_dev_stepdown_check_armed(uint64_t G, const uint32_t* stepdown_at,
+                                uint64_t* bad_scratch, void* stream);
 size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M);
 int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
                               const uint32_t* rec_group,

@@ -350,36 +350,40 @@ void orc_faithful_build_fixed(u32 n, u64 G, const u64* match, const void* voted,
   }
 }
 
-static u64 faithful_ci(const orc_group_maps* m) { /* majority.go:126-172 */
+/* MajorityConfig.CommittedIndex over a config table, each ID looked up in
+ * the progress table (majority.go:126-172, tracker.go:167-173). */
+static u64 faithful_half_ci(const u64* cfg_key, const u64* prs_key, const u64* prs_val) {
   int n = 0;
-  for (int k = 0; k < TBL; ++k) n += m->cfg_key[k] != 0;
-  if (n == 0) return INF;
+  for (int k = 0; k < TBL; ++k) n += cfg_key[k] != 0;
+  if (n == 0) return INF; /* majority.go:128-133 */
   u64 stk[7], *srt = stk, heap[TBL];
   if (n > 7) srt = heap;
   memset(srt, 0, sizeof(u64) * (size_t)n);
   int i = n - 1;
   for (int k = 0; k < TBL; ++k) { /* for id := range c */
-    u64 id = m->cfg_key[k];
+    u64 id = cfg_key[k];
     if (!id) continue;
     u32 p;
-    if (tbl_find(m->prs_key, id, &p)) srt[i--] = m->prs_val[p];
+    if (tbl_find(prs_key, id, &p)) srt[i--] = prs_val[p];
   }
   insertion_sort(srt, n);
   return srt[n - (n / 2 + 1)];
 }
 
-static u8 faithful_vote(const orc_group_maps* m) { /* majority.go:178-210 */
+/* MajorityConfig.VoteResult over a config table and the votes map
+ * (majority.go:178-210). */
+static u8 faithful_half_vote(const u64* cfg_key, const u64* vote_key, const u8* vote_val) {
   int n = 0, yes = 0, no = 0, missing = 0;
   for (int k = 0; k < TBL; ++k) {
-    u64 id = m->cfg_key[k];
+    u64 id = cfg_key[k];
     if (!id) continue;
     ++n;
     u32 p;
-    if (!tbl_find(m->vote_key, id, &p)) {
+    if (!tbl_find(vote_key, id, &p)) {
       ++missing;
       continue;
     }
-    if (m->vote_val[p]) ++yes;
+    if (vote_val[p]) ++yes;
     else ++no;
   }
   if (n == 0) return V_WON;
@@ -387,6 +391,69 @@ static u8 faithful_vote(const orc_group_maps* m) { /* majority.go:178-210 */
   if (yes >= q) return V_WON;
   if (yes + missing >= q) return V_PENDING;
   return V_LOST;
+}
+
+static u64 faithful_ci(const orc_group_maps* m) {
+  return faithful_half_ci(m->cfg_key, m->prs_key, m->prs_val);
+}
+
+static u8 faithful_vote(const orc_group_maps* m) {
+  return faithful_half_vote(m->cfg_key, m->vote_key, m->vote_val);
+}
+
+/* The CSR / joint form as the reference holds it: tracker.Config's
+ * JointConfig (two MajorityConfig maps, joint.go:22), the ProgressMap (every
+ * slot, learners included: ID -> Match) and the votes map.  IDs are slot + 1
+ * (slots are ascending IDs, MajorityConfig.Slice order). */
+typedef struct {
+  u64 in_key[TBL];
+  u64 out_key[TBL];
+  u64 prs_key[TBL];
+  u64 prs_val[TBL];
+  u64 vote_key[TBL];
+  u8 vote_val[TBL];
+} orc_joint_maps;
+
+size_t orc_joint_maps_size(void) { return sizeof(orc_joint_maps); }
+
+int orc_faithful_build_csr(u64 G, const u32* off, const u64* match, const u32* cfg,
+                           const u32* votes, orc_joint_maps* maps) {
+  for (u64 g = 0; g < G; ++g) {
+    orc_joint_maps* m = maps + g;
+    memset(m, 0, sizeof *m);
+    const u32 a = off[g], s = off[g + 1] - a;
+    if (s > 11) return -1; /* the tables hold <= 11 of 16 entries */
+    const u32 min_ = cfg[g] & 0xFFFF, mout = cfg[g] >> 16;
+    const u32 vd = votes ? votes[g] & 0xFFFF : 0, gr = votes ? votes[g] >> 16 : 0;
+    for (u32 j = 0; j < s; ++j) {
+      const u64 id = j + 1;
+      u32 p;
+      if ((min_ >> j) & 1) tbl_put(m->in_key, id, &p);
+      if ((mout >> j) & 1) tbl_put(m->out_key, id, &p);
+      tbl_put(m->prs_key, id, &p);
+      m->prs_val[p] = match[a + j];
+      if ((vd >> j) & 1) {
+        tbl_put(m->vote_key, id, &p);
+        m->vote_val[p] = (gr >> j) & 1;
+      }
+    }
+  }
+  return 0;
+}
+
+/* JointConfig.CommittedIndex / VoteResult (joint.go:49-75) over the maps. */
+void orc_faithful_joint_eval(u64 G, const orc_joint_maps* maps, u64* commit, u8* vote) {
+  for (u64 g = 0; g < G; ++g) {
+    const orc_joint_maps* m = maps + g;
+    if (commit) {
+      const u64 c0 = faithful_half_ci(m->in_key, m->prs_key, m->prs_val);
+      const u64 c1 = faithful_half_ci(m->out_key, m->prs_key, m->prs_val);
+      commit[g] = c0 < c1 ? c0 : c1;
+    }
+    if (vote)
+      vote[g] = joint_vote(faithful_half_vote(m->in_key, m->vote_key, m->vote_val),
+                           faithful_half_vote(m->out_key, m->vote_key, m->vote_val));
+  }
 }
 
 void orc_faithful_eval(u64 G, const orc_group_maps* maps, u64* commit, u8* vote) {
@@ -443,6 +510,9 @@ static void* orc_worker(void* p) {
   if (j->kind == 0) {
     orc_faithful_eval(cnt, (const orc_group_maps*)j->a + j->lo, j->commit ? j->commit + j->lo : 0,
                       j->vote ? j->vote + j->lo : 0);
+  } else if (j->kind == 3) {
+    orc_faithful_joint_eval(cnt, (const orc_joint_maps*)j->a + j->lo,
+                            j->commit ? j->commit + j->lo : 0, j->vote ? j->vote + j->lo : 0);
   } else if (j->kind == 1) {
     /* fixed layout, strided rows: evaluate groups lo..hi of the full table */
     for (u64 g = j->lo; g < j->hi; ++g) {
@@ -473,11 +543,12 @@ static void* orc_worker(void* p) {
   return 0;
 }
 
+#define ORC_MAX_THREADS 1024
 static void run_parallel(orc_job* proto, u64 G, int threads) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t tid[256];
-  orc_job jobs[256];
+  if (threads > ORC_MAX_THREADS) threads = ORC_MAX_THREADS;
+  pthread_t* tid = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+  orc_job* jobs = (orc_job*)malloc(sizeof(orc_job) * (size_t)threads);
   for (int t = 0; t < threads; ++t) {
     jobs[t] = *proto;
     jobs[t].lo = G * (u64)t / (u64)threads;
@@ -485,6 +556,8 @@ static void run_parallel(orc_job* proto, u64 G, int threads) {
     pthread_create(&tid[t], 0, orc_worker, &jobs[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(tid[t], 0);
+  free(tid);
+  free(jobs);
 }
 
 void orc_faithful_eval_mt(u64 G, const orc_group_maps* maps, u64* commit, u8* vote,
@@ -492,6 +565,17 @@ void orc_faithful_eval_mt(u64 G, const orc_group_maps* maps, u64* commit, u8* vo
   orc_job j;
   memset(&j, 0, sizeof j);
   j.kind = 0;
+  j.a = maps;
+  j.commit = commit;
+  j.vote = vote;
+  run_parallel(&j, G, threads);
+}
+
+void orc_faithful_joint_eval_mt(u64 G, const orc_joint_maps* maps, u64* commit, u8* vote,
+                                int threads) {
+  orc_job j;
+  memset(&j, 0, sizeof j);
+  j.kind = 3;
   j.a = maps;
   j.commit = commit;
   j.vote = vote;
@@ -576,11 +660,15 @@ static int commit_gate(u64 ci, u64 committed, u64 term_start) {
  * MaybeUpdate that returned true (raft.go:1259 -> 585-588).
  * Returns -1 if a record acks past the leader's log (index > last_index[g]),
  * which the reference treats as log corruption (log.go:239-241); else 0. */
-static int appresp_range(const orc_layout* L, u64 lo, u64 hi, u64 M, const u32* rg,
-                         const u8* rf, const u64* ri, const u64* rt, const u64* group_term,
-                         const u64* term_start, const u64* last_index, u64* match, u64* next,
-                         u16* active, u64* committed, u8* stepped_down, u64* stats) {
-  for (u64 i = 0; i < M; ++i) {
+static int appresp_range(const orc_layout* L, u64 lo, u64 hi, u64 M, const u32* order,
+                         const u32* rg, const u8* rf, const u64* ri, const u64* rt,
+                         const u64* group_term, const u64* term_start, const u64* last_index,
+                         u64* match, u64* next, u16* active, u64* committed, u8* stepped_down,
+                         u64* stats) {
+  /* order (nullable): the batch positions to visit, ascending — this
+   * partition's records only (appresp_run's owner partition); else 0..M-1 */
+  for (u64 k = 0; k < M; ++k) {
+    const u64 i = order ? order[k] : k;
     u64 g = rg[i];
     if (g >= L->G) {
       if (lo == 0) stats[5]++; /* counted once, by the first partition */
@@ -616,6 +704,7 @@ static int appresp_range(const orc_layout* L, u64 lo, u64 hi, u64 M, const u32* 
 typedef struct {
   const orc_layout* L;
   u64 lo, hi, M;
+  const u32* order;
   const u32* rg;
   const u8* rf;
   const u64 *ri, *rt, *gt, *ts, *last;
@@ -624,44 +713,109 @@ typedef struct {
   u8* sd;
   u64 stats[8];
   int rc;
+  /* owner partition (threads > 1) */
+  int phase, T, t;
+  u64 src_lo, src_hi;
+  u64* cnt; /* [T][T]: records of source slice t for owner d, then their positions */
+  u32* out;
 } orc_seq_job;
+
+/* The thread owning group g: the t with G*t/T <= g < G*(t+1)/T (a bad group
+ * goes to thread 0, which counts it once). */
+static inline int owner_of(u64 g, u64 G, int T) {
+  if (g >= G) return 0;
+  u64 d = (u64)(((unsigned __int128)g * (u64)T) / G);
+  while (d + 1 < (u64)T && G * (d + 1) / (u64)T <= g) ++d;
+  while (d > 0 && G * d / (u64)T > g) --d;
+  return (int)d;
+}
 
 static void* orc_seq_worker(void* p) {
   orc_seq_job* j = (orc_seq_job*)p;
-  j->rc = appresp_range(j->L, j->lo, j->hi, j->M, j->rg, j->rf, j->ri, j->rt, j->gt, j->ts,
-                        j->last, j->match, j->next, j->active, j->committed, j->sd, j->stats);
+  if (j->phase == 1) { /* count this source slice's records per owner */
+    u64* c = j->cnt + (u64)j->t * (u64)j->T;
+    for (u64 i = j->src_lo; i < j->src_hi; ++i) c[owner_of(j->rg[i], j->L->G, j->T)]++;
+  } else if (j->phase == 2) { /* scatter positions, stable */
+    u64* c = j->cnt + (u64)j->t * (u64)j->T;
+    for (u64 i = j->src_lo; i < j->src_hi; ++i) j->out[c[owner_of(j->rg[i], j->L->G, j->T)]++] = (u32)i;
+  } else {
+    j->rc = appresp_range(j->L, j->lo, j->hi, j->M, j->order, j->rg, j->rf, j->ri, j->rt, j->gt,
+                          j->ts, j->last, j->match, j->next, j->active, j->committed, j->sd,
+                          j->stats);
+  }
   return 0;
 }
 
+static void run_phase(orc_seq_job* jobs, pthread_t* tid, int T, int phase) {
+  for (int t = 0; t < T; ++t) {
+    jobs[t].phase = phase;
+    pthread_create(&tid[t], 0, orc_seq_worker, &jobs[t]);
+  }
+  for (int t = 0; t < T; ++t) pthread_join(tid[t], 0);
+}
+
+/* Sequential semantics on T threads: groups are partitioned into T ranges
+ * and the batch is stably partitioned by owner (count, scan, scatter of batch
+ * positions — each owner's list stays in batch order), then each thread
+ * replays its own records in batch order: exactly the one-thread result,
+ * with O(M) total work (a multi-raft host delivering each group's responses
+ * to the goroutine that owns it). */
 static int appresp_run(const orc_layout* L, u64 M, const u32* rg, const u8* rf, const u64* ri,
                        const u64* rt, const u64* group_term, const u64* term_start,
                        const u64* last_index, u64* match, u64* next, u16* active,
                        u64* committed, u8* stepped_down, u64* stats, int threads) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t tid[256];
-  orc_seq_job* jobs = (orc_seq_job*)calloc((size_t)threads, sizeof(orc_seq_job));
-  if (!jobs) return -2;
-  for (int t = 0; t < threads; ++t) {
+  if (threads > ORC_MAX_THREADS) threads = ORC_MAX_THREADS;
+  if ((u64)threads > L->G) threads = L->G ? (int)L->G : 1;
+  const int T = threads;
+  orc_seq_job* jobs = (orc_seq_job*)calloc((size_t)T, sizeof(orc_seq_job));
+  pthread_t* tid = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+  u64* cnt = T > 1 ? (u64*)calloc((size_t)T * (size_t)T, sizeof(u64)) : 0;
+  u32* order = T > 1 ? (u32*)malloc(sizeof(u32) * (M ? M : 1)) : 0;
+  if (!jobs || !tid || (T > 1 && (!cnt || !order))) {
+    free(jobs), free(tid), free(cnt), free(order);
+    return -2;
+  }
+  for (int t = 0; t < T; ++t) {
     orc_seq_job* j = &jobs[t];
-    memset(j, 0, sizeof *j);
     j->L = L;
-    j->lo = L->G * (u64)t / (u64)threads;
-    j->hi = L->G * (u64)(t + 1) / (u64)threads;
+    j->lo = L->G * (u64)t / (u64)T;
+    j->hi = L->G * (u64)(t + 1) / (u64)T;
     j->M = M;
     j->rg = rg, j->rf = rf, j->ri = ri, j->rt = rt, j->gt = group_term, j->ts = term_start;
     j->last = last_index, j->match = match, j->next = next, j->active = active;
     j->committed = committed, j->sd = stepped_down;
-    if (threads == 1) orc_seq_worker(j);
-    else pthread_create(&tid[t], 0, orc_seq_worker, j);
+    j->T = T, j->t = t, j->cnt = cnt, j->out = order;
+    j->src_lo = M * (u64)t / (u64)T;
+    j->src_hi = M * (u64)(t + 1) / (u64)T;
+  }
+  if (T == 1) {
+    orc_seq_worker(&jobs[0]);
+  } else {
+    run_phase(jobs, tid, T, 1);
+    /* owner-major, then source-major exclusive scan: cnt[t][d] becomes the
+     * first position of source t's records for owner d */
+    u64 run = 0;
+    for (int d = 0; d < T; ++d) {
+      const u64 start = run;
+      for (int t = 0; t < T; ++t) {
+        const u64 c = cnt[(u64)t * T + d];
+        cnt[(u64)t * T + d] = run;
+        run += c;
+      }
+      jobs[d].order = order + start;
+    }
+    run_phase(jobs, tid, T, 2);
+    /* after the scatter, cnt[T-1][d] is the end of owner d's list */
+    for (int d = 0; d < T; ++d) jobs[d].M = cnt[(u64)(T - 1) * T + d] - (u64)(jobs[d].order - order);
+    run_phase(jobs, tid, T, 3);
   }
   int rc = 0;
-  for (int t = 0; t < threads; ++t) {
-    if (threads > 1) pthread_join(tid[t], 0);
+  for (int t = 0; t < T; ++t) {
     for (int k = 0; k < 8; ++k) stats[k] += jobs[t].stats[k];
     if (jobs[t].rc) rc = jobs[t].rc;
   }
-  free(jobs);
+  free(jobs), free(tid), free(cnt), free(order);
   return rc;
 }
 

@@ -28,6 +28,10 @@ SIG = {
     "orc_faithful_build_fixed": (None, [_u32, _u64, _p, _p, _p, _p]),
     "orc_faithful_eval": (None, [_u64, _p, _p, _p]),
     "orc_faithful_eval_mt": (None, [_u64, _p, _p, _p, _i32]),
+    "orc_joint_maps_size": (C.c_size_t, []),
+    "orc_faithful_build_csr": (_i32, [_u64, _p, _p, _p, _p, _p]),
+    "orc_faithful_joint_eval": (None, [_u64, _p, _p, _p]),
+    "orc_faithful_joint_eval_mt": (None, [_u64, _p, _p, _p, _i32]),
     "orc_fixed_eval_mt": (None, [_u32, _u64, _p, _p, _p, _p, _p, _i32]),
     "orc_csr_eval_mt": (None, [_u64, _p, _p, _p, _p, _p, _p, _i32]),
     "orc_fixed_appresp_sequential": (_i32, [_u32, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p,
@@ -153,6 +157,29 @@ def faithful_eval(maps, G, threads=1):
         lib.orc_faithful_eval_mt(G, ptr(maps), ptr(commit), ptr(vote), threads)
     else:
         lib.orc_faithful_eval(G, ptr(maps), ptr(commit), ptr(vote))
+    return commit, vote
+
+
+def faithful_csr_maps(off, match, cfg, votes):
+    """Per-group Go-map tables of the CSR/joint form (oracle/quorum_oracle.c
+    orc_faithful_build_csr): JointConfig maps, ProgressMap, votes map."""
+    lib = load()
+    G = len(cfg)
+    maps = np.empty(max(G, 1) * lib.orc_joint_maps_size(), np.uint8)
+    m = match if match.size else np.zeros(1, np.uint64)
+    rc = lib.orc_faithful_build_csr(G, ptr(off), ptr(m), ptr(cfg), ptr(votes), ptr(maps))
+    assert rc == 0, "a group has more than 11 slots"
+    return maps
+
+
+def faithful_joint_eval(maps, G, threads=1):
+    lib = load()
+    commit = np.empty(G, np.uint64)
+    vote = np.empty(G, np.uint8)
+    if threads > 1:
+        lib.orc_faithful_joint_eval_mt(G, ptr(maps), ptr(commit), ptr(vote), threads)
+    else:
+        lib.orc_faithful_joint_eval(G, ptr(maps), ptr(commit), ptr(vote))
     return commit, vote
 
 

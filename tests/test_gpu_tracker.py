@@ -257,7 +257,7 @@ def test_pipelined_bucket_apply_equals_step():
                           torch.where(torch.rand(M, generator=gen, device=dev) < 0.001, 8, 7))
         batches.append(qb.AppRespBatch(grp, (slot | rej).to(torch.uint8), idx, trm.to(torch.int64)))
     for bt in batches:
-        a.step(bt, reset_stats=False)
+        a.step(bt, reset_stats=False, rearm=False)
     wss = [b.workspace(M), b.workspace(M)]
     side = torch.cuda.Stream(dev)
     main = torch.cuda.current_stream(dev)
@@ -276,3 +276,27 @@ def test_pipelined_bucket_apply_equals_step():
     torch.cuda.synchronize()
     for name in ("match", "committed", "active", "stepdown_at", "stats"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+def test_stepdown_entry_rule_check_and_rearm():
+    """The bucketed step's entry rule (stepdown_at all UINT32_MAX) is checked
+    on request (qb_dev_stepdown_check_armed); the Python step re-arms by
+    default, so stepped_down() names this batch's step-downs only."""
+    from etcd_amd._lib import QuorumBatchError
+    n, G = 5, 5000
+    rng = np.random.default_rng(17)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st, track_next=False)
+    tr.check_armed()
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, G, st, higher=0.01)
+    b = batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV)
+    tr.step(b, rearm=False)
+    down = int(tr.stepped_down().sum().item())
+    assert down > 0
+    with pytest.raises(QuorumBatchError, match=f"{down} group"):
+        tr.check_armed()
+    # a batch with no higher-term record: rearm=True clears the old markers
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, G, st, higher=0.0)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    assert int(tr.stepped_down().sum().item()) == 0
+    tr.check_armed()

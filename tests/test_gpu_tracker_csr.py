@@ -214,7 +214,7 @@ def test_csr_stepdown_untouched_outside_flagged_chunks():
     hi = 12345                              # one higher-term record, group 12345
     group[7], slot[7], term[7] = hi, 0, st["term"][hi] + np.uint64(3)
     tr.stepdown_at.fill_(777)
-    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV), rearm=False)
     sd = tr.stepdown_at.cpu().numpy().view(np.uint32)
     CH = 512  # groups per K5 chunk (qb_bucket.h csr_chunk_groups)
     lo, hi_end = (hi // CH) * CH, min(G, (hi // CH + 1) * CH)
@@ -267,6 +267,51 @@ def test_csr_step_deferred_chunks(lo_slots, track_next):
         want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
                          "bad_group", "after_stepdown"), stats.tolist()))
         assert got == want
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
+
+
+@pytest.mark.parametrize("max_slots", [4, 8])
+def test_csr_step_bound_breaking_chunk_takes_slow_path(max_slots):
+    """max_slots 4 / 8 (no second K5 launch: the first launch's buffer is
+    already max_slots wide): a chunk whose run is longer than its buffer —
+    only a table breaking its max_slots bound has one — goes to the exact
+    slow path instead of being dropped.  Voters sit in the first
+    three slots and the records address slots below the bound, so the
+    result is the sequential oracle's exactly."""
+    CH = 512
+    G, M = 4 * CH + 100, 30000
+    rng = np.random.default_rng(max_slots)
+    sizes = np.full(G, max_slots, np.int64)
+    wide = rng.choice(CH, size=12, replace=False)          # chunk 0 breaks the bound
+    sizes[wide] = max_slots + 2
+    sizes[2 * CH + 5] = max_slots + 1                     # and chunk 2 (one group)
+    sizes[3 * CH + 7] = 3                                 # chunk 3 stays within
+    off = np.zeros(G + 1, np.uint32)
+    off[1:] = np.cumsum(sizes).astype(np.uint32)
+    cfg = np.full(G, 0b111, np.uint32)
+    cfg[::3] = 0b111 | (0b110 << 16)                      # some joint configs
+    S = int(off[-1])
+    last = rng.integers(1 << 20, 1 << 40, size=G).astype(np.uint64)
+    match = np.repeat(last, sizes) - rng.integers(0, 200, size=S).astype(np.uint64)
+    st = {"match": match, "next": match + np.uint64(1), "active": np.zeros(G, np.uint16),
+          "term": rng.integers(2, 9, size=G).astype(np.uint64),
+          "term_start": last - rng.integers(0, 300, size=G).astype(np.uint64),
+          "last_index": last, "committed": np.zeros(G, np.uint64),
+          "stepped_down": np.zeros(G, np.uint8)}
+    oc.csr_commit_all(off, cfg, st["match"], st["term_start"], st["committed"])
+    tr = _tracker(off, cfg, st, max_slots=max_slots)
+    assert tr.max_slots == max_slots
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(2):
+        bounded = np.minimum(sizes, max_slots)
+        group, slot, index, term, rej, flags = _batch(rng, G, M, bounded, seq, stale=0.02)
+        stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, G)
+        want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                         "bad_group", "after_stepdown"), stats.tolist()))
+        assert tr.stats_dict() == want
         tr.stepdown_at.fill_(-1)
         seq["stepped_down"][:] = 0
 

@@ -205,3 +205,56 @@ def test_wide_eval_matches_python():
         votes = {j: bool(flags[j] & 8) for j in range(a, b) if flags[j] & 4}
         assert int(c[g]) == q.joint_committed_index(c0, c1, acked)
         assert int(v[g]) == q.joint_vote_result(c0, c1, votes)
+
+
+@pytest.mark.parametrize("csr", [False, True])
+@pytest.mark.parametrize("threads", [2, 7, 64])
+def test_sequential_appresp_owner_partition_equals_one_thread(csr, threads):
+    """The multi-thread sequential restatement (groups partitioned over
+    threads, the batch stably partitioned by owner) gives exactly the
+    one-thread result: state, step-downs and every stat counter, with
+    duplicates, higher terms, bad groups and non-members in the batch."""
+    rng = np.random.default_rng(threads * 3 + csr)
+    G, M = 3001, 40000
+    if csr:
+        off, match, cfg, _ = oc.gen_csr(0x5EED0003, "joint", G)
+        sizes = np.diff(off.astype(np.int64))
+    else:
+        match, _, _, _ = oc.gen_fixed(0x5EED0005, 5, G)
+        sizes = np.full(G, 5)
+    term = rng.integers(2, 9, size=G).astype(np.uint64)
+    st = {"match": match.copy(), "active": np.zeros(G, np.uint16), "term": term,
+          "term_start": np.zeros(G, np.uint64), "committed": np.zeros(G, np.uint64),
+          "stepped_down": np.zeros(G, np.uint8)}
+    group = rng.integers(0, G + 3, size=M).astype(np.uint32)
+    gg = np.minimum(group, G - 1)
+    slot = (rng.integers(0, 1 << 20, size=M) % (sizes[gg] + 1)).astype(np.uint8)
+    flags = (slot | ((rng.random(M) < 0.1).astype(np.uint8) << 7)).astype(np.uint8)
+    index = rng.integers(0, 1 << 40, size=M).astype(np.uint64)
+    rterm = (term[gg].astype(np.int64) + rng.choice([0, 0, 0, 0, -1, 1], size=M)).astype(np.uint64)
+    rec = (group, flags, index, rterm)
+    one = {k: v.copy() for k, v in st.items()}
+    many = {k: v.copy() for k, v in st.items()}
+    if csr:
+        s1 = oc.csr_appresp_sequential(off, cfg, rec, one, threads=1)
+        sT = oc.csr_appresp_sequential(off, cfg, rec, many, threads=threads)
+    else:
+        s1 = oc.appresp_sequential(5, G, rec, one, threads=1)
+        sT = oc.appresp_sequential(5, G, rec, many, threads=threads)
+    assert s1.tolist() == sT.tolist() and int(s1.sum()) == M
+    for k in one:
+        assert np.array_equal(one[k], many[k]), k
+
+
+@pytest.mark.parametrize("kind", ["ragged", "joint"])
+def test_faithful_joint_maps_agree_with_soa(kind):
+    """The Go-map restatement of the CSR/joint form (JointConfig of two
+    MajorityConfig maps, ProgressMap incl. learners, votes map) equals the
+    SoA restatement on the same synthetic groups, one thread and many."""
+    off, match, cfg, votes = oc.gen_csr(0x5EED0003, kind, 20000)
+    c0, v0 = oc.csr_eval(off, match, cfg, votes)
+    maps = oc.faithful_csr_maps(off, match, cfg, votes)
+    c1, v1 = oc.faithful_joint_eval(maps, 20000)
+    c2, v2 = oc.faithful_joint_eval(maps, 20000, threads=5)
+    assert np.array_equal(c0, c1) and np.array_equal(v0, v1)
+    assert np.array_equal(c0, c2) and np.array_equal(v0, v2)
