@@ -7,7 +7,8 @@ slot-major SoA layout.  One step = one pass of the hot path over one batch
 of 2^20 groups.  ``--batches`` distinct batches (default 16, ~0.96 GB with
 outputs) stay resident in HBM and are visited round-robin, so every step
 streams its batch from HBM instead of the 256 MB Infinity Cache (the
-MALL-warm single-batch rate is reported beside it as ``value_mall_warm``).
+MALL-warm single-batch rate is reported beside it as ``value_mall_warm``,
+timed exactly as the headline).
 
 Launch pipeline: consecutive steps are independent batches, so they are
 issued round-robin on ``--streams`` HIP streams (default 2): the tail of one
@@ -15,15 +16,24 @@ launch overlaps the ramp of the next.  HIP events on the launch streams bracket
 the timed region; the per-launch duration used for the roofline is the
 region's device time / K.
 
-``--workload ragged|joint`` runs BASELINE configs[2] / configs[3] instead
-(16M ragged 3-9-voter groups with learners / 8M JointConfig 5+5 groups per
-GPU, CSR layout, ``k_csr``) with the same timing and JSON contract; the default
-stays configs[1], the metric's headline config.
+``--workload ragged|joint`` runs BASELINE configs[2] / configs[3] (16M ragged
+3-9-voter groups with learners / 8M JointConfig 5+5 groups per GPU, CSR
+layout); ``--workload tracker|tracker-csr`` runs configs[4] (the streaming
+MsgAppResp tracker step, 16M groups per GPU).  The default stays configs[1],
+the metric's headline config.
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL), groups sharded by
-global group number (weak scaling, no collective in the timed region); for
-N > 1 the node-wide all-gather of one batch's commit/vote vectors is timed
-separately (``allgather_ms``).
+Parity: after the timed region every workload checks its own output against
+the C oracle (oracle/quorum_oracle.c) bit for bit and reports ``"parity"``;
+a mismatch exits non-zero.
+
+Multi-GPU: one process per GPU.  ``--gpus N`` with no launcher spawns the N
+ranks itself (children get RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; the
+parent touches no GPU); under torchrun ``--gpus`` must equal WORLD_SIZE.
+Groups shard by global group number (weak scaling, no collective in the
+timed region).  For N > 1 the node-wide collectives are timed after the
+region through the C ABI's RCCL communicator (etcd_amd/comm.py:
+qb_dev_allgather_results, qb_dev_route_records — what a Go embedder binds),
+and rank 0 checks the gathered vector against the oracle.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -33,6 +43,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -45,11 +57,11 @@ sys.path.insert(0, ROOT)
 
 from etcd_amd import _lib  # noqa: E402
 from etcd_amd.quorum import batch  # noqa: E402
-from etcd_amd.shard import allgather_results  # noqa: E402
 
 METRIC = "raft groups quorum-evaluated/sec (1 and 8 GPUs) + % peak HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SEED = 0x5EED0002      # 0x5EED0001 + config#
+CSR_SEED = {"ragged": 0x5EED0003, "joint": 0x5EED0004}
 
 
 def bytes_per_group(n: int) -> int:
@@ -58,6 +70,71 @@ def bytes_per_group(n: int) -> int:
     mb = 1 if n <= 8 else 2
     return 8 * n + 2 * mb + 8 + 1
 
+
+# ------------------------------------------------------------- launcher ---
+
+def launch_envs(n: int, base: dict, port: int):
+    """The environment of each of the n ranks ``--gpus n`` spawns (the
+    variables torch.distributed.run sets; 127.0.0.1 rendezvous)."""
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+        envs.append(e)
+    return envs
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n child ranks of this same command (before any GPU call in this
+    process: no exec, children are separate processes) and wait; returns the
+    first non-zero exit code (the others are then terminated) or 0."""
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e)
+             for e in launch_envs(n, os.environ, port)]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def resolve_world(gpus: int, env) -> tuple:
+    """(world, rank, local_rank, spawn): under a launcher WORLD_SIZE must
+    equal --gpus; without one, --gpus > 1 means spawn."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} "
+                             "ranks; they must agree")
+        return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0")), False
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return gpus, 0, 0, gpus > 1
+
+
+# --------------------------------------------------------------- timing ---
 
 class HipEvents:
     """Raw hipEvent timing on an arbitrary stream (the stream the kernels are
@@ -90,6 +167,36 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
+def timed_region(run, streams, K, barrier):
+    """K steps between barrier + synchronize.  Device time = from the earliest
+    start event to the latest end event, one event pair per launch stream
+    (no cross-stream hop inside the region: a fork + join around a 20-step
+    region cost ~30 us of device time).  The start events are recorded after
+    the barrier (device idle, so they stamp at once) and before t0; the wall
+    clock stops when the host sees every stream's end event complete, then
+    the device-wide synchronize runs (a torch.cuda.synchronize() costs ~20 us
+    more than the event waits, 10 % of a 20-step region).
+    Returns (wall seconds, device seconds per step)."""
+    TS = len(streams)
+    ev = HipEvents(2 * TS)
+    barrier()
+    for s_, st in enumerate(streams):
+        ev.record(ev.ev[s_], st.cuda_stream)
+    t0 = time.perf_counter()
+    run()
+    for s_, st in enumerate(streams):
+        ev.record(ev.ev[TS + s_], st.cuda_stream)
+    for s_ in range(TS):
+        ev.synchronize(TS + s_)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    barrier()
+    starts = [0.0] + [ev.elapsed_ms(0, s_) for s_ in range(1, TS)]
+    ends = [ev.elapsed_ms(0, TS + s_) for s_ in range(TS)]
+    ev.close()
+    return t1 - t0, (max(ends) - min(starts)) / 1e3 / K
+
+
 def load_traffic(workload_key: str):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (written by
     tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this
@@ -103,57 +210,93 @@ def load_traffic(workload_key: str):
         return None
 
 
-def cpu_baseline(n: int, sample_groups: int, seconds: float):
-    """The oracle's faithful C restatement of the Go loop (per-group hash-map
-    MajorityConfig + AckedIndexer lookups + insertionSort, majority.go:126-210)
-    timed on the host cores over a bounded sample of the same workload."""
-    from tests import oracle_c as oc
-    threads = max(1, min(16, os.cpu_count() or 1))
-    match, vd, gr, _ = oc.gen_fixed(SEED, n, sample_groups)
-    maps = oc.faithful_maps(n, match, vd, gr)
+# ---------------------------------------------------------- CPU baseline ---
 
-    def rate(th):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            oc.faithful_eval(maps, sample_groups, threads=th)
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds:
-                return reps * sample_groups / dt, reps
+def host_cpu_info() -> dict:
+    """The host the CPU baseline runs on (core count, CPU model,
+    thread count)."""
+    info = {"logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "model": None, "physical_cores": None, "cgroup_cpu_quota": None}
+    try:
+        cores = set()
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and info["model"] is None:
+                    info["model"] = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+        info["physical_cores"] = len(cores) or None
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            info["cgroup_cpu_quota"] = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    return info
 
-    r1, reps1 = rate(1)
-    rn, repsn = rate(threads)
-    return {
-        "value": rn, "unit": "groups/s", "cores": threads, "kind": "port",
-        "sample": (f"{sample_groups} groups x {n} voters (same synthetic spec), faithful C "
-                   f"restatement of majority.go CommittedIndex+VoteResult with Go-map-style "
-                   f"hash lookups; {repsn} passes on {threads} threads (GOMAXPROCS-equivalent "
-                   f"{threads}); 1 thread: {r1:.4g} groups/s over {reps1} passes"),
-        "value_1thread": r1,
-    }
 
-
-def cpu_baseline_csr(kind: str, seconds: float):
-    """The oracle's C SoA restatement (majority.go / joint.go per group) on a
-    bounded 1M-group sample of the same CSR workload, 16 host threads."""
-    from tests import oracle_c as oc
-    threads = max(1, min(16, os.cpu_count() or 1))
-    gs = 1 << 20
-    seed = {"ragged": 0x5EED0003, "joint": 0x5EED0004}[kind]
-    off, m, cfg, votes = oc.gen_csr(seed, kind, gs)
+def _rate(fn, units, seconds):
+    """units/s of fn() repeated for >= seconds (at least once)."""
     reps, t0 = 0, time.perf_counter()
     while True:
-        oc.csr_eval(off, m, cfg, votes, threads=threads)
+        fn()
         reps += 1
         dt = time.perf_counter() - t0
         if dt >= seconds:
-            break
-    return {"value": reps * gs / dt, "unit": "groups/s", "cores": threads, "kind": "port",
-            "sample": f"{gs} groups of the same {kind} workload, C SoA restatement of "
-                      f"majority.go/joint.go (oracle/quorum_oracle.c); {reps} passes on "
-                      f"{threads} threads"}
+            return reps * units / dt, reps
 
-# ------------------------------------------------------------------ tracker ---
+
+def cpu_baseline_eval(workload: str, n: int, seconds: float):
+    """configs[1]-[3]: the oracle's two C restatements of the Go loop on a
+    bounded 1M-group sample of the same workload, 1 thread and N = all host
+    cores (BASELINE.md:21): the faithful one (Go-map MajorityConfig /
+    JointConfig, ProgressMap and votes map, insertionSort; majority.go:126-210,
+    joint.go:49-75) — the value — and the SoA one beside it."""
+    from tests import oracle_c as oc
+    info = host_cpu_info()
+    N = info["affinity_cpus"]
+    gs = 1 << 20
+    if workload == "fixed":
+        match, vd, gr, _ = oc.gen_fixed(SEED, n, gs)
+        maps = oc.faithful_maps(n, match, vd, gr)
+        faithful = lambda th: oc.faithful_eval(maps, gs, threads=th)  # noqa: E731
+        soa = lambda th: oc.fixed_eval(n, match, vd, gr, threads=th)  # noqa: E731
+        what = f"{gs} groups x {n} voters"
+    else:
+        off, m, cfg, votes = oc.gen_csr(CSR_SEED[workload], workload, gs)
+        maps = oc.faithful_csr_maps(off, m, cfg, votes)
+        faithful = lambda th: oc.faithful_joint_eval(maps, gs, threads=th)  # noqa: E731
+        soa = lambda th: oc.csr_eval(off, m, cfg, votes, threads=th)  # noqa: E731
+        what = f"{gs} groups of the same {workload} workload"
+    legs = {}
+    for name, f in (("faithful", faithful), ("soa", soa)):
+        for th in (1, N):
+            legs[f"{name}_{th}t"] = _rate(lambda: f(th), gs, seconds / 4)[0]
+    return {
+        "value": legs[f"faithful_{N}t"], "unit": "groups/s", "cores": N, "kind": "port",
+        "threads": N, "gomaxprocs_equivalent": N, "host": info, "legs": legs,
+        "sample": (f"{what} (same synthetic spec); value = faithful C restatement of the Go loop "
+                   f"(Go-map configs + AckedIndexer lookups + insertionSort, majority.go:126-210, "
+                   f"joint.go:49-75) on {N} threads (all cores of the process's affinity, "
+                   f"GOMAXPROCS-equivalent {N}); legs: faithful and SoA restatements at 1 and {N} "
+                   f"threads"),
+    }
+
+
+# ------------------------------------------------------------- tracker ---
 # BASELINE configs[4]: "Streaming ProgressTracker: batched MsgAppResp
 # scatter-max + commit advance, 128M groups x8 GPUs" = 16M 5-voter groups per
 # GPU.  One step = one qb_dev_fixed_tracker_step over one batch of G records
@@ -171,6 +314,7 @@ TRACKER_MAX_BATCHES = 64
 # + match RMW 16 B + commit advance 64 B (match 40 + term_start 8 + committed 8
 # read, committed 8 written)
 TRACKER_BYTES = 101
+TRACKER_STATE = ("match", "committed", "active", "stepdown_at")
 
 
 def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7):
@@ -187,92 +331,17 @@ def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7):
     return out
 
 
-def tracker_cpu_baseline(seconds: float, csr: bool):
-    """The oracle's sequential stepLeader restatement (one record at a time in
-    batch order: term filter, MaybeUpdate, maybeCommit when updated;
-    oracle/quorum_oracle.c appresp_range) on a bounded sample of the same
-    stream: 1M groups, 8 consecutive 1M-record batches per pass, groups
-    partitioned over 16 host threads (each scans the batch for its own groups
-    — exactly the sequential result) and on 1 thread."""
-    from tests import oracle_c as oc
-    threads = max(1, min(16, os.cpu_count() or 1))
-    Gs, R, n = 1 << 20, 8, 5
-    rng = np.random.default_rng(5)
-    if csr:
-        off, m0, cfg, _ = oc.gen_csr(0x5EED0003, "ragged", Gs)
-        sizes = np.diff(off.astype(np.int64))
-        last = m0[off[:-1]].copy()            # slot 0 holds the leader's own match
-        ts0 = last - np.uint64(64)
-    else:
-        m0, _, _, ts0 = oc.gen_fixed(TRACKER_SEED, n, Gs)
-        last = m0[0].copy()
-    batches = []
-    for k in range(R):
-        grp = rng.integers(0, Gs, size=Gs).astype(np.uint32)
-        if csr:
-            slot = (1 + (rng.integers(0, 1 << 30, size=Gs) % (sizes[grp] - 1))).astype(np.uint8)
-        else:
-            slot = rng.integers(1, n, size=Gs).astype(np.uint8)
-        lag = rng.integers(0, 96, size=Gs).astype(np.uint64)
-        idx = last[grp] + np.uint64((k + 1) * TRACKER_E) - lag
-        trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
-        batches.append((grp, slot, idx, trm))
-    m_start = m0.copy()
-    if csr:
-        m_start[off[:-1]] = last + np.uint64(R * TRACKER_E)
-    else:
-        m_start[0] = last + np.uint64(R * TRACKER_E)
-
-    def fresh():
-        st = {"match": m_start.copy(), "active": np.zeros(Gs, np.uint16),
-              "term": np.full(Gs, 7, np.uint64), "term_start": ts0.copy(),
-              "committed": np.zeros(Gs, np.uint64), "stepped_down": np.zeros(Gs, np.uint8)}
-        if csr:
-            oc.csr_commit_all(off, cfg, st["match"], ts0, st["committed"])
-        else:
-            oc.commit_all(n, st["match"], ts0, st["committed"])
-        return st
-
-    def rate(th):
-        busy, passes = 0.0, 0
-        while busy < seconds:
-            st = fresh()
-            t = time.perf_counter()
-            for b in batches:
-                if csr:
-                    oc.csr_appresp_sequential(off, cfg, b, st, threads=th)
-                else:
-                    oc.appresp_sequential(n, Gs, b, st, threads=th)
-            busy += time.perf_counter() - t
-            passes += 1
-        return passes * R * Gs / busy, passes
-
-    rn, pn = rate(threads)
-    r1, p1 = rate(1)
-    return {"value": rn, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": (f"{Gs} {'ragged CSR' if csr else '5-voter'} groups x {R} consecutive "
-                       f"{Gs}-record batches of the same stream per pass, {pn} passes on {threads} "
-                       f"threads (groups partitioned; GOMAXPROCS-equivalent {threads}); "
-                       f"1 thread: {r1:.4g} group-steps/s over {p1} passes; sequential C "
-                       f"restatement of stepLeader's MsgAppResp path (oracle/quorum_oracle.c)"),
-            "value_1thread": r1}
-
-
-def tracker_main(args, world, rank, dev):
-    from etcd_amd.shard import route_records
-    csr = args.workload == "tracker-csr"
-    G = args.groups if args.groups != 1 << 20 else 1 << 24
-    K = args.steps if args.steps != 1000 else 20
-    W = args.warmup if args.warmup is not None else 4
-    nb = W + K
-    if nb > TRACKER_MAX_BATCHES:
-        raise SystemExit(f"--workload {args.workload} keeps one distinct batch per step resident: "
-                         f"--steps + --warmup must be <= {TRACKER_MAX_BATCHES}")
+def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool):
+    """The configs[4] stream as the bench runs it: the leader state (after
+    the initial maybeCommit, the leader's own match raised to the last of the
+    nb * E entries it appended) and the nb device batches.  Returns
+    (tracker, batches, info).  tests/ replays exactly this stream on the
+    oracle."""
     n = 5
     gen = torch.Generator(device=dev)
     gen.manual_seed(TRACKER_SEED + 7919 * rank)
     if csr:
-        grp = batch.CsrGroups.synth(0x5EED0003, "ragged", G, g_begin=rank * G, device=dev)
+        grp = batch.CsrGroups.synth(CSR_SEED["ragged"], "ragged", G, g_begin=rank * G, device=dev)
         tr = batch.CsrTracker(grp.off, grp.cfg, max_slots=grp.max_slots, device=dev)
         tr.match.copy_(grp.match[: tr.S])
         first = grp.off[:-1].long()
@@ -307,11 +376,153 @@ def tracker_main(args, world, rank, dev):
         tr.match[first] = last + nb * TRACKER_E   # the leader appended nb*E entries
     else:
         tr.match[0].copy_(last + nb * TRACKER_E)
-    names = ("match", "committed", "active", "stepdown_at")
-    snap = {k: getattr(tr, k).clone() for k in names}
+    torch.cuda.synchronize(dev)
+    return tr, batches, {"slots_mean": slots_mean, "voters_mean": voters_mean, "gen": gen}
+
+
+def tracker_host_state(tr, csr: bool, Gs: int):
+    """The first Gs groups of a tracker's state as the oracle's numpy dict
+    (off and cfg as well for the CSR layout)."""
+    Gs = min(Gs, tr.G)
+    if csr:
+        off = tr.off[: Gs + 1].cpu().numpy().view(np.uint32).copy()
+        S = int(off[-1])
+        match = batch.as_u64(tr.match[:S]).copy() if S else np.zeros(0, np.uint64)
+        cfg = tr.cfg[:Gs].cpu().numpy().view(np.uint32).copy()
+    else:
+        off = cfg = None
+        match = batch.as_u64(tr.match[:, :Gs]).copy()
+    st = {"match": match, "committed": batch.as_u64(tr.committed[:Gs]).copy(),
+          "active": tr.active[:Gs].cpu().numpy().view(np.uint16).copy(),
+          "term": batch.as_u64(tr.term[:Gs]).copy(),
+          "term_start": batch.as_u64(tr.term_start[:Gs]).copy(),
+          "stepped_down": (tr.stepdown_at[:Gs] != -1).cpu().numpy().astype(np.uint8)}
+    return off, cfg, st
+
+
+def host_records(b, Gs: int):
+    """The batch's records for groups < Gs, in batch order, as numpy."""
+    keep = (b.group.long() & 0xFFFFFFFF) < Gs
+    return (b.group[keep].cpu().numpy().view(np.uint32).copy(),
+            b.flags[keep].cpu().numpy().copy(),
+            batch.as_u64(b.index[keep]).copy(), batch.as_u64(b.term[keep]).copy())
+
+
+def tracker_state_mismatches(tr, csr, st, Gs):
+    """Fields where the device state of the first Gs groups differs from the
+    oracle's ``st``."""
+    _, _, dev_st = tracker_host_state(tr, csr, Gs)
+    return [k for k in ("match", "committed", "active", "stepped_down")
+            if not np.array_equal(dev_st[k], st[k])]
+
+
+def tracker_cpu_baseline(seconds: float, csr: bool):
+    """The oracle's sequential stepLeader restatement (one record at a time in
+    batch order: term filter, MaybeUpdate, maybeCommit when updated;
+    oracle/quorum_oracle.c appresp_range) on a bounded sample of the same
+    stream: 1M groups, 8 consecutive 1M-record batches per pass, on 1 thread
+    and on N = all host cores (groups partitioned over the threads, the batch
+    stably partitioned by owning thread — exactly the sequential result)."""
+    from tests import oracle_c as oc
+    info = host_cpu_info()
+    N = info["affinity_cpus"]
+    Gs, R, n = 1 << 20, 8, 5
+    rng = np.random.default_rng(5)
+    if csr:
+        off, m0, cfg, _ = oc.gen_csr(CSR_SEED["ragged"], "ragged", Gs)
+        sizes = np.diff(off.astype(np.int64))
+        last = m0[off[:-1]].copy()            # slot 0 holds the leader's own match
+        ts0 = last - np.uint64(64)
+    else:
+        m0, _, _, ts0 = oc.gen_fixed(TRACKER_SEED, n, Gs)
+        last = m0[0].copy()
+    batches = []
+    for k in range(R):
+        grp = rng.integers(0, Gs, size=Gs).astype(np.uint32)
+        if csr:
+            slot = (1 + (rng.integers(0, 1 << 30, size=Gs) % (sizes[grp] - 1))).astype(np.uint8)
+        else:
+            slot = rng.integers(1, n, size=Gs).astype(np.uint8)
+        lag = rng.integers(0, 96, size=Gs).astype(np.uint64)
+        idx = last[grp] + np.uint64((k + 1) * TRACKER_E) - lag
+        trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
+        batches.append((grp, slot, idx, trm))
+    m_start = m0.copy()
+    if csr:
+        m_start[off[:-1]] = last + np.uint64(R * TRACKER_E)
+    else:
+        m_start[0] = last + np.uint64(R * TRACKER_E)
+
+    def fresh():
+        st = {"match": m_start.copy(), "active": np.zeros(Gs, np.uint16),
+              "term": np.full(Gs, 7, np.uint64), "term_start": ts0.copy(),
+              "committed": np.zeros(Gs, np.uint64), "stepped_down": np.zeros(Gs, np.uint8)}
+        if csr:
+            oc.csr_commit_all(off, cfg, st["match"], ts0, st["committed"])
+        else:
+            oc.commit_all(n, st["match"], ts0, st["committed"])
+        return st
+
+    def rate(th, budget):
+        busy, passes = 0.0, 0
+        while busy < budget:
+            st = fresh()
+            t = time.perf_counter()
+            for b in batches:
+                if csr:
+                    oc.csr_appresp_sequential(off, cfg, b, st, threads=th)
+                else:
+                    oc.appresp_sequential(n, Gs, b, st, threads=th)
+            busy += time.perf_counter() - t
+            passes += 1
+        return passes * R * Gs / busy, passes
+
+    rn, pn = rate(N, seconds / 2)
+    r1, p1 = rate(1, seconds / 2)
+    return {"value": rn, "unit": "group-steps/s", "cores": N, "kind": "port", "threads": N,
+            "gomaxprocs_equivalent": N, "host": info,
+            "legs": {f"sequential_{N}t": rn, "sequential_1t": r1},
+            "sample": (f"{Gs} {'ragged CSR' if csr else '5-voter'} groups x {R} consecutive "
+                       f"{Gs}-record batches of the same stream per pass, {pn} passes on {N} "
+                       f"threads (all cores of the process's affinity, GOMAXPROCS-equivalent {N}; "
+                       f"groups partitioned, records stably partitioned by owner); 1 thread: "
+                       f"{r1:.4g} group-steps/s over {p1} passes; sequential C restatement of "
+                       f"stepLeader's MsgAppResp path (oracle/quorum_oracle.c)"),
+            "value_1thread": r1}
+
+
+def tracker_parity(tr, csr, snap_host, batches, Gs, threads):
+    """The final device state of the first Gs groups against the oracle's
+    sequential replay of every batch the bench applied since the last
+    restore (the nb batches in order), restricted to those groups."""
+    from tests import oracle_c as oc
+    off, cfg, st = snap_host
+    for b in batches:
+        rec = host_records(b, Gs)
+        if csr:
+            oc.csr_appresp_sequential(off, cfg, rec, st, threads=threads)
+        else:
+            oc.appresp_sequential(5, len(st["committed"]), rec, st, threads=threads)
+    return tracker_state_mismatches(tr, csr, st, Gs)
+
+
+def tracker_main(args, world, rank, dev, barrier):
+    csr = args.workload == "tracker-csr"
+    G = args.groups if args.groups != 1 << 20 else 1 << 24
+    K = args.steps if args.steps != 1000 else 20
+    W = args.warmup if args.warmup is not None else 4
+    nb = W + K
+    if nb > TRACKER_MAX_BATCHES:
+        raise SystemExit(f"--workload {args.workload} keeps one distinct batch per step resident: "
+                         f"--steps + --warmup must be <= {TRACKER_MAX_BATCHES}")
+    tr, batches, info = tracker_setup(G, nb, rank, dev, csr)
+    gen = info["gen"]
+    snap = {k: getattr(tr, k).clone() for k in TRACKER_STATE}
+    Gs = min(G, args.parity_groups)
+    snap_host = tracker_host_state(tr, csr, Gs) if not args.no_parity else None
 
     def restore():
-        for k in names:
+        for k in TRACKER_STATE:
             getattr(tr, k).copy_(snap[k])
 
     pipe = args.pipeline and not csr
@@ -332,6 +543,8 @@ def tracker_main(args, world, rank, dev):
 
     def step(b):
         if not pipe:
+            # the Go caller's protocol: stepdown_at stays armed (the stream has
+            # no higher-term record), no per-group re-arm write per tick
             tr.step(b, reset_stats=False, rearm=False)
             return
         j = nstep[0] & 1
@@ -342,11 +555,6 @@ def tracker_main(args, world, rank, dev):
         main.wait_event(ev_b[j])
         tr.apply_bucketed(b, wss[j])
         ev_a[j].record(main)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
 
     # pre-roll: whole passes over the batches, state restored before each
     preroll_steps, tp = 0, time.perf_counter()
@@ -362,51 +570,55 @@ def tracker_main(args, world, rank, dev):
         step(batches[k])
     tr.stats.zero_()
     st = torch.cuda.current_stream(dev)
-    ev = HipEvents(2)
-    barrier()
-    ev.record(ev.ev[0], st.cuda_stream)
-    if pipe:  # the side stream's first bucketing starts inside the region
-        for e in ev_a:
-            e.record(main)
-    t0 = time.perf_counter()
-    for k in range(W, nb):
-        step(batches[k])
-    ev.record(ev.ev[1], st.cuda_stream)
-    ev.synchronize(1)
-    t1 = time.perf_counter()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = t1 - t0
-    step_s = ev.elapsed_ms(0, 1) / 1e3 / K
-    ev.close()
+
+    def region():
+        if pipe:  # the side stream's first bucketing starts inside the region
+            for e in ev_a:
+                e.record(main)
+        for k in range(W, nb):
+            step(batches[k])
+    elapsed, step_s = timed_region(region, [st], K, barrier)
     stats = tr.stats_dict()
-    route_ms = None
+    parity = None
+    if snap_host is not None:
+        bad = tracker_parity(tr, csr, snap_host, batches, Gs, host_cpu_info()["affinity_cpus"])
+        parity = (f"bit-exact {Gs}/{Gs} groups (first {Gs} of the shard: match, committed, active, "
+                  f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
+                  else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
+    route_ms = route_impl = None
     if world > 1:
         t = torch.tensor([elapsed, step_s], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_s = (float(x) for x in t.tolist())
         # records arriving at arbitrary ranks: deliver one batch (G records per
-        # rank, global group numbers over all shards) to the owning ranks
-        # (etcd_amd.shard.route_records: RCCL all-to-all), timed apart
+        # rank, global group numbers over all shards) to the owning ranks,
+        # timed apart — the C ABI's RCCL routing (qb_dev_route_records) on
+        # nccl, torch's all-to-all on a gloo rehearsal
         b = batches[0]
         gl = torch.randint(0, world * G, (G,), generator=gen, device=dev, dtype=torch.int64)
         cols = {"group": gl.to(torch.int32), "flags": b.flags, "index": b.index, "term": b.term}
+        route, route_impl = _router(args, dev)
         for _ in range(2):
-            route_records(cols, world * G)
+            got = route(cols, world * G)
         barrier()
         tr_ = time.perf_counter()
         for _ in range(5):
-            route_records(cols, world * G)
+            got = route(cols, world * G)
         barrier()
         route_ms = (time.perf_counter() - tr_) / 5 * 1e3
+        n_in = torch.tensor([got["group"].numel()], dtype=torch.int64, device=dev)
+        dist.all_reduce(n_in)
+        if int(n_in.item()) != world * G:
+            raise SystemExit(f"routing lost records: {int(n_in.item())} of {world * G}")
+    parity = _agree(parity, world, dev)
     if rank != 0:
-        return
+        return parity
     bpg = TRACKER_BYTES
     if csr:
         # record 21 + match RMW 16 + commit advance: off 4, cfg 4, the voters'
         # match 8 each (learners ack but do not count), term_start 8,
         # committed 8 read + 8 written
-        bpg = 21 + 16 + 4 + 4 + 8 * voters_mean + 8 + 8 + 8
+        bpg = 21 + 16 + 4 + 4 + 8 * info["voters_mean"] + 8 + 8 + 8
     key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
     achieved = bpg * G / step_s / 1e9
     kern = ("k_bk_hist, k_scan_local, k_bk_sums_parts, k_bk_scatter, k_bk_split, "
@@ -416,7 +628,8 @@ def tracker_main(args, world, rank, dev):
         "metric": METRIC + " — configs[4] streaming tracker: group-steps/s",
         "value": world * G * K / elapsed,
         "unit": "group-steps/s",
-        "n_gpus": world, "steps": K, "warmup": W, "ms_per_step": elapsed / K * 1e3,
+        "n_gpus": world, "rccl_ranks": _rccl_ranks(args, world), "steps": K, "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic streaming MsgAppResp batches (torch RNG on device, seeded per rank); "
                 "leader state from the counter-based splitmix64 spec; HBM-resident",
@@ -425,8 +638,8 @@ def tracker_main(args, world, rank, dev):
                                 + (" — ragged CSR groups (3-9 voters + 0-2 learners)" if csr
                                    else ", 5 voters")),
                    "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
-                   "stale_term_fraction": 0.01, "mean_slots": slots_mean,
-                   "mean_voters": voters_mean,
+                   "stale_term_fraction": 0.01, "mean_slots": info["slots_mean"],
+                   "mean_voters": info["voters_mean"],
                    "pipelined_ticks": bool(pipe),
                    "parallelism": f"groups sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -439,68 +652,85 @@ def tracker_main(args, world, rank, dev):
                                + ("; pipelined: tick k+1's bucketing (qb_dev_fixed_tracker_bucket) "
                                   "on a second stream while tick k is applied "
                                   "(qb_dev_fixed_tracker_apply), two workspaces" if pipe else "")},
+        "parity": parity,
         "preroll_ms": preroll_ms, "preroll_steps": preroll_steps,
         "last_region_stats": {k: int(v) for k, v in stats.items()},
-        "route_ms": route_ms,
+        "route_ms": route_ms, "route_impl": route_impl,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
     print(json.dumps(out), flush=True)
+    return parity
 
 
+# ------------------------------------------------------ multi-GPU helpers ---
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed warm-up steps (default 2000 x ~9 us for configs[1], 300 x "
-                         "~0.2 ms for the CSR workloads: ~20-60 ms of work lets the clocks "
-                         "settle; 20 warm-up steps measured 2-3 %% slow)")
-    ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
-    ap.add_argument("--voters", type=int, default=5)
-    ap.add_argument("--settle-ms", type=float, default=2000.0,
-                    help="configs[1]-[3]: at most this long, untimed 64-step probes before the "
-                         "timed region until one runs within 10 %% of the pre-roll's fastest")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="tracker workload: 1 = overlap tick k+1's bucketing with tick k's apply "
-                         "on two streams (bucket / apply entry points; measured 5 %% slower: "
-                         "the concurrent kernels contend); 0 = one qb_dev_fixed_tracker_step "
-                         "per tick (default)")
-    ap.add_argument("--workload", default="fixed",
-                    choices=["fixed", "ragged", "joint", "tracker", "tracker-csr"],
-                    help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]; "
-                         "tracker = configs[4] (streaming MsgAppResp step, FIXED 5 voters); "
-                         "tracker-csr = the same stream over ragged CSR groups")
-    ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
-    ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps rotate over")
-    ap.add_argument("--cpu-seconds", type=float, default=3.0)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
-    ap.add_argument("--preroll-ms", type=float, default=300.0,
-                    help="untimed clock-settle pre-roll before the warm-up steps (wall ms)")
-    ap.add_argument("--graph", type=int, default=0,
-                    help="launch the steps from a captured HIP graph of this many steps "
-                         "(0 = direct launches); the remainder of K is launched directly")
-    args = ap.parse_args()
+_COMM = []
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:  # rehearsal of the N > 1 path on fewer GPUs
-            dist.init_process_group(args.backend)
 
-    if args.workload.startswith("tracker"):
-        tracker_main(args, world, rank, dev)
-        if world > 1:
-            dist.destroy_process_group()
-        return
+def _comm(dev):
+    """The C ABI's RCCL communicator (created once, after the timed region)."""
+    if not _COMM:
+        from etcd_amd.comm import RcclComm
+        _COMM.append(RcclComm.from_process_group(dev))
+    return _COMM[0]
+
+
+def _rccl_ranks(args, world):
+    return _COMM[0].world if _COMM else (world if args.backend == "nccl" and world > 1 else 0)
+
+
+def _router(args, dev):
+    if args.backend == "nccl":
+        c = _comm(dev)
+        return (lambda cols, total: c.route_records(cols, total)), "qb_dev_route_records (RCCL C ABI)"
+    from etcd_amd.shard import route_records
+    return route_records, f"etcd_amd.shard.route_records (torch {args.backend}, rehearsal)"
+
+
+def _gather(args, dev):
+    if args.backend == "nccl":
+        c = _comm(dev)
+        return (lambda cm, v, total: c.allgather_results(cm, v, total),
+                "qb_dev_allgather_results (RCCL C ABI)")
+    from etcd_amd.shard import allgather_results
+    return allgather_results, f"etcd_amd.shard.allgather_results (torch {args.backend}, rehearsal)"
+
+
+def _agree(parity, world, dev):
+    """Every rank's parity verdict (a mismatch anywhere is reported)."""
+    if world == 1 or parity is None:
+        return parity
+    ok = torch.tensor([0 if "MISMATCH" in parity else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if "MISMATCH" in parity:
+        return parity
+    if int(ok.item()) == 0:
+        return "MISMATCH on another rank"
+    return parity + f" (every one of the {world} ranks)"
+
+
+# ------------------------------------------------------- evaluation path ---
+
+def eval_inputs_host(workload, n, G, g_begin):
+    from tests import oracle_c as oc
+    if workload == "fixed":
+        match, vd, gr, _ = oc.gen_fixed(SEED, n, G, g_begin)
+        return ("fixed", match, vd, gr)
+    off, m, cfg, votes = oc.gen_csr(CSR_SEED[workload], workload, G, g_begin)
+    return ("csr", off, m, cfg, votes)
+
+
+def eval_oracle(inp, threads):
+    from tests import oracle_c as oc
+    if inp[0] == "fixed":
+        _, match, vd, gr = inp
+        return oc.fixed_eval(match.shape[0], match, vd, gr, threads=threads)
+    _, off, m, cfg, votes = inp
+    return oc.csr_eval(off, m, cfg, votes, threads=threads)
+
+
+def eval_main(args, world, rank, dev, barrier):
     csr = args.workload != "fixed"
     if args.warmup is None:
         args.warmup = 300 if csr else 2000
@@ -520,9 +750,8 @@ def main():
     # B resident batches; global group numbers shard by rank (weak scaling)
     if csr:
         fn = lib.qb_dev_csr_committed_vote
-        seed = {"ragged": 0x5EED0003, "joint": 0x5EED0004}[args.workload]
-        groups = [batch.CsrGroups.synth(seed, args.workload, G, g_begin=(rank * B + b) * G,
-                                        device=dev) for b in range(B)]
+        groups = [batch.CsrGroups.synth(CSR_SEED[args.workload], args.workload, G,
+                                        g_begin=(rank * B + b) * G, device=dev) for b in range(B)]
         slots = sum(int(g.off[-1].item()) for g in groups) / B
     else:
         fn = lib.qb_dev_fixed_committed_vote
@@ -540,6 +769,7 @@ def main():
                        c.data_ptr(), v.data_ptr(), st.cuda_stream)
                       for g, (c, v) in zip(groups, outs)] for st in streams]
     torch.cuda.synchronize()
+    fname = "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote"
 
     def run_steps(count, fixed_batch=None, fork=True):
         # fork=False: the caller has synchronised the device, so the launch
@@ -553,7 +783,7 @@ def main():
             b = k % B if fixed_batch is None else fixed_batch
             rc = fn(*call_args[k % S][b])
             if rc:
-                _lib.check(rc, "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote")
+                _lib.check(rc, fname)
         if fork:
             for st in streams:
                 main_stream.wait_stream(st)
@@ -586,11 +816,6 @@ def main():
             if count % L:
                 eager_steps(count % L)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     # Clock-settle pre-roll: untimed steps of the same workload until at least
     # --preroll-ms of wall time has passed, whatever --warmup is (a 5-step
     # warm-up leaves the clocks ramping: the round-1 driver line measured
@@ -622,63 +847,65 @@ def main():
             settle_ratio = (time.perf_counter() - tc) / best64
             if settle_ratio <= 1.10:
                 break
-    # Timed region: K steps between barrier + synchronize.  Device time = from
-    # the earliest start event to the latest end event, one event pair per
-    # launch stream (no cross-stream hop inside the region: a fork + join
-    # around a 20-step region cost ~30 us of device time).  The start events
-    # are recorded after the barrier (device idle, so they stamp at once) and
-    # before t0; the wall clock stops when the host sees every stream's end
-    # event complete (hipEventSynchronize: all K steps are done), then the
-    # device-wide synchronize runs (tools/lab/sync_overhead.py: a
-    # torch.cuda.synchronize() costs ~20 us more than the event waits, a fixed
-    # cost that is 10 % of a 20-step region).
     # (graph replays run on the main stream, forked inside the graph)
     tstreams = [main_stream] if graph is not None else streams
-    TS = len(tstreams)
-    ev = HipEvents(2 * TS)
-    barrier()
-    for s_, st in enumerate(tstreams):
-        ev.record(ev.ev[s_], st.cuda_stream)
-    t0 = time.perf_counter()
-    run_steps(K, fork=graph is not None)
-    for s_, st in enumerate(tstreams):
-        ev.record(ev.ev[TS + s_], st.cuda_stream)
-    for s_ in range(TS):
-        ev.synchronize(TS + s_)
-    t1 = time.perf_counter()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = t1 - t0
-    starts = [0.0] + [ev.elapsed_ms(0, s_) for s_ in range(1, TS)]
-    ends = [ev.elapsed_ms(0, TS + s_) for s_ in range(TS)]
-    avg_kernel_s = (max(ends) - min(starts)) / 1e3 / K
+    elapsed, avg_kernel_s = timed_region(lambda: run_steps(K, fork=graph is not None), tstreams, K,
+                                         barrier)
 
-    # MALL-warm single-batch rate (informational)
+    # MALL-warm single-batch rate (informational): one batch (51 MB at
+    # configs[1], inside the 256 MB MALL) re-read K times, timed exactly as
+    # the region above (events on the launch streams, no fork/join)
     run_steps(W, fixed_batch=0)
     torch.cuda.synchronize()
-    tw = time.perf_counter()
-    run_steps(K, fixed_batch=0)
-    torch.cuda.synchronize()
-    warm_elapsed = time.perf_counter() - tw
-    ev.close()
+    warm_elapsed, warm_kernel_s = timed_region(lambda: run_steps(K, fixed_batch=0, fork=False),
+                                               streams, K, barrier)
 
-    allgather_ms = None
+    # parity: every resident batch's outputs (the last values written by the
+    # timed steps; the MALL-warm pass rewrote batch 0 with the same result)
+    # against the oracle on the same counter-based inputs
+    parity = None
+    threads = host_cpu_info()["affinity_cpus"]
+    if not args.no_parity:
+        torch.cuda.synchronize()
+        bad = 0
+        for b in range(B):
+            ec, ev_ = eval_oracle(eval_inputs_host(args.workload, n, G, (rank * B + b) * G), threads)
+            c, v = outs[b]
+            bad += int(not (np.array_equal(batch.as_u64(c), ec)
+                            and np.array_equal(v.cpu().numpy(), ev_)))
+        parity = (f"bit-exact {B}/{B} resident batches ({B * G} groups: CommittedIndex + "
+                  f"VoteResult vs oracle/quorum_oracle.c)" if bad == 0
+                  else f"MISMATCH in {bad}/{B} batches")
+
+    allgather_ms = gather_impl = None
     if world > 1:
-        t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s], dtype=torch.float64,
+                         device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, warm_elapsed, avg_kernel_s = (float(x) for x in t.tolist())
+        elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s = (float(x) for x in t.tolist())
         # node-wide result: all-gather one batch's commit (u64) and vote (u8)
-        # vectors over RCCL (etcd_amd.shard)
+        # vectors
+        gather, gather_impl = _gather(args, dev)
         c, v = outs[0]
         for _ in range(3):
-            allgather_results(c, v, world * G)
+            gc, gv = gather(c, v, world * G)
         barrier()
         ta = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            allgather_results(c, v, world * G)
+            gc, gv = gather(c, v, world * G)
         barrier()
         allgather_ms = (time.perf_counter() - ta) / reps * 1e3
+        if rank == 0 and not args.no_parity:
+            # the node-wide vector against the oracle over every rank's batch 0
+            ok = True
+            for r in range(world):
+                ec, ev_ = eval_oracle(eval_inputs_host(args.workload, n, G, (r * B) * G), threads)
+                ok &= np.array_equal(batch.as_u64(gc[r * G:(r + 1) * G]), ec)
+                ok &= np.array_equal(gv[r * G:(r + 1) * G].cpu().numpy(), ev_)
+            parity = (parity or "") + ("; node-wide all-gather bit-exact" if ok
+                                       else "; MISMATCH in the node-wide all-gather")
+    parity = _agree(parity, world, dev)
 
     if rank == 0:
         total_groups = world * G * K
@@ -706,12 +933,12 @@ def main():
         cfg.update({"batches_resident": B, "streams": S, "graph_steps": args.graph,
                     "parallelism": f"groups sharded by id over {world} GPU(s)"})
         achieved = bpg * G / avg_kernel_s / 1e9
-        traffic = load_traffic(key)
         out = {
             "metric": METRIC,
             "value": value,
             "unit": "groups/s",
             "n_gpus": world,
+            "rccl_ranks": _rccl_ranks(args, world),
             "steps": K,
             "warmup": W,
             "ms_per_step": elapsed / K * 1e3,
@@ -724,33 +951,114 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
+                "traffic": load_traffic(key),
                 "kernel": kname,
                 "bytes_per_group": bpg,
                 "avg_kernel_us": avg_kernel_s * 1e6,
                 "timing": (f"HIP events at the start and end of the timed region on each of the "
-                           f"{S} launch stream(s); per-launch duration = (latest end - earliest "
-                           f"start) / K, consecutive launches overlapping across the streams; "
-                           f"wall clock from after the barrier to the host seeing every end "
-                           f"event complete"
+                           f"{len(tstreams)} launch stream(s); per-launch duration = (latest end - "
+                           f"earliest start) / K, consecutive launches overlapping across the "
+                           f"streams; wall clock from after the barrier to the host seeing every "
+                           f"end event complete"
                            + (f", launched from a HIP graph of {args.graph} steps"
                               if args.graph else "")),
             },
+            "parity": parity,
             "preroll_ms": preroll_ms,
             "preroll_steps": preroll_steps,
             "settle_probes": settle_probes,
             "settle_last_ratio": settle_ratio,
             "value_mall_warm": world * G * K / warm_elapsed,
+            "mall_warm_kernel_us": warm_kernel_s * 1e6,
             "allgather_ms": allgather_ms,
+            "allgather_impl": gather_impl,
         }
-        if world == 1 and not args.no_cpu_baseline and not csr:
-            out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample, args.cpu_seconds)
-        elif world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_csr(args.workload, args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_eval(args.workload, n, args.cpu_seconds)
         print(json.dumps(out), flush=True)
+    return parity
 
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a launcher, > 1 spawns them")
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warm-up steps (default 2000 x ~9 us for configs[1], 300 x "
+                         "~0.2 ms for the CSR workloads: ~20-60 ms of work lets the clocks "
+                         "settle; 20 warm-up steps measured 2-3 %% slow)")
+    ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU per step")
+    ap.add_argument("--voters", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=2000.0,
+                    help="configs[1]-[3]: at most this long, untimed 64-step probes before the "
+                         "timed region until one runs within 10 %% of the pre-roll's fastest")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="tracker workload: 1 = overlap tick k+1's bucketing with tick k's apply "
+                         "on two streams (bucket / apply entry points; measured 5 %% slower: "
+                         "the concurrent kernels contend); 0 = one qb_dev_fixed_tracker_step "
+                         "per tick (default)")
+    ap.add_argument("--workload", default="fixed",
+                    choices=["fixed", "ragged", "joint", "tracker", "tracker-csr"],
+                    help="fixed = configs[1] (default); ragged = configs[2]; joint = configs[3]; "
+                         "tracker = configs[4] (streaming MsgAppResp step, FIXED 5 voters); "
+                         "tracker-csr = the same stream over ragged CSR groups")
+    ap.add_argument("--batches", type=int, default=16, help="distinct HBM-resident batches")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps rotate over")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline budget (split over its legs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the post-region oracle check")
+    ap.add_argument("--parity-groups", type=int, default=1 << 20,
+                    help="tracker workloads: groups of the shard checked against the oracle")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--preroll-ms", type=float, default=300.0,
+                    help="untimed clock-settle pre-roll before the warm-up steps (wall ms)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="launch the steps from a captured HIP graph of this many steps "
+                         "(0 = direct launches); the remainder of K is launched directly")
+    ap.add_argument("--lab-lib", default=None,
+                    help="A/B lab runs: bind this build of libquorumbatch.so instead of the "
+                         "in-tree one (etcd_amd._lib.use_lab_library)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    world, rank, local, spawn = resolve_world(args.gpus, os.environ)
+    if spawn:  # no GPU call has happened in this process
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
+    if args.launch_check:  # launcher wiring self-test (tests/test_bench_launcher.py)
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:"
+                                    f"{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
+    if args.lab_lib:
+        _lib.use_lab_library(args.lab_lib)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # rehearsal of the N > 1 path on fewer GPUs
+            dist.init_process_group(args.backend)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if args.workload.startswith("tracker"):
+        parity = tracker_main(args, world, rank, dev, barrier)
+    else:
+        parity = eval_main(args, world, rank, dev, barrier)
+    for c in _COMM:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and "MISMATCH" in parity:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

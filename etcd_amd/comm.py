@@ -1,0 +1,105 @@
+"""The node-wide collectives through the C ABI's RCCL communicator — the
+calls a Go embedder binds (include/quorum_batch.h: qb_comm_init,
+qb_dev_allgather_results, qb_dev_route_records), not torch's collectives.
+
+SURVEY.md §8e: groups shard by id over the GPUs of one node; RCCL over xGMI
+is used only to all-gather the per-shard commit/vote vectors into the
+node-wide result, and to deliver record batches that arrive at any rank to
+the rank owning their group.  The communicator's unique id travels over the
+embedder's own channel; here that channel is torch.distributed's default
+process group (one broadcast of 128 bytes at construction).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from etcd_amd import _lib
+
+QB_COMM_ID_BYTES = 128
+_ROUTE_COLS = ("group", "flags", "index", "term", "hint", "log_term")
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class RcclComm:
+    """One rank's qb_comm (RCCL communicator over the node's GPUs)."""
+
+    def __init__(self, world: int, rank: int, device, uid: bytes):
+        if len(uid) != QB_COMM_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        self.world, self.rank, self.device = world, rank, torch.device(device)
+        self._uid = C.create_string_buffer(uid, QB_COMM_ID_BYTES)
+        self._h = C.c_void_p()
+        _lib.call("qb_comm_init", C.byref(self._h), world, rank, self._uid)
+        self._ws = None
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(QB_COMM_ID_BYTES)
+        _lib.call("qb_comm_get_unique_id", buf)
+        return buf.raw
+
+    @classmethod
+    def from_process_group(cls, device, group: Optional[dist.ProcessGroup] = None) -> "RcclComm":
+        """Rank 0 makes the id; torch.distributed carries it to every rank."""
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls(world, rank, device, box[0])
+
+    def close(self) -> None:
+        if self._h:
+            _lib.call("qb_comm_destroy", self._h)
+            self._h = C.c_void_p()
+
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def allgather_results(self, commit: torch.Tensor, vote: torch.Tensor, total: int,
+                          commit_all: Optional[torch.Tensor] = None,
+                          vote_all: Optional[torch.Tensor] = None):
+        """Node-wide commit (u64) / vote (u8) vectors from this rank's shard
+        (qb_dev_allgather_results; shard_range order)."""
+        if commit_all is None:
+            commit_all = torch.empty(total, dtype=torch.int64, device=self.device)
+        if vote_all is None:
+            vote_all = torch.empty(total, dtype=torch.uint8, device=self.device)
+        need = _lib.fn("qb_allgather_workspace_bytes")(total, self.world)
+        ws = self._workspace(need)
+        _lib.call("qb_dev_allgather_results", self._h, total, commit.data_ptr(), vote.data_ptr(),
+                  commit_all.data_ptr(), vote_all.data_ptr(), ws.data_ptr(), ws.numel(),
+                  _stream(self.device))
+        return commit_all, vote_all
+
+    def route_records(self, cols: Dict[str, torch.Tensor], total: int,
+                      out_cap: Optional[int] = None) -> Dict[str, torch.Tensor]:
+        """This rank's records after delivery (qb_dev_route_records): every
+        rank's records for groups of this shard, group rebased to the local
+        index, in (source rank, source position) order."""
+        from etcd_amd.shard import _device_columns
+        cols = _device_columns(cols)
+        M = cols["group"].numel()
+        if out_cap is None:
+            out_cap = self.world * M
+        out = {}
+        for name, col in cols.items():
+            out[name] = torch.empty(max(out_cap, 1), dtype=col.dtype, device=self.device)
+        need = _lib.fn("qb_route_workspace_bytes")(self.world, M)
+        ws = self._workspace(need)
+        count = C.c_uint64(0)
+
+        def p(d, n):
+            t = d.get(n)
+            return t.data_ptr() if t is not None else None
+        _lib.call("qb_dev_route_records", self._h, total, M, *[p(cols, n) for n in _ROUTE_COLS],
+                  *[p(out, n) for n in _ROUTE_COLS], out_cap, C.byref(count), ws.data_ptr(),
+                  ws.numel(), _stream(self.device))
+        return {n: t[: count.value] for n, t in out.items()}

@@ -18,7 +18,11 @@ bench tooling import it.  Paths relative to the reference's raft/raftpb/:
 Every decoder returns (ok, fields) with ok False exactly where the Go
 Unmarshal returns an error.  Field numbers are int32(key >> 3) as in Go.
 
-Pinning: the encoder is cross-checked against Google's protobuf runtime (an
+Pinning: SCHEMAS (field numbers, wire types, embedded kinds) equals the
+schema decoded from the reference's own FileDescriptorProto bytes
+(raft.pb.go:698, descriptor_fields below; tests/golden/raftpb_schema.json),
+which also exercises the decoder's nested-message path on reference bytes.
+The encoder is cross-checked against Google's protobuf runtime (an
 independent implementation of the same wire format, on a dynamically built
 descriptor of raft.proto:68-86) in tests/test_wire_oracle.py, and the decoder
 against the encoder and against hand-built malformed inputs for every error
@@ -127,14 +131,16 @@ SCHEMAS = {
 }
 
 
-def unmarshal(kind: str, b: bytes, i: int = 0, l: int = None) -> dict:
+def unmarshal(kind: str, b: bytes, i: int = 0, l: int = None, schemas: dict = None) -> dict:
     """Generic restatement of the generated Unmarshal methods above on
     dAtA[i:l]; raises WireError where Go returns an error.  Returns the last
     value of every varint field, bytes fields, and counts of nested/repeated
-    elements."""
+    elements.  ``schemas`` (default SCHEMAS) names the message kinds."""
     if l is None:
         l = len(b)
-    schema = SCHEMAS[kind]
+    if schemas is None:
+        schemas = SCHEMAS
+    schema = schemas[kind]
     out = {}
     while i < l:
         pre = i
@@ -180,9 +186,72 @@ def unmarshal(kind: str, b: bytes, i: int = 0, l: int = None) -> dict:
             if wt != 2:
                 raise WireError("wrong wiretype")
             s, post = _len_field(b, i, l)
-            sub = unmarshal(kind_f[1], b, s, post)
+            sub = unmarshal(kind_f[1], b, s, post, schemas)
             out.setdefault(fnum, []).append(sub)
             i = post
+    return out
+
+
+# --------------------------------------------- the reference's descriptor ---
+# raft.pb.go:698 holds raft.proto's FileDescriptorProto (gzipped), the one
+# protobuf blob of raftpb the reference ships.  Decoding it with the decoder
+# above (google/protobuf/descriptor.proto's schema, restated for the fields
+# read here, plus gogoproto's (nullable) field option, gogo.proto: 65001)
+# yields the field numbers, wire types and non-nullable embedded messages of
+# the reference's own schema, against which SCHEMAS is pinned
+# (tests/golden/make_raftpb_schema.py, tests/test_wire_oracle.py).
+DESCRIPTOR_SCHEMAS = {
+    "FileDescriptorProto": {1: "b", 2: "b", 4: ("m", "DescriptorProto")},
+    "DescriptorProto": {1: "b", 2: ("m", "FieldDescriptorProto"),
+                        3: ("m", "DescriptorProto")},
+    "FieldDescriptorProto": {1: "b", 3: "v", 4: "v", 5: "v", 6: "b",
+                             8: ("m", "FieldOptions")},
+    "FieldOptions": {2: "v", 65001: "v"},
+}
+# FieldDescriptorProto.Type (descriptor.proto) -> wire type
+_TYPE_WIRE = {1: 1, 2: 5, 3: 0, 4: 0, 5: 0, 6: 1, 7: 5, 8: 0, 9: 2, 11: 2, 12: 2, 13: 0, 14: 0,
+              15: 5, 16: 1, 17: 0, 18: 0}
+LABEL_REPEATED = 3
+TYPE_MESSAGE = 11
+
+
+def descriptor_fields(fdp: bytes) -> dict:
+    """{message: {field number: {"name", "type", "label", "wire", "type_name",
+    "nullable"}}} of a FileDescriptorProto, decoded with unmarshal()."""
+    f = unmarshal("FileDescriptorProto", fdp, schemas=DESCRIPTOR_SCHEMAS)
+    out = {}
+    for m in f.get(4, []):
+        fields = {}
+        for fd in m.get(2, []):
+            opts = (fd.get(8) or [{}])[-1]
+            fields[int(fd[3])] = {
+                "name": fd[1].decode(), "type": int(fd[5]), "label": int(fd[4]),
+                "wire": _TYPE_WIRE[int(fd[5])], "type_name": fd.get(6, b"").decode(),
+                "nullable": bool(opts.get(65001, 1)), "packed": bool(opts.get(2, 0))}
+        out[m[1].decode()] = fields
+    return out
+
+
+def schema_from_descriptor(fields: dict, kinds=("Message", "Entry", "Snapshot",
+                                                "SnapshotMetadata", "ConfState")) -> dict:
+    """The SCHEMAS form of descriptor_fields() for the given messages:
+    "v" varint scalar, "b" bytes, "r" repeated varint, ("m", kind) embedded
+    message (a repeated or non-nullable embedded message decodes the same)."""
+    out = {}
+    for k in kinds:
+        sch = {}
+        for num, fd in fields[k].items():
+            if fd["type"] == TYPE_MESSAGE:
+                sch[num] = ("m", fd["type_name"].rsplit(".", 1)[-1])
+            elif fd["label"] == LABEL_REPEATED and fd["wire"] == 0:
+                sch[num] = "r"
+            elif fd["wire"] == 0:
+                sch[num] = "v"
+            elif fd["wire"] == 2:
+                sch[num] = "b"
+            else:
+                raise ValueError(f"{k}.{fd['name']}: wire type {fd['wire']} not in SCHEMAS' forms")
+        out[k] = sch
     return out
 
 

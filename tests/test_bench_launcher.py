@@ -1,0 +1,93 @@
+"""CPU tests of bench.py's multi-rank launcher and host-side helpers: the
+``--gpus N`` spawn path (environment wiring, world agreement under a
+launcher), the CPU-baseline host description, and the device-column
+normalisation of the record routing (etcd_amd/shard.py)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from etcd_amd import shard  # noqa: E402
+
+
+def test_launch_envs_wiring():
+    envs = bench.launch_envs(4, {"PATH": "/x", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, 29123)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29123"
+        assert e["PATH"] == "/x" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert bench.launch_envs(1, {}, 1)[0]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_resolve_world():
+    assert bench.resolve_world(1, {}) == (1, 0, 0, False)
+    assert bench.resolve_world(8, {}) == (8, 0, 0, True)
+    env = {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}
+    assert bench.resolve_world(2, env) == (2, 1, 1, False)
+    with pytest.raises(SystemExit, match="must agree"):
+        bench.resolve_world(8, env)          # torchrun started 2 ranks, --gpus says 8
+    with pytest.raises(SystemExit):
+        bench.resolve_world(0, {})
+
+
+def test_gpus_n_spawns_n_ranks_without_a_launcher():
+    """``python bench.py --gpus 3`` with no torchrun starts three ranks, each
+    with its own RANK / LOCAL_RANK, one WORLD_SIZE and one rendezvous."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                          "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rows = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    assert sorted(r["rank"] for r in rows) == [0, 1, 2]
+    assert sorted(r["local_rank"] for r in rows) == [0, 1, 2]
+    assert {r["world"] for r in rows} == {3}
+    assert len({r["master"] for r in rows}) == 1 and rows[0]["master"].startswith("127.0.0.1:")
+
+
+def test_gpus_mismatch_under_launcher_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8",
+                          "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "must agree" in out.stderr
+
+
+def test_host_cpu_info_fields():
+    info = bench.host_cpu_info()
+    assert info["affinity_cpus"] == len(os.sched_getaffinity(0)) >= 1
+    assert info["logical_cpus"] == os.cpu_count()
+    assert info["model"]                       # /proc/cpuinfo model name
+    assert info["physical_cores"] is None or info["physical_cores"] >= 1
+
+
+def test_route_columns_normalised_or_refused():
+    """The device routing reads raw pointers: columns are converted to the
+    layout it expects (any integer group dtype masked to uint32 bits, as the
+    host path does; strided views made contiguous) or refused by dtype."""
+    M = 10
+    g64 = torch.arange(M, dtype=torch.int64) + (1 << 32)      # high bits masked off
+    idx = torch.arange(2 * M, dtype=torch.int64)[::2]          # strided view
+    cols = shard._device_columns({"group": g64, "flags": torch.zeros(M, dtype=torch.uint8),
+                                  "index": idx, "term": torch.ones(M, dtype=torch.int64)})
+    assert cols["group"].dtype == torch.int32 and cols["group"].tolist() == list(range(M))
+    assert cols["index"].is_contiguous() and cols["index"].tolist() == list(range(0, 2 * M, 2))
+    with pytest.raises(ValueError, match="flags"):
+        shard._device_columns({"group": g64, "flags": torch.zeros(M, dtype=torch.int32),
+                               "index": idx, "term": idx})
+    with pytest.raises(ValueError, match="term"):
+        shard._device_columns({"group": g64, "flags": torch.zeros(M, dtype=torch.uint8),
+                               "index": idx, "term": idx.to(torch.int32)})
+    with pytest.raises(ValueError, match="length"):
+        shard._device_columns({"group": g64, "flags": torch.zeros(M + 1, dtype=torch.uint8),
+                               "index": idx, "term": idx})
+    with pytest.raises(ValueError, match="required"):
+        shard._device_columns({"group": g64, "flags": torch.zeros(M, dtype=torch.uint8)})

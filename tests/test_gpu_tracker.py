@@ -300,3 +300,16 @@ def test_stepdown_entry_rule_check_and_rearm():
     tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
     assert int(tr.stepped_down().sum().item()) == 0
     tr.check_armed()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("csr", [False, True])
+def test_bench_live_stream_full_size_every_tick(csr):
+    """BASELINE configs[4] at full size, the bench's exact stream
+    (bench.tracker_setup: 16M groups, E = 64, 4 warm-up + 20 timed ticks,
+    1 % stale terms) stepped as the bench steps it, against the sequential C
+    oracle after every tick: match, committed, active, stepped_down for all
+    16M groups, and every stat counter (the 16M test checked one
+    tick without active or stats)."""
+    from tests.parity_checks import check_tracker_stream
+    check_tracker_stream(DEV, csr, 1 << 24, 24)

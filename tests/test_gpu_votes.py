@@ -14,47 +14,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-NONE = 0xFFFFFFFF
+from tests.parity_checks import NONE, sequential_votes  # noqa: E402,F401
 
 
 def _slots(mask):
     return {s for s in range(16) if (mask >> s) & 1}
-
-
-def sequential_votes(prevote, cfg, votes0, gterm, group, flags, term):
-    """The batch through one oracle Candidate per group, in batch order
-    (oracle/quorum_ref.py Candidate).  Returns (votes words, stepdown_at,
-    decided_at, stats[8]) as qb_dev_record_votes reports them."""
-    G = len(cfg)
-    cands = {}
-    sd = np.full(G, NONE, np.uint32)
-    dec = np.full(G, NONE, np.uint32)
-    stats = np.zeros(8, np.uint64)
-    for i in range(len(group)):
-        g = int(group[i])
-        if g >= G:
-            stats[q.STAT_BAD] += 1
-            continue
-        c = cands.get(g)
-        if c is None:
-            w = int(votes0[g])
-            vd, gr = w & 0xFFFF, (w >> 16) & w
-            pre = {j: bool((gr >> j) & 1) for j in range(16) if (vd >> j) & 1}
-            c = cands[g] = q.Candidate(prevote, int(gterm[g]), _slots(int(cfg[g]) & 0xFFFF),
-                                       _slots(int(cfg[g]) >> 16), pre)
-        was = c.decided
-        st = c.step(int(flags[i]) & 0x0F, bool(flags[i] & 0x80), int(term[i]))
-        stats[st] += 1
-        if st == q.STAT_HIGHER:
-            sd[g] = i
-        if c.decided and not was:
-            dec[g] = i
-    out = np.asarray(votes0, np.uint32).copy()
-    for g, c in cands.items():
-        vd = sum(1 << j for j in c.votes)
-        gr = sum(1 << j for j, v in c.votes.items() if v)
-        out[g] = vd | (gr << 16)
-    return out, sd, dec, stats
 
 
 def _run(prevote, G, M, seed, p_dup=0.3):

@@ -229,3 +229,55 @@ def test_wire_primitives_pinned_by_reference_bytes(monkeypatch):
     for cut in (len(body) - len(info), len(body) - 1):
         with pytest.raises(R.WireError):
             R.unmarshal("walpb.Record", body[:cut])
+
+
+def _fixture_schema():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "raftpb_schema.json")
+    with open(path) as f:
+        d = json.load(f)
+    return {k: {int(n): v for n, v in fs.items()} for k, fs in d["messages"].items()}
+
+
+def test_schemas_pinned_by_reference_descriptor():
+    """SCHEMAS (field numbers, wire types, embedded kinds) equals the schema
+    decoded from the reference's own FileDescriptorProto bytes
+    (raft.pb.go:698; tests/golden/raftpb_schema.json).  Message-value parity
+    stays unpinned: the reference holds no encoded raftpb.Message."""
+    from oracle import raftpb_ref as r
+    fields = _fixture_schema()
+    assert r.schema_from_descriptor(fields) == r.SCHEMAS
+
+
+def test_fast_prefix_assumptions_pinned_by_reference_descriptor():
+    """What the wire kernel's fast prefix (qb_wire.hip)
+    relies on, read from the reference's descriptor: every Message field but
+    context is non-nullable (gogoproto always writes it, in field order), as
+    are Snapshot.metadata, SnapshotMetadata.conf_state and its index / term,
+    Entry's Term / Index / Type; ConfState's repeated ids are unpacked
+    (proto2) and auto_leave is non-nullable."""
+    f = _fixture_schema()
+    msg = f["Message"]
+    assert [n for n in sorted(msg) if msg[n]["nullable"]] == [12]        # context
+    assert msg[7]["label"] == 3 and msg[9]["label"] == 1                 # entries repeated
+    assert not f["Snapshot"][2]["nullable"] and f["Snapshot"][1]["nullable"]
+    assert not any(f["SnapshotMetadata"][n]["nullable"] for n in (1, 2, 3))
+    assert not any(f["Entry"][n]["nullable"] for n in (1, 2, 3))
+    cs = f["ConfState"]
+    assert all(cs[n]["label"] == 3 and not cs[n]["packed"] for n in (1, 2, 3, 4))
+    assert not cs[5]["nullable"]
+
+
+def test_descriptor_fixture_regenerates_from_reference():
+    """Where /root/reference is present (the build container), decoding its
+    descriptor blob with the restated decoder reproduces the fixture, and
+    Google's runtime agrees field by field (make_raftpb_schema.cross_check)."""
+    import os
+    if not os.path.exists("/root/reference/raft/raftpb/raft.pb.go"):
+        pytest.skip("reference not present (GPU box)")
+    from tests.golden import make_raftpb_schema as mk
+    fdp = mk.reference_descriptor("/root/reference")
+    schema = mk.decoded_schema(fdp)
+    mk.cross_check(fdp, schema)
+    assert {k: {int(n): v for n, v in fs.items()} for k, fs in schema.items()} == _fixture_schema()
