@@ -214,7 +214,11 @@ def load_traffic(workload_key: str):
 
 def host_cpu_info() -> dict:
     """The host the CPU baseline runs on (core count, CPU model,
-    thread count)."""
+    thread count).  ``threads`` = the CPUs this process can actually run on:
+    its affinity set, capped by the cgroup's CPU quota when one is set (the
+    GPU box: 256 logical CPUs in the affinity set, a 16-CPU quota per GPU —
+    256 threads there measured 2.5x slower than 16 on the tracker leg,
+    quota throttling)."""
     info = {"logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "model": None, "physical_cores": None, "cgroup_cpu_quota": None}
     try:
@@ -245,6 +249,8 @@ def host_cpu_info() -> dict:
             info["cgroup_cpu_quota"] = float(q) / float(p)
     except (OSError, ValueError):
         pass
+    q = info["cgroup_cpu_quota"]
+    info["threads"] = max(1, min(info["affinity_cpus"], int(q))) if q else info["affinity_cpus"]
     return info
 
 
@@ -267,7 +273,7 @@ def cpu_baseline_eval(workload: str, n: int, seconds: float):
     joint.go:49-75) — the value — and the SoA one beside it."""
     from tests import oracle_c as oc
     info = host_cpu_info()
-    N = info["affinity_cpus"]
+    N = info["threads"]
     gs = 1 << 20
     if workload == "fixed":
         match, vd, gr, _ = oc.gen_fixed(SEED, n, gs)
@@ -290,7 +296,8 @@ def cpu_baseline_eval(workload: str, n: int, seconds: float):
         "threads": N, "gomaxprocs_equivalent": N, "host": info, "legs": legs,
         "sample": (f"{what} (same synthetic spec); value = faithful C restatement of the Go loop "
                    f"(Go-map configs + AckedIndexer lookups + insertionSort, majority.go:126-210, "
-                   f"joint.go:49-75) on {N} threads (all cores of the process's affinity, "
+                   f"joint.go:49-75) on {N} threads = every CPU the process may use (affinity "
+                   f"{info['affinity_cpus']} logical CPUs, cgroup quota {info['cgroup_cpu_quota']}; "
                    f"GOMAXPROCS-equivalent {N}); legs: faithful and SoA restatements at 1 and {N} "
                    f"threads"),
     }
@@ -425,7 +432,7 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
     stably partitioned by owning thread — exactly the sequential result)."""
     from tests import oracle_c as oc
     info = host_cpu_info()
-    N = info["affinity_cpus"]
+    N = info["threads"]
     Gs, R, n = 1 << 20, 8, 5
     rng = np.random.default_rng(5)
     if csr:
@@ -484,7 +491,8 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
             "legs": {f"sequential_{N}t": rn, "sequential_1t": r1},
             "sample": (f"{Gs} {'ragged CSR' if csr else '5-voter'} groups x {R} consecutive "
                        f"{Gs}-record batches of the same stream per pass, {pn} passes on {N} "
-                       f"threads (all cores of the process's affinity, GOMAXPROCS-equivalent {N}; "
+                       f"threads (every CPU the process may use: affinity {info['affinity_cpus']}, "
+                       f"cgroup quota {info['cgroup_cpu_quota']}; GOMAXPROCS-equivalent {N}; "
                        f"groups partitioned, records stably partitioned by owner); 1 thread: "
                        f"{r1:.4g} group-steps/s over {p1} passes; sequential C restatement of "
                        f"stepLeader's MsgAppResp path (oracle/quorum_oracle.c)"),
@@ -581,7 +589,7 @@ def tracker_main(args, world, rank, dev, barrier):
     stats = tr.stats_dict()
     parity = None
     if snap_host is not None:
-        bad = tracker_parity(tr, csr, snap_host, batches, Gs, host_cpu_info()["affinity_cpus"])
+        bad = tracker_parity(tr, csr, snap_host, batches, Gs, host_cpu_info()["threads"])
         parity = (f"bit-exact {Gs}/{Gs} groups (first {Gs} of the shard: match, committed, active, "
                   f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
                   else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
@@ -864,7 +872,7 @@ def eval_main(args, world, rank, dev, barrier):
     # timed steps; the MALL-warm pass rewrote batch 0 with the same result)
     # against the oracle on the same counter-based inputs
     parity = None
-    threads = host_cpu_info()["affinity_cpus"]
+    threads = host_cpu_info()["threads"]
     if not args.no_parity:
         torch.cuda.synchronize()
         bad = 0

@@ -17,27 +17,65 @@ constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
 using scan::kScanPer;
 constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
 
-// Bucketed record payload, structure of arrays (three u64 columns of M), so
-// every scatter store is one contiguous wave-wide write:
-//   index, term, and mr = meta | ridx << 32 with
+// Bucketed record payload, structure of arrays, so every scatter store is
+// one contiguous wave-wide write.  Two forms:
+//
+// Wide (the leader step): three u64 columns of M — index, term, and
+//   mr = meta | ridx << 32 with
 //   meta = lg (bits 0-9) | chunk-low (10-16) | record flags byte (17-24:
 //          slot 17-20, kind 21-22, no-progress 23, reject 24),
 //   ridx = batch index of the record (step-down ordering).
-// term32 (optional, in the term column's space): the term as u32, or
-// kTermEscape when it does not fit, in which case the consumer reads the
-// full term from the original batch by ridx (the leader step).  The tracker
-// step uses the packed form (two columns): index, and mr = meta | term32 << 32.
+//   term32 (optional, in the term column's space): the term as u32, or
+//   kTermEscape when it does not fit, in which case the consumer reads the
+//   full term from the original batch by ridx.
+//
+// Compact (the tracker steps, Cols::compact): ONE u64 per record through
+// both levels — what K5 needs and nothing else — plus a u8 chunk-low column
+// between the levels (K4's sort key; K5 knows its chunk):
+//   bits [0, lgb)            lg, the group within its chunk (lgb = log2 CH)
+//   [lgb, lgb + slb)         slot (slb = 3 when the slot bound n <= 8, else 4)
+//   bit lgb + slb            reject
+//   [lgb + slb + 1, 24)      term (tb = 23 - lgb - slb bits: 10 or 11)
+//   [24, 64)                 index (40 bits)
+// A record whose index >= 2^40 or whose term does not fit tb bits is an
+// escape: its term field is all ones and the index field holds the record's
+// batch position, from which K5 reads the exact index and term in the
+// original batch.  Raft indexes below 2^40 and terms below 1023 keep every
+// record in 8 bytes; an escape costs K5 two 8-byte gathers, never a wrong
+// answer.  (Round 2's packed form moved index + meta|term32, 16 bytes, four
+// times per record: K3 write, K4 read + write, K5 read.)
 struct Cols {
   u64* index;
   u64* term;
   u64* mr;
   u32* term32;
-  u32 packed;  // no term column and no ridx: mr = meta | term_to32(term) << 32
+  u8* cl;        // compact: chunk-low of each record (K3 -> K4)
+  u32 compact;
 };
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
 __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
+constexpr u32 kIndexBits = 40;
+constexpr u32 kRecHdrBits = 24;  // lg | slot | reject | term
+struct RecFmt {
+  u32 lgb, slb, tb;
+  __host__ __device__ u32 rej_shift() const { return lgb + slb; }
+  __host__ __device__ u32 term_shift() const { return lgb + slb + 1; }
+  __host__ __device__ u32 tesc() const { return (1u << tb) - 1u; }
+  __device__ __forceinline__ u64 encode(u32 lg, u32 slot, bool rej, u64 index, u64 term,
+                                        u32 ridx) const {
+    const bool esc = term >= u64(tesc()) || (index >> kIndexBits) != 0;
+    const u64 hdr = u64(lg) | (u64(slot) << lgb) | (u64(rej) << rej_shift()) |
+                    (u64(esc ? tesc() : u32(term)) << term_shift());
+    return hdr | ((esc ? u64(ridx) : index) << kRecHdrBits);
+  }
+  __device__ __forceinline__ u32 lg(u64 r) const { return u32(r) & ((1u << lgb) - 1u); }
+  __device__ __forceinline__ u32 slot(u64 r) const { return (u32(r) >> lgb) & ((1u << slb) - 1u); }
+  __device__ __forceinline__ bool rej(u64 r) const { return (u32(r) >> rej_shift()) & 1u; }
+  __device__ __forceinline__ u32 term(u64 r) const { return (u32(r) >> term_shift()) & tesc(); }
+  __device__ __forceinline__ u64 payload(u64 r) const { return r >> kRecHdrBits; }
+};
 
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
 // with its own L2.  xcd_major maps blockIdx to a logical tile so that tiles
@@ -99,6 +137,7 @@ struct Geometry {
   // workgroup c, round-robin over the XCDs, so a super-bucket's 128 chunks
   // run together on one XCD while K5 still walks the state in memory order.
   u32 il;
+  RecFmt fmt;  // compact record layout (lg / slot / term bit widths)
   __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
   __host__ __device__ u32 sb_of_chunk(u32 c) const {
     return il ? (c & (kXcds - 1u)) | ((c >> 10) << 3) : c >> 7;
@@ -126,19 +165,22 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   static_assert(kChunksPerSb * 8 == 1024, "il: 8 XCDs x 128 chunks per window");
   g.NT = u32((M + kTile - 1) / kTile);
   g.xcd = g.NSB > 0 && u32(kTile) / g.NSB < 32u;
+  g.fmt.lgb = g.ch_shift;
+  g.fmt.slb = n <= 8 ? 3u : 4u;
+  g.fmt.tb = kRecHdrBits - 1u - g.fmt.lgb - g.fmt.slb;
   return g;
 }
 
 // Workspace carve (all offsets 256-byte aligned).
 struct Carve {
-  size_t shards, flags, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, total;
+  size_t shards, flags, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, cl, total;
 };
 // Upper bound on parts: every super-bucket contributes at most one partial.
 inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
-// ncols = 3: index, term and mr move with the records; ncols = 2: index and a
-// packed mr (Cols::packed); ncols = 1: only mr (callers that read the payload
-// from the original batch by ridx).
+// ncols = 3: index, term and mr move with the records; ncols = 1: only mr
+// (callers that read the payload from the original batch by ridx, and the
+// compact form, whose u8 chunk-low column rides in the carve's cl area).
 inline Carve carve(const Geometry& g, int ncols = 3) {
   Carve c{};
   size_t o = 0;
@@ -155,18 +197,21 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   // an empty chunk)
   c.buf1 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
   c.buf2 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
+  c.cl = o;  o += ncols == 1 ? up256(g.M ? g.M : 1) : 0;
   c.total = o;
   return c;
 }
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
   const size_t col = up256(sizeof(u64) * (M ? M : 1));
-  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, 0};
-  if (ncols == 2)
-    return Cols{reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u64*>(base + col), nullptr,
-                1};
+  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, nullptr, 0};
   return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
-              reinterpret_cast<u64*>(base + 2 * col), nullptr, 0};
+              reinterpret_cast<u64*>(base + 2 * col), nullptr, nullptr, 0};
+}
+// The compact form's columns: the u64 records at `base`, the chunk-low bytes
+// at `cl` (K3's output only; K4's output needs none).
+inline Cols compact_at(char* base, char* cl) {
+  return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u8*>(cl), 1};
 }
 
 
@@ -276,14 +321,15 @@ struct RunTable {
 // with n < 16 those with slot >= n into shards[QB_STAT_NON_MEMBER].
 // rec_index == rec_term == nullptr buckets the mr column alone (carve with
 // ncols = 1).  term32: the term column moves as u32 (term_to32), 4 bytes
-// per record less through both levels; read it with Cols::term32.  packed
-// (carve with ncols = 2): index + mr = meta | term_to32 << 32, no batch index.
+// per record less through both levels; read it with Cols::term32.  compact
+// (carve with ncols = 1): the 8-byte compact record (RecFmt) through both
+// levels, chunk-low in the carve's cl bytes between them.
 // K2 zeroes [cv.shards, cv.flags + 256) (stat shards and flag words) before
 // anything counts into them, so the caller needs no memset; K2's add-back is folded into its readers
 // (the hist array keeps per-4096 local scans, see off_at).
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32 = false, bool packed = false);
+                   hipStream_t st, bool term32 = false, bool compact = false);
 
 
 }  // namespace bk

@@ -128,6 +128,7 @@ struct alignas(16) TileLds {
   u16 rank[kTile];
   u16 perm[kTile];
   u64 stage[kTile];
+  u8 cl[kTile];  // compact records: chunk-low, the next level's key
   u32 wsum[kPartThreads / 64];
 };
 
@@ -256,6 +257,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   __syncthreads();
   if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
     u64 bins = 0, ranks = 0;
+    u32 cls = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       u32 b = kNoBin, r = 0;
@@ -265,9 +267,11 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
       }
       bins |= u64(b) << (16 * j);
       ranks |= u64(r & 0xFFFFu) << (16 * j);
+      cls |= geo.cl_of_chunk(geo.chunk_of(g[j])) << (8 * j);
     }
     *reinterpret_cast<u64*>(&L.bin[4u * threadIdx.x]) = bins;
     *reinterpret_cast<u64*>(&L.rank[4u * threadIdx.x]) = ranks;
+    if (out.compact) *reinterpret_cast<u32*>(&L.cl[4u * threadIdx.x]) = cls;
   } else {
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -277,6 +281,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
       if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
         b = u16(geo.sb_of(g[j]));
         L.rank[k] = u16(atomicAdd(&start[b], 1u));
+        L.cl[k] = u8(geo.cl_of_chunk(geo.chunk_of(g[j])));
       }
       L.bin[k] = b;
     }
@@ -284,10 +289,9 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
   __syncthreads();
   const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
   tile_perm(L, start, nrec);
-  // three payload columns: index, term, mr = meta | ridx << 32 (packed: index
-  // and mr = meta | term32 << 32)
-  for (int col = ri ? 0 : 2; col < 3; ++col) {
-    if (col == 1 && out.packed) continue;
+  // wide: three payload columns, index, term, mr = meta | ridx << 32;
+  // compact: one, the 8-byte record (RecFmt), plus the chunk-low bytes
+  for (int col = out.compact ? 2 : ri ? 0 : 2; col < 3; ++col) {
     u64 v[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -296,11 +300,14 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
         v[j] = vi[j];
       } else if (col == 1) {
         v[j] = vt[j];
+      } else if (out.compact) {
+        v[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j],
+                              vt[j], u32(t0 + k));
       } else {
         const u32 chunk = geo.chunk_of(g[j]);
         const u32 meta = (g[j] & (geo.CH - 1u)) | (geo.cl_of_chunk(chunk) << 10) |
                          ((f[j] & 0xFFu) << 17);
-        v[j] = u64(meta) | (u64(out.packed ? term_to32(vt[j]) : u32(t0 + k)) << 32);
+        v[j] = u64(meta) | (u64(u32(t0 + k)) << 32);
       }
     }
     if (vec) {  // two 16-byte LDS stores per lane (8-byte stores at a 32-byte stride conflict)
@@ -318,6 +325,13 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
         const u32 k = L.perm[e];
         const u32 b = L.bin[k];
         out.term32[gstart[b] + (e - start[b])] = term_to32(L.stage[k]);
+      }
+    } else if (out.compact) {
+      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+        const u32 k = L.perm[e];
+        const u32 d = gstart[L.bin[k]] + (e - start[L.bin[k]]);
+        dst[d] = L.stage[k];
+        out.cl[d] = L.cl[k];
       }
     } else {
       for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
@@ -439,16 +453,18 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
     for (int j = 0; j < kPer; ++j) {
       const u32 k = threadIdx.x + j * kPartThreads;
       vi[j] = k < nrec ? in.index[lo + k] : 0ull;
-      vt[j] = k >= nrec || in.packed ? 0ull
-              : in.term32            ? u64(in.term32[lo + k])
-                                     : in.term[lo + k];
+      vt[j] = k >= nrec     ? 0ull
+              : in.term32   ? u64(in.term32[lo + k])
+                            : in.term[lo + k];
     }
   }
   u64 vm[kPer];  // loaded together: one round trip, not one per record
+  u32 vc[kPer];  // compact: the chunk-low bytes
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
     vm[j] = k < nrec ? in.mr[lo + k] : 0ull;
+    vc[j] = k < nrec && in.compact ? u32(in.cl[lo + k]) : 0u;
   }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
@@ -456,7 +472,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   for (int j = 0; j < kPer; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
     if (k >= nrec) continue;
-    const u16 b = u16((u32(vm[j]) >> 10) & 127u);
+    const u16 b = u16(in.compact ? vc[j] : (u32(vm[j]) >> 10) & 127u);
     L.bin[k] = b;
     L.rank[k] = u16(atomicAdd(&start[b], 1u));
     L.stage[k] = vm[j];
@@ -469,7 +485,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   tile_perm(L, start, nrec);
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
   __syncthreads();
-  for (int col = in.index ? 0 : 2; col < (in.packed ? 1 : 2); ++col) {
+  for (int col = in.index ? 0 : 2; col < 2; ++col) {
     u64* dst = col == 0 ? out.index : out.term;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -489,13 +505,13 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 
 
 // ---------------------------------------------------------------- K5 ----
-// Records arrive packed (index, mr = meta | term32 << 32): no batch index.
-// A chunk whose records all compare exactly against their group's term and
-// none of which is higher (the steady state) is applied here.  A chunk with
-// a higher-term record (the sequential leader steps down there and ignores
-// what follows, raft.go:875-879: batch order matters) or with a term32 escape
-// against a group term >= 2^32 - 1 (ambiguous compare) is "slow": K5 leaves
-// its state untouched, flags it, and k_bk_slow applies it from the original
+// Records arrive compact (one u64 each, RecFmt: lg, slot, reject, term,
+// index; an escape record carries its batch position and K5 reads its exact
+// index and term from the original batch).  A chunk none of whose records is
+// above its group's term (the steady state) is applied here.  A chunk with a
+// higher-term record (the sequential leader steps down there and ignores what
+// follows, raft.go:875-879: batch order matters) is "slow": K5 leaves its
+// state untouched, flags it, and k_bk_slow applies it from the original
 // batch in batch order (the exact two-pass form of qb_tracker.hip).
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
 // act[CH] u32.
@@ -510,6 +526,7 @@ __host__ __device__ constexpr u32 k5_block(int n) {
 template <int N, bool NEXT>
 __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
+    const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
@@ -579,7 +596,8 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   u32 total = rt.finish(rq);
   __syncthreads();
   constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
-  u64 rmr[kRecPer], rix[kRecPer];
+  const RecFmt fmt = geo.fmt;
+  u64 rec[kRecPer];
   // branch-free (clamped; an empty chunk reads record 0, which exists)
   auto fetch = [&](u32 f0, u32 tot) {
     u32 ix[kRecPer];
@@ -589,10 +607,7 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
       ix[r] = tot ? rt.locate_fixed(f < tot ? f : tot - 1) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kRecPer; ++r) {
-      rmr[r] = recs.mr[ix[r]];
-      rix[r] = recs.index[ix[r]];
-    }
+    for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
   };
   auto apply = [&](u32 f0, u32 tot) {
 #pragma unroll
@@ -600,24 +615,25 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
       const u32 f = f0 + u32(r) * B + threadIdx.x;
       bool stale = false, applied = false, rejected = false;
       if (f < tot) {
-        const u64 mr = rmr[r];
-        const u32 t32 = u32(mr >> 32), meta = u32(mr);
-        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+        const u64 x = rec[r];
+        const u32 lg = fmt.lg(x), s = fmt.slot(x);
+        u64 t = fmt.term(x), idx = fmt.payload(x);
+        if (t == fmt.tesc()) {  // escape: the exact values from the batch
+          const u32 ridx = u32(idx);
+          idx = rec_index[ridx];
+          t = rec_term[ridx];
+        }
         const u64 gt = gterm[lg];
-        // t32 == kTermEscape: term >= 2^32 - 1, higher than any smaller group
-        // term and not comparable with a group term >= 2^32 - 1
-        const bool esc = t32 == kTermEscape;
-        if (esc || u64(t32) > gt) {
-          slow = 1;  // higher term (step-down order) or ambiguous compare
-        } else if (u64(t32) < gt) {
+        if (t > gt) {
+          slow = 1;  // higher term: step-down order (raft.go:875-879)
+        } else if (t < gt) {
           stale = true;                                   // raft.go:883-921
         } else {
           atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-          if (meta & (1u << 24)) {  // QB_REC_REJECT
+          if (fmt.rej(x)) {
             rejected = true;                              // raft.go:1109: not MaybeUpdate
           } else {
             applied = true;
-            const u64 idx = rix[r];
             atomicMax(&acc_m[s * CH + lg], idx);          // progress.go:146-150
             if constexpr (NEXT) atomicMax(&acc_n[s * CH + lg], idx + 1ull);  // :151
           }
@@ -631,20 +647,16 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   // The first batch (at the bench's ~512 records per chunk, all of them) in
   // straight-line code: its wait is for its own loads and the state issued
   // before them, not a conservative drain at a loop head.
-#ifdef QB_LAB_K5_NORECS
-  total = 0;
-#endif
   fetch(0, total);
-  // pinned: both columns are loaded here, not sunk into apply's branches
-  // (each a round trip of its own)
+  // pinned: the records are loaded here, not sunk into apply's branches
 #pragma unroll
-  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
   apply(0, total);
   for (u32 pb = p0, f0 = B * kRecPer;;) {
     for (; f0 < total; f0 += B * kRecPer) {
       fetch(f0, total);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
       apply(f0, total);
     }
     pb += RunTable::kRuns;
@@ -680,9 +692,7 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
       const u64 a = acc_m[s * CH + lg];
       const bool up = live && a > v[k][s];
       if (up) v[k][s] = a;
-#ifndef QB_LAB_K5_NOSTORE
       if (QB_K5_FULL >= 2 ? (__ballot(up) != 0 && live) : up) match[u64(s) * geo.G + g] = v[k][s];
-#endif
       if constexpr (NEXT) {
         if (live) {
           u64* q = next + u64(s) * geo.G + g;
@@ -694,19 +704,16 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
     const u64 ci = select_quorum<N>(v[k]);
     const bool adv = live && ci > cm[k] && ci >= ts[k];  // log.go:328-334
     const u32 na = live ? act[lg] : 0u;
-#ifndef QB_LAB_K5_NOSTORE
     if (QB_K5_FULL >= 1 ? (__ballot(adv) != 0 && live) : adv) committed[g] = adv ? ci : cm[k];
     if (advanced && live) advanced[g] = adv ? 1 : 0;
     if (QB_K5_FULL >= 1 ? (__ballot(na != 0) != 0 && live) : na != 0) active[g] = u16(av[k] | na);
-#else
-    if (ci == 0x1234567ull && av[k] == 7) committed[g] = ci;  // keeps the loads live
-#endif
   }
   const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
   tally.flush(tl, shard_of(shards), slot);
 }
 
 struct ApplyArgs {
+  const u64 *ri, *rt;  // the original batch (escape records)
   const u64 *gt, *ts;
   u64 *match, *next;
   u16* active;
@@ -723,11 +730,11 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                   const ApplyArgs& a, hipStream_t st) {
   if (a.next)
     hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
-                       cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
+                       cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
   else
     hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
-                       cs, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
+                       cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
 }
 
@@ -766,14 +773,14 @@ namespace bk {
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32, bool packed) {
+                   hipStream_t st, bool term32, bool compact) {
   u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
   u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const int ncols = !rec_index ? 1 : packed ? 2 : 3;
-  Cols buf1 = cols_at(ws + cv.buf1, geo.M, ncols);
-  Cols buf2 = cols_at(ws + cv.buf2, geo.M, ncols);
+  const int ncols = !rec_index || compact ? 1 : 3;
+  Cols buf1 = compact ? compact_at(ws + cv.buf1, ws + cv.cl) : cols_at(ws + cv.buf1, geo.M, ncols);
+  Cols buf2 = compact ? compact_at(ws + cv.buf2, nullptr) : cols_at(ws + cv.buf2, geo.M, ncols);
   if (term32 && ncols == 3) {
     buf1.term32 = reinterpret_cast<u32*>(buf1.term);
     buf2.term32 = reinterpret_cast<u32*>(buf2.term);
@@ -811,7 +818,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
 
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
-  return bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 2).total;
+  return bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 1).total;
 }
 
 namespace {
@@ -824,7 +831,7 @@ int fixed_tracker_check(uint32_t n, uint64_t G, uint64_t M, const void* workspac
   QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
   QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
   *geo = bk::geometry(n, G, M, 0, bk::kSbIl);
-  *cv = bk::carve(*geo, 2);
+  *cv = bk::carve(*geo, 1);
   QB_REQUIRE(workspace && workspace_bytes >= cv->total,
              "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv->total);
   QB_REQUIRE(geo->NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
@@ -850,7 +857,7 @@ extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
   return bk::bucket_records(geo, cv, ws, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
                             reinterpret_cast<const u64*>(rec_term),
                             reinterpret_cast<u64*>(ws + cv.shards), as_stream(stream),
-                            /*term32=*/false, /*packed=*/true);
+                            /*term32=*/false, /*compact=*/true);
 }
 
 extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
@@ -874,13 +881,15 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const bk::Cols recs = bk::cols_at(ws + cv.buf2, M, 2);
+  const bk::Cols recs = bk::compact_at(ws + cv.buf2, nullptr);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
-  const bk::ApplyArgs a{reinterpret_cast<const u64*>(group_term),
+  const bk::ApplyArgs a{reinterpret_cast<const u64*>(rec_index),
+                        reinterpret_cast<const u64*>(rec_term),
+                        reinterpret_cast<const u64*>(group_term),
                         reinterpret_cast<const u64*>(term_start),
                         reinterpret_cast<u64*>(match),
                         reinterpret_cast<u64*>(next),

@@ -55,13 +55,14 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
 // CAPW: LDS slots per group; SECOND: the launch for the deferred chunks.
 #define QB_CSR_APPLY_PARAMS                                                                      \
   Geometry geo, Cols recs, const u32 *__restrict__ pt, const u32 *__restrict__ cs,                \
+      const u64 *__restrict__ rec_index, const u64 *__restrict__ rec_term,                        \
       const u32 *__restrict__ off, const u32 *__restrict__ cfg,                                   \
       const u64 *__restrict__ group_term, const u64 *__restrict__ term_start,                     \
       u64 *__restrict__ match, u64 *__restrict__ next, u16 *__restrict__ active,                  \
       u64 *__restrict__ committed, u32 *__restrict__ stepdown_at, u8 *__restrict__ advanced,      \
       u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards
 #define QB_CSR_APPLY_ARGS                                                                      \
-  geo, recs, pt, cs, off, cfg, group_term, term_start, match, next, active, committed,          \
+  geo, recs, pt, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
       stepdown_at, advanced, chunk_slow, any_slow, shards
 
 // One chunk c (the whole workgroup).
@@ -163,7 +164,8 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   u32 total = rtab.finish(rq);
   __syncthreads();
   constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
-  u64 rmr[kRecPer], rix[kRecPer];
+  const RecFmt fmt = geo.fmt;
+  u64 rec[kRecPer];
   auto load = [&](u32 f0, u32 n) {
     u32 ix[kRecPer];
 #pragma unroll
@@ -172,10 +174,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       ix[r] = n ? rtab.locate_fixed(f < n ? f : n - 1) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kRecPer; ++r) {
-      rmr[r] = recs.mr[ix[r]];
-      rix[r] = recs.index[ix[r]];
-    }
+    for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
   };
   auto apply = [&](u32 f0, u32 n) {
 #pragma unroll
@@ -183,26 +182,32 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       const u32 f = f0 + u32(r) * B + threadIdx.x;
       bool stale = false, applied = false, rejected = false, non = false;
       if (f < n && fits) {
-        const u64 mr = rmr[r];
-        const u32 t32 = u32(mr >> 32), meta = u32(mr);
-        const u32 lg = meta & 1023u, s = (meta >> 17) & 15u;
+        const u64 x = rec[r];
+        const u32 lg = fmt.lg(x), s = fmt.slot(x);
         const u32 base = offs[lg] - a0, sg = offs[lg + 1] - offs[lg];
-        const u64 gt = gterm[lg];
         if (s >= sg) {
           non = true;                                     // no Progress: raft.go:1100-1104
-        } else if (t32 == kTermEscape || u64(t32) > gt) {
-          slow = 1;  // higher term (step-down order) or ambiguous compare
-        } else if (u64(t32) < gt) {
-          stale = true;                                   // raft.go:883-921
         } else {
-          atomicOr(&act[lg], 1u << s);                    // raft.go:1107
-          if (meta & (1u << 24)) {  // QB_REC_REJECT
-            rejected = true;                              // raft.go:1109: not MaybeUpdate
+          u64 t = fmt.term(x), idx = fmt.payload(x);
+          if (t == fmt.tesc()) {  // escape: the exact values from the batch
+            const u32 ridx = u32(idx);
+            idx = rec_index[ridx];
+            t = rec_term[ridx];
+          }
+          const u64 gt = gterm[lg];
+          if (t > gt) {
+            slow = 1;  // higher term: step-down order (raft.go:875-879)
+          } else if (t < gt) {
+            stale = true;                                 // raft.go:883-921
           } else {
-            applied = true;
-            const u64 idx = rix[r];
-            atomicMax(&acc[base + s], idx);               // progress.go:146-150
-            if constexpr (NEXT) atomicMax(&accn[base + s], idx + 1ull);  // :151
+            atomicOr(&act[lg], 1u << s);                  // raft.go:1107
+            if (fmt.rej(x)) {
+              rejected = true;                            // raft.go:1109: not MaybeUpdate
+            } else {
+              applied = true;
+              atomicMax(&acc[base + s], idx);             // progress.go:146-150
+              if constexpr (NEXT) atomicMax(&accn[base + s], idx + 1ull);  // :151
+            }
           }
         }
       }
@@ -214,13 +219,13 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   };
   load(0, total);
 #pragma unroll
-  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
   apply(0, total);
   for (u32 pb = p0, f0 = B * kRecPer;;) {
     for (; f0 < total; f0 += B * kRecPer) {
       load(f0, total);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rmr[r]), "+v"(rix[r]));
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
       apply(f0, total);
     }
     pb += RunTable::kRuns;
@@ -313,6 +318,7 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY
 }
 
 struct CsrStepArgs {
+  const u64 *ri, *rt;  // the original batch (escape records)
   const u32 *off, *cfg;
   const u64 *gt, *ts;
   u64 *match, *next;
@@ -332,7 +338,8 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX> : k_csr_apply<WMAX, CAPW, NX>), \
-                     grid, dim3(csr_block()), 0, st, geo, recs, pt, cs, a.off, a.cfg, a.gt, a.ts,  \
+                     grid, dim3(csr_block()), 0, st, geo, recs, pt, cs, a.ri, a.rt, a.off, a.cfg,  \
+                     a.gt, a.ts,                                                                   \
                      a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
                      a.any_slow, a.shards)
   if (a.next) QB_CSR_LAUNCH(true);
@@ -366,7 +373,7 @@ u32 csr_wmax(uint32_t max_slots) {
 extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
   if (max_slots > QB_MAX_SLOTS) return 0;
   const u32 w = csr_wmax(max_slots);
-  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 2).total;
+  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 1).total;
 }
 
 extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
@@ -392,7 +399,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   // chunk size follows the LDS run capacity (chunk_groups(wmax))
   bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax), bk::kSbIl);
   geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
-  const bk::Carve cv = bk::carve(geo, 2);
+  const bk::Carve cv = bk::carve(geo, 1);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
              "workspace too small: need %zu bytes (qb_csr_tracker_workspace_bytes)", cv.total);
   QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
@@ -401,16 +408,18 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const bk::Cols buf2 = bk::cols_at(ws + cv.buf2, M, 2);
+  const bk::Cols buf2 = bk::compact_at(ws + cv.buf2, nullptr);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
   {
     const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags, ri, rtm, shards, st,
-                                      /*term32=*/false, /*packed=*/true);
+                                      /*term32=*/false, /*compact=*/true);
     if (rc != QB_OK) return rc;
   }
-  const bk::CsrStepArgs a{off,
+  const bk::CsrStepArgs a{ri,
+                          rtm,
+                          off,
                           cfg,
                           reinterpret_cast<const u64*>(group_term),
                           reinterpret_cast<const u64*>(term_start),

@@ -33,7 +33,8 @@ STAT_ORDER = ("applied", "rejected", "stale_term", "non_member", "higher_term", 
 
 
 def host_threads() -> int:
-    return max(1, len(os.sched_getaffinity(0)))
+    import bench
+    return bench.host_cpu_info()["threads"]
 
 
 def check_fixed(dev, n: int, G: int, seed: int = 0x5EED0002) -> str:

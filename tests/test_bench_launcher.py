@@ -67,6 +67,7 @@ def test_host_cpu_info_fields():
     assert info["logical_cpus"] == os.cpu_count()
     assert info["model"]                       # /proc/cpuinfo model name
     assert info["physical_cores"] is None or info["physical_cores"] >= 1
+    assert 1 <= info["threads"] <= info["affinity_cpus"]
 
 
 def test_route_columns_normalised_or_refused():
