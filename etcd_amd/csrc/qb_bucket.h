@@ -102,6 +102,10 @@ constexpr bool kSbIl = QB_SB_IL != 0;
 #ifndef QB_CSR_FULL
 #define QB_CSR_FULL 0
 #endif
+// Records a K5 workgroup has in flight per pass (both tracker steps).
+#ifndef QB_K5_INFLIGHT
+#define QB_K5_INFLIGHT 1024
+#endif
 __device__ __forceinline__ u32 xcd_major() {
   return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
 }

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
   // loaded before the first is classified.
   u32 total = rt.finish(rq);
   __syncthreads();
-  constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
+  constexpr int kRecPer = int(QB_K5_INFLIGHT / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
   // branch-free (clamped; an empty chunk reads record 0, which exists)

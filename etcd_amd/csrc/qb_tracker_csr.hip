@@ -163,7 +163,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
   u32 total = rtab.finish(rq);
   __syncthreads();
-  constexpr int kRecPer = int(1024 / B);  // 1024 records in flight per workgroup
+  constexpr int kRecPer = int(QB_K5_INFLIGHT / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
   auto load = [&](u32 f0, u32 n) {

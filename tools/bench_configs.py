@@ -479,7 +479,12 @@ def main():
     ap.add_argument("--only", default="3,4,5")
     ap.add_argument("--gpu-only", action="store_true",
                     help="leader, wire, confchange: skip the CPU baseline (A/B)")
+    ap.add_argument("--lab-lib", default=None,
+                    help="A/B runs: bind this libquorumbatch.so build (etcd_amd._lib.use_lab_library)")
     a = ap.parse_args()
+    if a.lab_lib:
+        from etcd_amd import _lib
+        _lib.use_lab_library(a.lab_lib)
     global GPU_ONLY
     GPU_ONLY = a.gpu_only
     which = set(a.only.split(","))

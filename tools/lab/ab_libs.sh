@@ -8,7 +8,7 @@ cfg=$1; rounds=$2; shift 2
 for i in $(seq $rounds); do
   for name in "$@"; do
     if [ "$name" = tree ]; then lp=""; else lp=$PWD/tools/lab/ab/$name.so; fi
-    QB_LIB_PATH=$lp timeout -k 10 150 python tools/bench_configs.py --only $cfg --gpu-only --reps 20 2>/dev/null \
+    timeout -k 10 150 python tools/bench_configs.py ${lp:+--lab-lib $lp} --only $cfg --gpu-only --reps 20 2>/dev/null \
       | python -c "import sys,json
 for l in sys.stdin:
     d=json.loads(l); print('$name', d['config'][:40], 'us', round(d['per_launch_us'],1), 'frac', round(d.get('frac_hbm_peak',0),3), flush=True)"

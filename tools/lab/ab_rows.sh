@@ -8,7 +8,7 @@ rounds=$1; row=$2; shift 2
 for i in $(seq $rounds); do
   for name in "$@"; do
     if [ "$name" = tree ]; then lp=""; else lp=$PWD/tools/lab/ab/$name.so; fi
-    if QB_LIB_PATH=$lp timeout -k 10 150 python3 tools/bench_configs.py --only $row --reps 10 --gpu-only \
+    if timeout -k 10 150 python3 tools/bench_configs.py ${lp:+--lab-lib $lp} --only $row --reps 10 --gpu-only \
         > /tmp/abr_$name.json 2> /tmp/abr_$name.err; then
       echo "$name $(tail -1 /tmp/abr_$name.json)"
     else

@@ -8,7 +8,7 @@ rounds=$1; wl=$2; shift 2
 for i in $(seq $rounds); do
   for name in "$@"; do
     if [ "$name" = tree ]; then lp=""; else lp=$PWD/tools/lab/ab/$name.so; fi
-    if QB_LIB_PATH=$lp timeout -k 10 150 python3 bench.py --workload $wl --no-cpu-baseline --preroll-ms 200 \
+    if timeout -k 10 150 python3 bench.py ${lp:+--lab-lib $lp} --workload $wl --no-cpu-baseline --preroll-ms 200 \
         > /tmp/ab_$name.json 2> /tmp/ab_$name.err; then
       python3 -c "import sys,json
 d=json.loads(open('/tmp/ab_$name.json').read().strip().splitlines()[-1]); r=d['roofline']

@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 cfg=$1; shift
 for name in "$@"; do
   if [ "$name" = tree ]; then lp=""; else lp=$PWD/tools/lab/ab/$name.so; fi
-  QB_LIB_PATH=$lp timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$name -o run \
-    -- python3 tools/bench_configs.py --only $cfg --gpu-only --reps 20 > gpurun_out/prof_$name.log 2>&1
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$name -o run \
+    -- python3 tools/bench_configs.py ${lp:+--lab-lib $lp} --only $cfg --gpu-only --reps 20 > gpurun_out/prof_$name.log 2>&1
   f=$(find gpurun_out/prof_$name -name '*kernel_stats.csv' | head -1)
   echo "== $name"; python3 -c "
 import csv,sys
