@@ -523,8 +523,15 @@ __host__ __device__ constexpr u32 k5_block(int n) {
   return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
 }
 
+#ifndef QB_K5_WAVES
+#define QB_K5_WAVES 0  // 0: the compiler's choice; else a VGPR cap (amdgpu_num_vgpr, A/B knob)
+#endif
 template <int N, bool NEXT>
-__global__ __launch_bounds__(k5_block(N)) void k_bk_apply(
+__global__ __launch_bounds__(k5_block(N))
+#if QB_K5_WAVES > 0
+__attribute__((amdgpu_num_vgpr(QB_K5_WAVES)))
+#endif
+void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
     const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
