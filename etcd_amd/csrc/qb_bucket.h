@@ -100,7 +100,7 @@ constexpr bool kSbIl = QB_SB_IL != 0;
 #define QB_K5_FULL 2
 #endif
 #ifndef QB_CSR_FULL
-#define QB_CSR_FULL 0
+#define QB_CSR_FULL 2  // round 3 (compact records): 776 -> 764 us per 16M ragged tick
 #endif
 // Records a K5 workgroup has in flight per pass (both tracker steps).
 #ifndef QB_K5_INFLIGHT

@@ -253,8 +253,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       const u64 a = acc[j];
       const bool up = a > old[p];
       if (up) old[p] = a;
-      // QB_CSR_FULL (as QB_K5_FULL): whole wave segments measured neutral in
-      // time here with twice the bytes written, so changed slots only
+      // QB_CSR_FULL (as QB_K5_FULL): whole wave segments where any slot
+      // changed — neutral in round 2, 12 us faster per 16M-group tick with
+      // the compact records (profiles/r03/k5_variants/)
       if (QB_CSR_FULL >= 2 ? __ballot(up) != 0 : up) match[a0 + j] = old[p];
       acc[j] = old[p];
       if constexpr (NEXT) {
