@@ -20,8 +20,17 @@
 //
 // Per group (one thread): the old slots and the changes are replayed on a
 // small working table in LDS (IDs + role bitmasks over table entries), then
-// the surviving entries are sorted by ID into the new slots.  Two launches
+// the surviving entries are sorted by ID into the new slots.  Two passes
 // (count, then write after a scan of the counts) recompute the same replay.
+//
+// Table size (round 3): the replay is latency-bound and its occupancy is set
+// by the table's LDS (24 entries x 8 B x 128 threads = 24 KB per workgroup:
+// 3 waves per SIMD).  A group whose old slots plus change entries number at
+// most kSmall can never hold more than kSmall table entries (each change adds
+// at most one), so each pass runs twice: a kSmall-entry launch for those
+// groups (8 KB per workgroup: 10 waves per SIMD), then a kTab-entry launch,
+// grid-strided, for the rest — which returns at once when the first launch
+// saw none (a flag word in the workspace).  Same replay, same results.
 #include "qb_common.h"
 #include "qb_scan.h"
 
@@ -29,7 +38,9 @@ namespace qb {
 namespace cc {
 
 constexpr int kBlk = 128;
-constexpr int kTab = 24;  // working table: old slots + new IDs alive at once
+constexpr int kTab = 24;   // working table: old slots + new IDs alive at once
+constexpr int kSmall = 8;  // the first launch's table (old slots + changes <= 8)
+constexpr unsigned kBigGrid = 1024;  // workgroups of the grid-strided kTab launches
 
 // A thread's working table, column-major in the workgroup's LDS block
 // (entry k of thread t at [k][t]): the lanes of a wave touch consecutive
@@ -70,7 +81,14 @@ struct Args {
   u64* n_infl_buf;
   u8* err;
   u64* err_id;
+  u32* any_big;  // workspace word: a group needs the kTab table
 };
+
+// A group's table can exceed kSmall entries only when its old slots plus its
+// change entries do (each change adds at most one entry).
+__device__ __forceinline__ bool needs_big(const Args& A, u64 g) {
+  return (A.off[g + 1] - A.off[g]) + (A.cc_off[g + 1] - A.cc_off[g]) > u32(kSmall);
+}
 
 // Role bitmasks over table entries.
 struct Roles {
@@ -109,6 +127,7 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
 // Replays group g's operation.  On success fills the table/roles of the new
 // config and returns 0; otherwise an error code (the table then holds the
 // old config).  Roles.fresh marks entries whose Progress is (re)created.
+template <int TAB>
 __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autoleave, u64* bad,
                       int* n_old) {
   const u32 s0 = A.off[g], s1 = A.off[g + 1];
@@ -161,7 +180,7 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
     if (typ == QB_CC_ADD_NODE || typ == QB_CC_ADD_LEARNER) {
       if (!has_pr) {  // initProgress
         if (x < 0) {
-          if (r.n < kTab) {
+          if (r.n < TAB) {
             x = r.n++;
           } else {
             // Reuse an entry this change list freed (an ID it added and then
@@ -233,19 +252,43 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
   return 0;
 }
 
+// The groups of pass BIG in [base, base + kBlk): kSmall launch (BIG false) —
+// one workgroup per block of groups, the small ones; kTab launch (BIG true) —
+// grid-strided over all blocks, the others, nothing at all when the kSmall
+// launch flagged none.
+template <bool BIG, class F>
+__device__ __forceinline__ void for_my_groups(const Args& A, F&& f) {
+  if constexpr (!BIG) {
+    const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
+    const bool live = g < A.G;
+    const bool big = live && needs_big(A, g);
+    if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(A.any_big, 1u);  // one per wave
+    if (!live || big) return;
+    f(g);
+  } else {
+    if (*A.any_big == 0) return;  // uniform: the first launch saw no big group
+    for (u64 base = u64(blockIdx.x) * kBlk; base < A.G; base += u64(gridDim.x) * kBlk) {
+      const u64 g = base + threadIdx.x;
+      const bool mine = g < A.G && needs_big(A, g);
+      if (mine) f(g);
+    }
+  }
+}
+
+template <int TAB, bool BIG>
 __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
-  __shared__ u64 tabs[kTab][kBlk];
-  const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
-  if (g >= A.G) return;
-  Tab t = tab_of(tabs);
-  Roles r;
-  bool al;
-  u64 bad = 0;
-  int n_old;
-  const int rc = replay(A, g, t, r, al, &bad, &n_old);
-  A.new_cnt[g] = rc ? u32(n_old) : u32(__popc(r.prs));
-  A.err[g] = u8(rc);
-  if (A.err_id) A.err_id[g] = rc ? bad : 0;
+  __shared__ u64 tabs[TAB][kBlk];
+  for_my_groups<BIG>(A, [&](u64 g) {
+    Tab t = tab_of(tabs);
+    Roles r;
+    bool al;
+    u64 bad = 0;
+    int n_old;
+    const int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
+    A.new_cnt[g] = rc ? u32(n_old) : u32(__popc(r.prs));
+    A.err[g] = u8(rc);
+    if (A.err_id) A.err_id[g] = rc ? bad : 0;
+  });
 }
 
 // The per-group pass only stores: new IDs, masks, and initProgress for fresh
@@ -265,16 +308,14 @@ constexpr u8 kFresh = 0xFE;
 #define QB_CC_FRESH_IN_COPY 1
 #endif
 
-__global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
-  __shared__ u64 tabs[kTab][kBlk];
-  const u64 g = u64(blockIdx.x) * kBlk + threadIdx.x;
-  if (g >= A.G) return;
+template <int TAB>
+__device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
   Tab t = tab_of(tabs);
   Roles r;
   bool al;
   u64 bad = 0;
   int n_old;
-  int rc = replay(A, g, t, r, al, &bad, &n_old);
+  int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
   const u32 s0 = A.off[g];
   const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
   if (d1 > A.S_cap) return;  // the caller's capacity is exceeded (reported by new_off[G])
@@ -296,8 +337,9 @@ __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
     if (r.out & b) ncfg_out |= 1u << j;
     if (r.lnext & b) nlnext |= 1u << j;
     const u64 d = d0 + j;
+    const bool carried = best < n_old && !(r.fresh & b);
     A.n_ids[d] = t.id(best);
-    if (best < n_old && !(r.fresh & b)) {  // carried Progress: k_cc_copy
+    if (carried) {  // carried Progress: k_cc_copy
       A.n_pstate[d] = kCarried;
       A.n_infl_pos[d] = s0 + u32(best);
     } else if (QB_CC_FRESH_IN_COPY) {  // initProgress (confchange.go:258-281): k_cc_copy
@@ -370,6 +412,12 @@ __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
   A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
 }
 
+template <int TAB, bool BIG>
+__global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
+  __shared__ u64 tabs[TAB][kBlk];
+  for_my_groups<BIG>(A, [&](u64 g) { write_group<TAB>(A, g, tabs); });
+}
+
 // One thread per new slot d < min(new_off[G], S_cap), grid-stride: a carried
 // slot's match / next / pendingSnapshot / inflight position / state byte and
 // its ring come from the old slot; a fresh slot's ring is zeroed.  A slot of
@@ -423,7 +471,8 @@ __global__ __launch_bounds__(256) void k_cc_copy(Args A) {
 using namespace qb;
 
 extern "C" size_t qb_conf_change_workspace_bytes(uint64_t G) {
-  return (scan::blocks(G) + 1) * sizeof(u32) + 256;
+  // the scan's block sums, then the any_big word
+  return (scan::blocks(G) + 1) * sizeof(u32) + 256 + 256;
 }
 
 extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_change_out* out,
@@ -475,12 +524,21 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
   A.err = out->err;
   A.err_id = reinterpret_cast<u64*>(out->err_id);
   hipStream_t st = as_stream(stream);
+  const size_t scan_bytes = (scan::blocks(G) + 1) * sizeof(u32);
+  A.any_big = reinterpret_cast<u32*>(static_cast<char*>(workspace) + (scan_bytes + 255) / 256 * 256);
+  {
+    const hipError_t e = hipMemsetAsync(A.any_big, 0, sizeof(u32), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(any_big)");
+  }
   const unsigned grid = unsigned((G + cc::kBlk - 1) / cc::kBlk);
-  hipLaunchKernelGGL(cc::k_cc_count, dim3(grid), dim3(cc::kBlk), 0, st, A);
+  const unsigned big_grid = grid < cc::kBigGrid ? grid : cc::kBigGrid;
+  hipLaunchKernelGGL((cc::k_cc_count<cc::kSmall, false>), dim3(grid), dim3(cc::kBlk), 0, st, A);
+  hipLaunchKernelGGL((cc::k_cc_count<cc::kTab, true>), dim3(big_grid), dim3(cc::kBlk), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_count");
   scan::launch(out->new_off, G, static_cast<u32*>(workspace), st);
   QB_CHECK_LAUNCH("scan(conf change)");
-  hipLaunchKernelGGL(cc::k_cc_write, dim3(grid), dim3(cc::kBlk), 0, st, A);
+  hipLaunchKernelGGL((cc::k_cc_write<cc::kSmall, false>), dim3(grid), dim3(cc::kBlk), 0, st, A);
+  hipLaunchKernelGGL((cc::k_cc_write<cc::kTab, true>), dim3(big_grid), dim3(cc::kBlk), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_write");
   hipLaunchKernelGGL(cc::k_cc_copy, dim3(2048), dim3(256), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_copy");
