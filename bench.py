@@ -778,6 +778,27 @@ def eval_main(args, world, rank, dev, barrier):
                       for g, (c, v) in zip(groups, outs)] for st in streams]
     torch.cuda.synchronize()
     fname = "qb_dev_csr_committed_vote" if csr else "qb_dev_fixed_committed_vote"
+    native = not csr and args.launcher == "native"
+    if native:
+        # configs[1]: the steps are enqueued from C (qb_dev_fixed_committed_vote_batches,
+        # one ABI call per period of the batch/stream rotation) instead of one
+        # ctypes call per launch
+        import math
+
+        class FixedBatch(C.Structure):
+            _fields_ = [(f, C.c_void_p) for f in ("match", "voted", "granted", "commit_out",
+                                                   "vote_out")]
+        P = B * S // math.gcd(B, S)  # step k -> batch k % B on stream k % S
+
+        def batch_table(pick):
+            return (FixedBatch * P)(*[FixedBatch(groups[pick(k)].match.data_ptr(),
+                                                 groups[pick(k)].voted.data_ptr(),
+                                                 groups[pick(k)].granted.data_ptr(),
+                                                 outs[pick(k)][0].data_ptr(),
+                                                 outs[pick(k)][1].data_ptr()) for k in range(P)])
+        tables = {None: batch_table(lambda k: k % B), 0: batch_table(lambda k: 0)}
+        stream_arr = (C.c_void_p * S)(*[st.cuda_stream for st in streams])
+        fnb = lib.qb_dev_fixed_committed_vote_batches
 
     def run_steps(count, fixed_batch=None, fork=True):
         # fork=False: the caller has synchronised the device, so the launch
@@ -787,11 +808,19 @@ def eval_main(args, world, rank, dev, barrier):
         if fork:
             for st in streams:
                 st.wait_stream(main_stream)
-        for k in range(count):
-            b = k % B if fixed_batch is None else fixed_batch
-            rc = fn(*call_args[k % S][b])
-            if rc:
-                _lib.check(rc, fname)
+        if native:
+            tab = tables[fixed_batch]
+            full, rem = divmod(count, P)
+            for c in [P] * full + ([rem] if rem else []):
+                rc = fnb(n, G, c, tab, stream_arr, S)
+                if rc:
+                    _lib.check(rc, "qb_dev_fixed_committed_vote_batches")
+        else:
+            for k in range(count):
+                b = k % B if fixed_batch is None else fixed_batch
+                rc = fn(*call_args[k % S][b])
+                if rc:
+                    _lib.check(rc, fname)
         if fork:
             for st in streams:
                 main_stream.wait_stream(st)
@@ -939,6 +968,7 @@ def eval_main(args, world, rank, dev, barrier):
             kname = (f"k_fixed_lds<{n},{4 if n <= 5 else 2},true>" if n <= 8
                      else f"k_fixed<{n},2,true,true>")
         cfg.update({"batches_resident": B, "streams": S, "graph_steps": args.graph,
+                    "launcher": "native" if native else "python",
                     "parallelism": f"groups sharded by id over {world} GPU(s)"})
         achieved = bpg * G / avg_kernel_s / 1e9
         out = {
@@ -1025,6 +1055,9 @@ def parse_args(argv=None):
     ap.add_argument("--graph", type=int, default=0,
                     help="launch the steps from a captured HIP graph of this many steps "
                          "(0 = direct launches); the remainder of K is launched directly")
+    ap.add_argument("--launcher", default="native", choices=["native", "python"],
+                    help="configs[1]: enqueue the steps from C (qb_dev_fixed_committed_vote_batches) "
+                         "or with one ctypes call per launch")
     ap.add_argument("--lab-lib", default=None,
                     help="A/B lab runs: bind this build of libquorumbatch.so instead of the "
                          "in-tree one (etcd_amd._lib.use_lab_library)")

@@ -58,6 +58,7 @@ SIGNATURES = {
     "qb_stream_sync": (_i32, [_p]),
     "qb_host_compile_configs": (_i32, [_u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _p]),
     "qb_dev_fixed_committed_vote": (_i32, [_u32, _u64, _p, _p, _p, _p, _p, _p]),
+    "qb_dev_fixed_committed_vote_batches": (_i32, [_u32, _u64, _u32, _p, _p, _u32]),
     "qb_dev_csr_committed_vote": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p]),
     "qb_dev_csr_validate": (_i32, [_u64, _u32, _p, _p, _p]),
     "qb_dev_csr_committed_vote_checked": (_i32, [_u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p]),

@@ -309,6 +309,20 @@ extern "C" int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_
   return QB_OK;
 }
 
+extern "C" int qb_dev_fixed_committed_vote_batches(uint32_t n, uint64_t G, uint32_t count,
+                                                   const qb_fixed_batch* batches,
+                                                   void* const* streams, uint32_t nstreams) {
+  if (count == 0) return QB_OK;
+  QB_REQUIRE(batches && streams && nstreams >= 1, "batches / streams NULL or nstreams == 0");
+  for (uint32_t i = 0; i < count; ++i) {
+    const qb_fixed_batch& b = batches[i];
+    const int rc = qb_dev_fixed_committed_vote(n, G, b.match, b.voted, b.granted, b.commit_out,
+                                               b.vote_out, streams[i % nstreams]);
+    if (rc != QB_OK) return rc;
+  }
+  return QB_OK;
+}
+
 // -------------------------------------------------------------------- CSR ---
 //
 // A workgroup owns kBlock consecutive groups.  Their slots are one contiguous

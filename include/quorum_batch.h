@@ -175,6 +175,22 @@ int qb_dev_fixed_committed_vote(uint32_t n, uint64_t G, const uint64_t* match,
                                 uint64_t* commit_out, uint8_t* vote_out,
                                 void* stream);
 
+/* Several FIXED batches of one shape in one call (one cgo call per tick for
+ * an embedder holding several shards' batches, instead of one per batch):
+ * batch i is qb_dev_fixed_committed_vote(n, G, batches[i]...) enqueued on
+ * streams[i % nstreams] (nstreams >= 1; a NULL entry is the default stream),
+ * in order; stops at the first failing batch and returns its code. */
+typedef struct qb_fixed_batch {
+  const uint64_t* match;  /* [n][G] */
+  const void* voted;      /* [G] u8 (n <= 8) or u16 */
+  const void* granted;
+  uint64_t* commit_out;   /* [G] or NULL */
+  uint8_t* vote_out;      /* [G] or NULL */
+} qb_fixed_batch;
+int qb_dev_fixed_committed_vote_batches(uint32_t n, uint64_t G, uint32_t count,
+                                        const qb_fixed_batch* batches, void* const* streams,
+                                        uint32_t nstreams);
+
 /* CommittedIndex and/or VoteResult for G ragged/joint groups (CSR layout).
  * Replaces JointConfig.CommittedIndex (quorum/joint.go:49-56) and
  * JointConfig.VoteResult (quorum/joint.go:61-75), which reduce to the

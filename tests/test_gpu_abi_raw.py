@@ -365,3 +365,49 @@ def test_route_records_world1_raw_abi():
         assert np.array_equal(s.down(dout[k], v), v), k
     _lib.check(lib.qb_comm_destroy(comm), "comm destroy")
     s.close()
+
+
+def test_fixed_batches_raw_abi():
+    """qb_dev_fixed_committed_vote_batches: several batches of one shape in
+    one call over two streams (batch i on stream i % 2), each bit-exact vs
+    the oracle; a bad batch stops the call with its error."""
+    lib = _lib.load()
+    _lib.check(lib.qb_set_device(0), "qb_set_device")
+    sts = [C.c_void_p(), C.c_void_p()]
+    for s in sts:
+        _lib.check(lib.qb_stream_create(C.byref(s)), "qb_stream_create")
+    d = Dev()
+    n, G, B = 7, 30001, 5
+
+    class FB(C.Structure):
+        _fields_ = [(f, C.c_void_p) for f in ("match", "voted", "granted", "commit_out",
+                                               "vote_out")]
+    host, tab = [], (FB * B)()
+    for b in range(B):
+        match, vd, gr, _ = oc.gen_fixed(0x5EED0002, n, G, g_begin=b * G)
+        dm, dvd, dgr, dc, dv = (d.alloc(match.nbytes), d.alloc(G), d.alloc(G), d.alloc(8 * G),
+                                d.alloc(G))
+        for dst, src in ((dm, match), (dvd, vd), (dgr, gr)):
+            _lib.check(lib.qb_copy_h2d_async(dst, src.ctypes.data, src.nbytes, sts[0]), "h2d")
+        tab[b] = FB(dm, dvd, dgr, dc, dv)
+        host.append((match, vd, gr, dc, dv))
+    _lib.check(lib.qb_stream_sync(sts[0]), "sync")
+    streams = (C.c_void_p * 2)(sts[0].value, sts[1].value)
+    _lib.check(lib.qb_dev_fixed_committed_vote_batches(n, G, B, tab, streams, 2), "batches")
+    for s in sts:
+        _lib.check(lib.qb_stream_sync(s), "sync")
+    for match, vd, gr, dc, dv in host:
+        c, v = np.empty(G, np.uint64), np.empty(G, np.uint8)
+        _lib.check(lib.qb_copy_d2h_async(c.ctypes.data, dc, c.nbytes, sts[0]), "d2h")
+        _lib.check(lib.qb_copy_d2h_async(v.ctypes.data, dv, v.nbytes, sts[0]), "d2h")
+        _lib.check(lib.qb_stream_sync(sts[0]), "sync")
+        ec, ev = oc.fixed_eval(n, match, vd, gr)
+        assert np.array_equal(c, ec) and np.array_equal(v, ev)
+    tab[2] = FB(None, host[2][1].ctypes.data, None, host[2][3], None)  # commit without match
+    assert lib.qb_dev_fixed_committed_vote_batches(n, G, B, tab, streams, 2) == _lib.QB_EINVAL
+    assert lib.qb_dev_fixed_committed_vote_batches(n, G, B, tab, None, 0) == _lib.QB_EINVAL
+    for s in sts:
+        _lib.check(lib.qb_stream_sync(s), "sync")
+    d.close()
+    for s in sts:
+        _lib.check(lib.qb_stream_destroy(s), "qb_stream_destroy")
