@@ -403,7 +403,7 @@ def test_fixed_batches_raw_abi():
         _lib.check(lib.qb_stream_sync(sts[0]), "sync")
         ec, ev = oc.fixed_eval(n, match, vd, gr)
         assert np.array_equal(c, ec) and np.array_equal(v, ev)
-    tab[2] = FB(None, host[2][1].ctypes.data, None, host[2][3], None)  # commit without match
+    tab[2] = FB(None, None, None, host[2][3], None)  # commit_out without match
     assert lib.qb_dev_fixed_committed_vote_batches(n, G, B, tab, streams, 2) == _lib.QB_EINVAL
     assert lib.qb_dev_fixed_committed_vote_batches(n, G, B, tab, None, 0) == _lib.QB_EINVAL
     for s in sts:
