@@ -527,11 +527,37 @@ struct SlotStage {
   u64 next[kSpanCap];
   u32 ipos[kSpanCap];
   u8 st[kSpanCap];
-  u8 dirty[kSpanCap];  // slot reached through pr_of: written back
+  u8 dirty[kSpanCap];  // fields of the slot whose value changed: written back
+};
+// dirty bits per staged field
+constexpr u8 kDirtyMatch = 1, kDirtyNext = 2, kDirtyIpos = 4, kDirtySt = 8;
+
+// A staged field: reads convert to the value; an assignment that changes it
+// marks the field dirty, so the write-back stores only changed fields (a
+// heartbeat response that leaves RecentActive set stores nothing; round 2
+// wrote all four arrays of every slot the step touched).
+template <class T, u8 BIT>
+struct StagedRef {
+  T& v;
+  u8& d;
+  __device__ __forceinline__ operator T() const { return v; }
+  __device__ __forceinline__ const StagedRef& operator=(T x) const {
+    if (x != v) {
+      v = x;
+      d |= BIT;
+    }
+    return *this;
+  }
 };
 __device__ __forceinline__ SlotStage& slot_stage() {
   __shared__ SlotStage ss;
   return ss;
+}
+
+// The HBM form (span too wide to stage) tracks nothing: a per-thread byte.
+__device__ __forceinline__ u8& dummy_dirty() {
+  __shared__ u8 sink[kBlock];
+  return sink[threadIdx.x];
 }
 
 template <bool S>
@@ -539,31 +565,30 @@ struct PrT {
   const Args* A;
   u64 p;  // slot index in the group arrays
   u32 j;  // slot index in the staged span (S)
-  __device__ __forceinline__ u64& match() const {
-    if constexpr (S) return slot_stage().match[j];
-    else return U(A->lg.match)[p];
+  __device__ __forceinline__ auto match() const {
+    if constexpr (S) return StagedRef<u64, kDirtyMatch>{slot_stage().match[j], slot_stage().dirty[j]};
+    else return StagedRef<u64, 0>{U(A->lg.match)[p], dummy_dirty()};
   }
-  __device__ __forceinline__ u64& next() const {
-    if constexpr (S) return slot_stage().next[j];
-    else return U(A->lg.next)[p];
+  __device__ __forceinline__ auto next() const {
+    if constexpr (S) return StagedRef<u64, kDirtyNext>{slot_stage().next[j], slot_stage().dirty[j]};
+    else return StagedRef<u64, 0>{U(A->lg.next)[p], dummy_dirty()};
   }
-  __device__ __forceinline__ u8& st() const {
-    if constexpr (S) return slot_stage().st[j];
-    else return A->lg.pstate[p];
+  __device__ __forceinline__ auto st() const {
+    if constexpr (S) return StagedRef<u8, kDirtySt>{slot_stage().st[j], slot_stage().dirty[j]};
+    else return StagedRef<u8, 0>{A->lg.pstate[p], dummy_dirty()};
   }
-  __device__ __forceinline__ u32& ipos() const {
-    if constexpr (S) return slot_stage().ipos[j];
-    else return A->lg.infl_pos[p];
+  __device__ __forceinline__ auto ipos() const {
+    if constexpr (S) return StagedRef<u32, kDirtyIpos>{slot_stage().ipos[j], slot_stage().dirty[j]};
+    else return StagedRef<u32, 0>{A->lg.infl_pos[p], dummy_dirty()};
   }
   __device__ __forceinline__ u64& psnap() const { return U(A->lg.pending_snapshot)[p]; }
   __device__ __forceinline__ u64* ibuf() const { return U(A->lg.infl_buf) + p * A->lg.inflight_cap; }
   __device__ __forceinline__ u32 K() const { return A->lg.inflight_cap; }
 };
-// Every Progress write goes through a PrT from here, so marking the slot
-// dirty here covers them all (maybe_commit only reads match).
+// Every Progress write goes through a PrT's StagedRef (maybe_commit only
+// reads match), which marks the changed fields.
 template <bool S>
 __device__ __forceinline__ PrT<S> pr_of(const Args& A, const Group& G_, u32 j) {
-  if constexpr (S) slot_stage().dirty[G_.j0 + j] = 1;
   return PrT<S>{&A, u64(G_.s0) + j, G_.j0 + j};
 }
 __device__ __forceinline__ u32 st_state(u8 s) { return s & 3u; }
@@ -964,11 +989,12 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
   if (staged) {
     __syncthreads();
     for (u32 j = threadIdx.x; j < span; j += kBlock) {
-      if (!ss.dirty[j]) continue;
-      U(A.lg.match)[sb + j] = ss.match[j];
-      U(A.lg.next)[sb + j] = ss.next[j];
-      A.lg.infl_pos[sb + j] = ss.ipos[j];
-      A.lg.pstate[sb + j] = ss.st[j];
+      const u8 dm = ss.dirty[j];
+      if (!dm) continue;
+      if (dm & kDirtyMatch) U(A.lg.match)[sb + j] = ss.match[j];
+      if (dm & kDirtyNext) U(A.lg.next)[sb + j] = ss.next[j];
+      if (dm & kDirtyIpos) A.lg.infl_pos[sb + j] = ss.ipos[j];
+      if (dm & kDirtySt) A.lg.pstate[sb + j] = ss.st[j];
     }
   }
   // Per-wave sums of per-thread counts, then one flush per block.
