@@ -611,12 +611,33 @@ template <class P>
 __device__ void infl_free_le(const P& p, u64 to) {
   const u32 pos = p.ipos();
   const u32 start = pos & 0xFFFFu, count = pos >> 16;
-  if (count == 0 || to < p.ibuf()[start]) return;
-  u32 idx = start, i = 0;
-  for (; i < count; ++i) {
-    if (to < p.ibuf()[idx]) break;
-    if (++idx >= p.K()) idx -= p.K();
+  const u32 K = p.K();
+  const u64* buf = p.ibuf();
+  // i = the ring's prefix of entries <= to (inflights.go:95-122), read four
+  // entries per round trip (clamped, branch-free) instead of one dependent
+  // load per entry
+  u32 i = 0;
+  bool done = count == 0;
+  while (!done && i < count) {
+    u64 e[4];
+#pragma unroll
+    for (u32 q = 0; q < 4; ++q) {
+      const u32 k = i + q < count ? i + q : count - 1;
+      u32 idx = start + k;
+      if (idx >= K) idx -= K;
+      e[q] = buf[idx];
+    }
+#pragma unroll
+    for (u32 q = 0; q < 4; ++q) {
+      if (!done && i < count) {
+        if (to < e[q]) done = true;
+        else ++i;
+      }
+    }
   }
+  if (i == 0) return;
+  u32 idx = start + i;
+  if (idx >= K) idx -= K;
   const u32 c2 = count - i;
   p.ipos() = c2 == 0 ? 0u : (idx | (c2 << 16));
 }
@@ -787,12 +808,17 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const PrT<S>&
   u64* qctx = U(A.lg.rq_ctx) + G_.g * cap;
   u64* qidx = U(A.lg.rq_index) + G_.g * cap;
   u32* qmeta = A.lg.rq_meta + G_.g * cap;
+  // The queue's contexts four at a time (branch-free, clamped): one round
+  // trip per four entries instead of one per entry of a dependent scan.
   u32 found = kNone;
-  for (u32 k = 0; k < qlen; ++k)
-    if (qctx[k] == ctx) {
-      found = k;
-      break;
-    }
+  for (u32 k0 = 0; k0 < qlen && found == kNone; k0 += 4) {
+    u64 c[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) c[i] = qctx[k0 + i < qlen ? k0 + i : qlen - 1];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i)
+      if (found == kNone && k0 + i < qlen && c[i] == ctx) found = k0 + i;
+  }
   u32 acks = 0;  // a nil map when the context is unknown
   if (found != kNone) {
     qmeta[found] |= 1u << slot;
@@ -801,12 +827,25 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const PrT<S>&
   if (acks_vote(G_, acks) != QB_VOTE_WON) return;
   if (found == kNone) return;  // advance finds nothing (read_only.go:113-121)
   // read_only.go:84-112 advance + raft.go:1304-1308 responses, oldest first.
-  for (u32 k = 0; k <= found; ++k) {
-    const u32 from = qmeta[k] >> 16;
-    if (from == kNoSlot || from == leader_slot(G_))
-      emit(A, G_, QB_READ_STATE, kNoSlot, qidx[k], 0, 0, qctx[k]);
-    else
-      emit(A, G_, QB_MSG_READ_INDEX_RESP, from, qidx[k], 0, 0, qctx[k]);
+  for (u32 k0 = 0; k0 <= found; k0 += 4) {  // loads of four entries issued together
+    u32 mt[4];
+    u64 ix[4], cx[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+      const u32 k = k0 + i <= found ? k0 + i : found;
+      mt[i] = qmeta[k];
+      ix[i] = qidx[k];
+      cx[i] = qctx[k];
+    }
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+      if (k0 + i > found) break;
+      const u32 from = mt[i] >> 16;
+      if (from == kNoSlot || from == leader_slot(G_))
+        emit(A, G_, QB_READ_STATE, kNoSlot, ix[i], 0, 0, cx[i]);
+      else
+        emit(A, G_, QB_MSG_READ_INDEX_RESP, from, ix[i], 0, 0, cx[i]);
+    }
   }
   const u32 rest = qlen - (found + 1);
   for (u32 k = 0; k < rest; ++k) {
