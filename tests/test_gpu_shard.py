@@ -189,3 +189,43 @@ def test_allgather_results_rccl_world1():
     the one GPU (RCCL refuses two ranks on one device)."""
     ok_c, ok_v, on_dev, n = _spawn(_nccl_world1_worker, 1, 50_000)
     assert ok_c and ok_v and on_dev and n == 50_000
+
+
+def _rccl_comm_world1_worker(rank, world, port, q, total):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from etcd_amd.comm import RcclComm
+        from etcd_amd.quorum import batch
+        dev = torch.device("cuda", 0)
+        comm = RcclComm.from_process_group(dev)
+        grp = batch.FixedGroups.synth(SEED, 5, total, device=dev)
+        c, v = grp.committed_vote()
+        gc, gv = comm.allgather_results(c, v, total)      # qb_dev_allgather_results
+        M = 10_000
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(3)
+        cols = {"group": torch.randint(0, total + 5, (M,), generator=gen, device=dev),  # int64
+                "flags": torch.randint(0, 5, (M,), generator=gen, device=dev).to(torch.uint8),
+                "index": torch.arange(M, device=dev, dtype=torch.int64)[::-1].contiguous(),
+                "term": torch.full((M,), 7, dtype=torch.int64, device=dev)}
+        got = comm.route_records(cols, total)               # qb_dev_route_records
+        torch.cuda.synchronize()
+        same = all(torch.equal(got[k].to(torch.int64), (cols[k] & 0xFFFFFFFF if k == "group"
+                                                         else cols[k]).to(torch.int64))
+                   for k in cols)
+        comm.close()
+        q.put((bool(torch.equal(gc, c)), bool(torch.equal(gv, v)), same, comm.world))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_rccl_comm_c_abi_world1():
+    """etcd_amd.comm.RcclComm — the C ABI's communicator, what bench.py's N > 1
+    path times — on a single-rank group: unique id over torch.distributed,
+    qb_comm_init, the all-gather and the record routing (every record stays,
+    in order, an int64 group column converted) against the inputs."""
+    ok_c, ok_v, ok_r, w = _spawn(_rccl_comm_world1_worker, 1, 50_000)
+    assert ok_c and ok_v and ok_r and w == 1
