@@ -102,6 +102,27 @@ constexpr bool kSbIl = QB_SB_IL != 0;
 #ifndef QB_CSR_FULL
 #define QB_CSR_FULL 2  // round 3 (compact records): 776 -> 764 us per 16M ragged tick
 #endif
+// Write granule of the whole-segment write-back (QB_K5_FULL / QB_CSR_FULL
+// = 2): a lane stores when any lane of its aligned granule of QB_WB_GRAN
+// 8-byte elements changed (64 = the whole wave segment).
+#ifndef QB_WB_GRAN
+#define QB_WB_GRAN 64
+#endif
+// Whether p holds on any lane of this lane's granule of W consecutive
+// elements, lane l holding element e0 + l (W a power of two < 64; e is this
+// lane's element index, so granules follow the memory alignment); W >= 64:
+// any lane of the wave.
+template <u32 W>
+__device__ __forceinline__ bool granule_any(bool p, u64 e) {
+  const u64 m = __ballot(p);
+  if constexpr (W >= 64) {
+    return m != 0;
+  } else {
+    const int lf = int(threadIdx.x & 63u) - int(e & (W - 1u));  // first lane of the granule
+    const u64 sel = (1ull << W) - 1ull;
+    return (m & (lf >= 0 ? sel << lf : sel >> -lf)) != 0;
+  }
+}
 // Records a K5 workgroup has in flight per pass (both tracker steps).
 #ifndef QB_K5_INFLIGHT
 #define QB_K5_INFLIGHT 1024

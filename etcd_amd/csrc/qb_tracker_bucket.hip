@@ -699,7 +699,8 @@ void k_bk_apply(
       const u64 a = acc_m[s * CH + lg];
       const bool up = live && a > v[k][s];
       if (up) v[k][s] = a;
-      if (QB_K5_FULL >= 2 ? (__ballot(up) != 0 && live) : up) match[u64(s) * geo.G + g] = v[k][s];
+      if (QB_K5_FULL >= 2 ? (granule_any<QB_WB_GRAN>(up, g) && live) : up)
+        match[u64(s) * geo.G + g] = v[k][s];
       if constexpr (NEXT) {
         if (live) {
           u64* q = next + u64(s) * geo.G + g;
@@ -711,9 +712,11 @@ void k_bk_apply(
     const u64 ci = select_quorum<N>(v[k]);
     const bool adv = live && ci > cm[k] && ci >= ts[k];  // log.go:328-334
     const u32 na = live ? act[lg] : 0u;
-    if (QB_K5_FULL >= 1 ? (__ballot(adv) != 0 && live) : adv) committed[g] = adv ? ci : cm[k];
+    if (QB_K5_FULL >= 1 ? (granule_any<QB_WB_GRAN>(adv, g) && live) : adv)
+      committed[g] = adv ? ci : cm[k];
     if (advanced && live) advanced[g] = adv ? 1 : 0;
-    if (QB_K5_FULL >= 1 ? (__ballot(na != 0) != 0 && live) : na != 0) active[g] = u16(av[k] | na);
+    if (QB_K5_FULL >= 1 ? (granule_any<4 * QB_WB_GRAN>(na != 0, g) && live) : na != 0)
+      active[g] = u16(av[k] | na);
   }
   const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
   tally.flush(tl, shard_of(shards), slot);

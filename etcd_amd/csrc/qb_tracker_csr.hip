@@ -256,7 +256,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       // QB_CSR_FULL (as QB_K5_FULL): whole wave segments where any slot
       // changed — neutral in round 2, 12 us faster per 16M-group tick with
       // the compact records (profiles/r03/k5_variants/)
-      if (QB_CSR_FULL >= 2 ? __ballot(up) != 0 : up) match[a0 + j] = old[p];
+      if (QB_CSR_FULL >= 2 ? granule_any<QB_WB_GRAN>(up, a0 + j) : up) match[a0 + j] = old[p];
       acc[j] = old[p];
       if constexpr (NEXT) {
         const u64 nn = accn[j];
@@ -283,10 +283,11 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     // log.go:328-334; an empty config's ci = MaxUint64 is past lastIndex,
     // whose term is 0 (log.go:271-273): never committed
     const bool adv = ci != kInf && ci > cm[k] && ci >= ts[k];
-    if (QB_CSR_FULL >= 1 ? __ballot(adv) != 0 : adv) committed[g] = adv ? ci : cm[k];
+    if (QB_CSR_FULL >= 1 ? granule_any<QB_WB_GRAN>(adv, g) : adv) committed[g] = adv ? ci : cm[k];
     if (advanced) advanced[g] = adv ? 1 : 0;
     const u32 na = act[lg];
-    if (QB_CSR_FULL >= 1 ? __ballot(na != 0) != 0 : na != 0) active[g] = u16(av[k] | na);
+    if (QB_CSR_FULL >= 1 ? granule_any<4 * QB_WB_GRAN>(na != 0, g) : na != 0)
+      active[g] = u16(av[k] | na);
   }
   const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
   tally.flush(tl, shard_of(shards), slot);

@@ -7,7 +7,9 @@ with the single-process C oracle over all groups, bit for bit.  gloo moves
 host tensors, so the collectives run on the .cpu() copies (the driver's
 multi-GPU bench runs the same calls over RCCL)."""
 import os
+import queue
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -30,13 +32,29 @@ def _free_port():
 
 
 def _spawn(target, world, *args):
+    """Run target on world ranks; rank 0's queued result.  A rank that dies
+    before queueing fails the test at once (not after the queue timeout)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
-    out = q.get(timeout=240)
+    deadline = time.monotonic() + 240
+    while True:
+        try:
+            out = q.get(timeout=1)
+            break
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"a rank exited with {dead[0]} before reporting")
+            if time.monotonic() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail("no result within 240 s")
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -208,7 +226,7 @@ def _rccl_comm_world1_worker(rank, world, port, q, total):
         gen.manual_seed(3)
         cols = {"group": torch.randint(0, total + 5, (M,), generator=gen, device=dev),  # int64
                 "flags": torch.randint(0, 5, (M,), generator=gen, device=dev).to(torch.uint8),
-                "index": torch.arange(M, device=dev, dtype=torch.int64)[::-1].contiguous(),
+                "index": torch.arange(M, device=dev, dtype=torch.int64).flip(0),
                 "term": torch.full((M,), 7, dtype=torch.int64, device=dev)}
         got = comm.route_records(cols, total)               # qb_dev_route_records
         torch.cuda.synchronize()
