@@ -132,7 +132,22 @@ struct BlockTally {
     __syncthreads();
     if (threadIdx.x < K && lds[threadIdx.x]) atomicAdd(dst + slot[threadIdx.x], u64(lds[threadIdx.x]));
   }
+  // flush() in two halves around a barrier the caller has anyway (no
+  // barriers of its own): stage() adds this wave's counts into lds (K u32,
+  // zeroed before an earlier barrier); after the caller's next
+  // __syncthreads(), publish() adds the block totals to dst.
+  __device__ __forceinline__ void stage(u32* lds) const {
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (t[k]) atomicAdd(&lds[k], t[k]);
+    }
+  }
+  __device__ __forceinline__ static void publish(const u32* lds, u64* dst, const int (&slot)[K]) {
+    if (threadIdx.x < K && lds[threadIdx.x]) atomicAdd(dst + slot[threadIdx.x], u64(lds[threadIdx.x]));
+  }
 };
+
 
 // ------------------------------------------------------------- LDS-DMA ---
 // global_load_lds_dwordx4: each lane's 16 bytes land at the wave-uniform LDS

@@ -38,6 +38,8 @@ namespace bk {
 // Invalid records (group >= G, slot >= n) are counted per tile into inval[2
 // * tile + {0, 1}] with plain stores; k_bk_sums_parts adds them to the stat
 // shards after zeroing those (so the step needs no memset).
+// (100 SGPRs hold it at 6 of its 256-thread blocks per CU by the residency
+// rule; capping them at 80 for 8 blocks measured neutral: not kept)
 __global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __restrict__ rg,
                                                     const u8* __restrict__ rf,
                                                     u32* __restrict__ hist,
@@ -184,8 +186,16 @@ __device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec
 // the first LDS step, so the loads overlap each other and the ranking; the
 // payload then goes register -> LDS -> permuted LDS read -> coalesced store.
 constexpr int kPer = kTile / kPartThreads;  // records per thread
+// Compact records (the tracker steps) go from registers straight to their
+// sorted LDS slot in K3 and K4 (QB_DIRECT; 0 = the permutation walk, A/B).
+#ifndef QB_DIRECT
+#define QB_DIRECT 1
+#endif
 
-__global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
+// (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs: the
+// direct placement's registers would otherwise leave one)
+__global__ __launch_bounds__(kPartThreads)
+__attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
     const u32* __restrict__ bsum, Cols out) {
@@ -255,6 +265,41 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_scatter(
     gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
   }
   __syncthreads();
+  if (QB_DIRECT && out.compact) {
+    // compact records: bin, rank and the encoded record stay in registers;
+    // after the scan each record is stored at its sorted LDS slot with its
+    // bin and chunk-low, and the output pass reads the slots in order
+    u32 bj[kPer], rj[kPer], cj[kPer];
+    u64 vj[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = rk(j);
+      const bool ok = g[j] < geo.G && (f[j] & 0x0Fu) < geo.n;  // (k >= nrec has g = ~0)
+      bj[j] = ok ? geo.sb_of(g[j]) : u32(kNoBin);
+      rj[j] = ok ? atomicAdd(&start[bj[j]], 1u) : 0u;
+      cj[j] = geo.cl_of_chunk(geo.chunk_of(g[j]));
+      vj[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j], vt[j],
+                             u32(t0 + k));
+    }
+    __syncthreads();
+    const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (bj[j] == u32(kNoBin)) continue;
+      const u32 e = start[bj[j]] + rj[j];
+      L.stage[e] = vj[j];
+      L.bin[e] = u16(bj[j]);
+      L.cl[e] = u8(cj[j]);
+    }
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+      const u32 b = L.bin[e];
+      const u32 d = gstart[b] + (e - start[b]);
+      out.mr[d] = L.stage[e];
+      out.cl[d] = L.cl[e];
+    }
+    return;
+  }
   if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
     u64 bins = 0, ranks = 0;
     u32 cls = 0;
@@ -468,6 +513,30 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
+  if (QB_DIRECT && in.compact) {
+    // compact records: each record's rank stays in a register and the record
+    // goes straight to its sorted LDS slot after the scan, so the output is
+    // read in order (no permutation array, no bin / rank stores)
+    u32 rk[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = threadIdx.x + j * kPartThreads;
+      rk[j] = k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    tile_scan_bins(start, kChunksPerSb, L.wsum);
+    if (threadIdx.x <= kChunksPerSb)
+      cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
+          lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const u32 k = threadIdx.x + j * kPartThreads;
+      if (k < nrec) L.stage[start[vc[j]] + rk[j]] = vm[j];
+    }
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[e];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
@@ -523,6 +592,13 @@ __host__ __device__ constexpr u32 k5_block(int n) {
   return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
 }
 
+// SGPR cap: the hardware admits min(8, 800 / (ceil(sgpr / 16) * 16 + 16))
+// waves per SIMD (MI355X_MICROARCH.md, residency), so the compiler's 92
+// SGPRs held K5 at 3 workgroups per CU where its VGPRs and LDS allow 4;
+// capped at 80 (a few SGPRs spill to VGPR lanes): -11 us per 16M-group tick.
+#ifndef QB_K5_SGPR
+#define QB_K5_SGPR 80
+#endif
 #ifndef QB_K5_WAVES
 #define QB_K5_WAVES 0  // 0: the compiler's choice; else a VGPR cap (amdgpu_num_vgpr, A/B knob)
 #endif
@@ -530,6 +606,9 @@ template <int N, bool NEXT>
 __global__ __launch_bounds__(k5_block(N))
 #if QB_K5_WAVES > 0
 __attribute__((amdgpu_num_vgpr(QB_K5_WAVES)))
+#endif
+#if QB_K5_SGPR > 0
+__attribute__((amdgpu_num_sgpr(QB_K5_SGPR)))
 #endif
 void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
@@ -596,6 +675,7 @@ void k_bk_apply(
     act[threadIdx.x + k * B] = 0;
   }
   if (threadIdx.x == 0) slow = 0;
+  if (threadIdx.x < 3) tl[threadIdx.x] = 0;
   // This chunk's records: one short run per part of its super-bucket,
   // flattened into one index space (RunTable) so every thread has a record
   // in flight at once; kRecPer records per thread, both columns of each
@@ -671,6 +751,10 @@ void k_bk_apply(
     total = rt.build(cs, pb, p1, cl);  // more than kRuns parts (synchronises)
     f0 = 0;
   }
+  // the counts are final: staged before the barrier the block takes anyway,
+  // published after it (a flush with barriers of its own at the end cost
+  // 15 us per 16M-group tick)
+  tally.stage(tl);
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
 #pragma unroll
@@ -685,6 +769,10 @@ void k_bk_apply(
     return;
   }
   if (threadIdx.x == 0) chunk_slow[c] = 0;
+  {
+    const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
+    BlockTally<3>::publish(tl, shard_of(shards), slot);
+  }
   // maybeCommit for every group of the chunk + write-back (coalesced rows).
   // Write-back granularity (QB_K5_FULL): a store only where the value
   // changed leaves partially written lines; 2 = a wave whose segment of a
@@ -718,8 +806,6 @@ void k_bk_apply(
     if (QB_K5_FULL >= 1 ? (granule_any<4 * QB_WB_GRAN>(na != 0, g) && live) : na != 0)
       active[g] = u16(av[k] | na);
   }
-  const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
-  tally.flush(tl, shard_of(shards), slot);
 }
 
 struct ApplyArgs {

@@ -113,6 +113,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     if constexpr (NEXT) accn[k] = 0;
   }
   if (threadIdx.x == 0) slow = 0;
+  if (threadIdx.x < 4) tl[threadIdx.x] = 0;
 #pragma unroll
   for (u32 q = 0; q < OPT; ++q) {
     const u32 k = threadIdx.x + q * B;
@@ -234,6 +235,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     f0 = 0;
   }
   if (!fits && threadIdx.x == 0) slow = 1;
+  tally.stage(tl);  // the counts are final; published after the barrier
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
     for (u32 lg = threadIdx.x; lg < ng; lg += B) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
@@ -244,6 +246,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     return;
   }
   if (threadIdx.x == 0) chunk_slow[c] = 0;
+  {
+    const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
+    BlockTally<4>::publish(tl, shard_of(shards), slot);
+  }
   // MaybeUpdate write-back over the run (coalesced), leaving max(old, acc)
   // in LDS for the CommittedIndex of every group
 #pragma unroll
@@ -289,8 +295,6 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     if (QB_CSR_FULL >= 1 ? granule_any<4 * QB_WB_GRAN>(na != 0, g) : na != 0)
       active[g] = u16(av[k] | na);
   }
-  const int slot[4] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED, QB_STAT_NON_MEMBER};
-  tally.flush(tl, shard_of(shards), slot);
 }
 
 template <int WMAX, int CAPW, bool NEXT>
