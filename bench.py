@@ -593,7 +593,7 @@ def tracker_main(args, world, rank, dev, barrier):
         parity = (f"bit-exact {Gs}/{Gs} groups (first {Gs} of the shard: match, committed, active, "
                   f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
                   else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
-    route_ms = route_impl = None
+    route_ms = route_impl = delta_ms = delta_impl = delta_changed = None
     if world > 1:
         t = torch.tensor([elapsed, step_s], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -618,6 +618,28 @@ def tracker_main(args, world, rank, dev, barrier):
         dist.all_reduce(n_in)
         if int(n_in.item()) != world * G:
             raise SystemExit(f"routing lost records: {int(n_in.item())} of {world * G}")
+        # the changed-commit delta: the node-wide commit vector
+        # kept current from the groups whose commit moved.  A real changed set:
+        # the state replayed to the last warm-up tick, then one tick with
+        # advanced_out (untimed); the exchange is timed apart, like the routing
+        adv = torch.zeros(G, dtype=torch.uint8, device=dev)
+        restore()
+        for k in range(W):
+            tr.step(batches[k], reset_stats=False, rearm=False)
+        tr.step(batches[W], advanced_out=adv, reset_stats=False, rearm=False)
+        commit_all = torch.zeros(world * G, dtype=torch.int64, device=dev)
+        delta, delta_impl = _delta(args, dev)
+        for _ in range(2):
+            delta_changed = delta(adv, tr.committed, world * G, commit_all)
+        barrier()
+        td = time.perf_counter()
+        for _ in range(5):
+            delta_changed = delta(adv, tr.committed, world * G, commit_all)
+        barrier()
+        delta_ms = (time.perf_counter() - td) / 5 * 1e3
+        b0 = rank * G
+        if not torch.equal(commit_all[b0:b0 + G][adv.bool()], tr.committed[adv.bool()]):
+            raise SystemExit("changed-commit delta gather: this shard's commits did not arrive")
     parity = _agree(parity, world, dev)
     if rank != 0:
         return parity
@@ -664,6 +686,8 @@ def tracker_main(args, world, rank, dev, barrier):
         "preroll_ms": preroll_ms, "preroll_steps": preroll_steps,
         "last_region_stats": {k: int(v) for k, v in stats.items()},
         "route_ms": route_ms, "route_impl": route_impl,
+        "allgather_changed_ms": delta_ms, "allgather_changed_impl": delta_impl,
+        "allgather_changed_groups": delta_changed,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
@@ -703,6 +727,15 @@ def _gather(args, dev):
                 "qb_dev_allgather_results (RCCL C ABI)")
     from etcd_amd.shard import allgather_results
     return allgather_results, f"etcd_amd.shard.allgather_results (torch {args.backend}, rehearsal)"
+
+
+def _delta(args, dev):
+    if args.backend == "nccl":
+        c = _comm(dev)
+        return (lambda ch, cm, total, out: c.allgather_changed(ch, cm, total, out),
+                "qb_dev_allgather_changed (RCCL C ABI)")
+    from etcd_amd.shard import allgather_changed
+    return allgather_changed, f"etcd_amd.shard.allgather_changed (torch {args.backend}, rehearsal)"
 
 
 def _agree(parity, world, dev):

@@ -95,6 +95,11 @@ SIGNATURES = {
     "qb_comm_destroy": (_i32, [_p]),
     "qb_allgather_workspace_bytes": (C.c_size_t, [_u64, _i32]),
     "qb_dev_allgather_results": (_i32, [_p, _u64, _p, _p, _p, _p, _p, C.c_size_t, _p]),
+    "qb_compact_changed_workspace_bytes": (C.c_size_t, [_u64]),
+    "qb_dev_compact_changed": (_i32, [_u64, _p, _p, _u64, _p, _p, _p, _p, C.c_size_t, _p]),
+    "qb_dev_scatter_changed": (_i32, [_u64, _p, _p, _u64, _p, _p]),
+    "qb_allgather_changed_workspace_bytes": (C.c_size_t, [_u64, _i32]),
+    "qb_dev_allgather_changed": (_i32, [_p, _u64, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_route_partition_workspace_bytes": (C.c_size_t, [_i32, _u64]),
     "qb_dev_route_partition": (_i32, [_u64, _i32, _u64] + [_p] * 13 + [C.c_size_t, _p]),
     "qb_route_workspace_bytes": (C.c_size_t, [_i32, _u64]),

@@ -79,6 +79,26 @@ class RcclComm:
                   _stream(self.device))
         return commit_all, vote_all
 
+    def allgather_changed(self, changed: torch.Tensor, commit: torch.Tensor, total: int,
+                          commit_all: torch.Tensor) -> int:
+        """Apply every rank's changed-commit delta (qb_dev_allgather_changed)
+        to ``commit_all`` (device, total u64 kept across ticks, updated in
+        place).  ``changed`` (u8) / ``commit``: this rank's shard.  Returns the
+        number of changed groups node-wide."""
+        if changed.dtype not in (torch.uint8, torch.bool) or commit.element_size() != 8 \
+                or commit_all.element_size() != 8 or commit_all.numel() != total:
+            raise ValueError("allgather_changed: changed u8, commit / commit_all 8-byte, "
+                             "commit_all of length total")
+        changed = changed.contiguous().view(torch.uint8)
+        commit = commit.contiguous()
+        need = _lib.fn("qb_allgather_changed_workspace_bytes")(total, self.world)
+        ws = self._workspace(need)
+        n = C.c_uint64(0)
+        _lib.call("qb_dev_allgather_changed", self._h, total, changed.data_ptr(), commit.data_ptr(),
+                  commit_all.data_ptr(), C.byref(n), ws.data_ptr(), ws.numel(),
+                  _stream(self.device))
+        return int(n.value)
+
     def route_records(self, cols: Dict[str, torch.Tensor], total: int,
                       out_cap: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """This rank's records after delivery (qb_dev_route_records): every

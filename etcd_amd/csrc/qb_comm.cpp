@@ -165,6 +165,96 @@ extern "C" int qb_dev_allgather_results(qb_comm* c, uint64_t total,
   return QB_OK;
 }
 
+// ------------------------------------------------------- changed deltas ---
+// qb_dev_allgather_changed: the node-wide commit vector kept current by
+// exchanging only the groups whose commit moved (at 8 GPUs the
+// full all-gather receives 7/8 of G * 9 bytes per GPU every tick).  Each rank
+// compacts its shard's changed groups (qb_delta.hip), the counts are
+// all-gathered (one host wait: the exchange size is data-dependent), every
+// rank pads its pairs to the largest count (gid UINT32_MAX) and one grouped
+// pair of ncclAllGathers moves them; the scatter applies every rank's pairs
+// (its own included) to commit_all, which the caller keeps across ticks.
+extern "C" size_t qb_allgather_changed_workspace_bytes(uint64_t total, int world) {
+  if (world < 1) return 0;
+  const uint64_t cap = shard_cap(total, world);
+  return qb_compact_changed_workspace_bytes(cap) + up256(4 * cap) + up256(8 * cap) + 256 +
+         2 * up256(sizeof(uint64_t) * size_t(world)) + up256(4 * cap * uint64_t(world)) +
+         up256(8 * cap * uint64_t(world));
+}
+
+extern "C" int qb_dev_allgather_changed(qb_comm* c, uint64_t total, const uint8_t* changed_shard,
+                                        const uint64_t* commit_shard, uint64_t* commit_all,
+                                        uint64_t* changed_total, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  QB_REQUIRE(c && changed_total, "comm / changed_total NULL");
+  QB_REQUIRE(commit_all, "commit_all NULL");
+  QB_REQUIRE(total <= 0xFFFFFFFFull, "total must fit uint32 (%llu)", (unsigned long long)total);
+  const int W = c->world;
+  QB_REQUIRE(workspace && workspace_bytes >= qb_allgather_changed_workspace_bytes(total, W),
+             "workspace too small (qb_allgather_changed_workspace_bytes)");
+  *changed_total = 0;
+  hipStream_t st = qb::as_stream(stream);
+  uint64_t b = 0, e = 0;
+  shard_range(total, W, c->rank, &b, &e);
+  const uint64_t n = e - b, cap = shard_cap(total, W);
+  QB_REQUIRE(n == 0 || (changed_shard && commit_shard), "changed_shard / commit_shard NULL");
+  char* ws = static_cast<char*>(workspace);
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    char* p = ws + o;
+    o += up256(bytes);
+    return p;
+  };
+  const size_t cws = qb_compact_changed_workspace_bytes(cap);
+  void* cw = take(cws);
+  uint32_t* gid = reinterpret_cast<uint32_t*>(take(4 * cap));
+  uint64_t* val = reinterpret_cast<uint64_t*>(take(8 * cap));
+  uint64_t* count = reinterpret_cast<uint64_t*>(take(256));
+  uint64_t* counts = reinterpret_cast<uint64_t*>(take(sizeof(uint64_t) * size_t(W)));
+  (void)take(sizeof(uint64_t) * size_t(W));
+  uint32_t* gid_all = reinterpret_cast<uint32_t*>(take(4 * cap * uint64_t(W)));
+  uint64_t* val_all = reinterpret_cast<uint64_t*>(take(8 * cap * uint64_t(W)));
+  // a local failure travels as count ~0 in the gathered counts, so every rank
+  // returns together instead of some waiting in the exchange
+  const int rc = qb_dev_compact_changed(n, changed_shard, commit_shard, b, gid, val, count, cw,
+                                        cws, stream);
+  std::string local_err = rc == QB_OK ? std::string() : std::string(qb_last_error());
+  if (rc != QB_OK) {
+    const hipError_t me = hipMemsetAsync(count, 0xFF, sizeof(uint64_t), st);
+    if (me != hipSuccess) return qb::hip_fail(me, "hipMemsetAsync(count)");
+  }
+  QB_NCCL(ncclAllGather(count, counts, 1, ncclUint64, c->nccl, st), "ncclAllGather(counts)");
+  std::vector<uint64_t> h(static_cast<size_t>(W));
+  hipError_t he = hipMemcpyAsync(h.data(), counts, sizeof(uint64_t) * h.size(),
+                                 hipMemcpyDeviceToHost, st);
+  if (he == hipSuccess) he = hipStreamSynchronize(st);
+  if (he != hipSuccess) return qb::hip_fail(he, "changed counts to host");
+  if (rc != QB_OK) {
+    qb::set_error("%s", local_err.c_str());
+    return rc;
+  }
+  uint64_t mx = 0, sum = 0;
+  for (int r = 0; r < W; ++r) {
+    const uint64_t x = h[size_t(r)];
+    QB_REQUIRE(x != ~0ull, "rank %d failed before the exchange (its qb_last_error has the reason)", r);
+    mx = x > mx ? x : mx;
+    sum += x;
+  }
+  *changed_total = sum;
+  if (mx == 0) return QB_OK;
+  // this rank's pairs padded to the largest count (gid UINT32_MAX: skipped)
+  const uint64_t mine = h[size_t(c->rank)];
+  if (mine < mx) {
+    he = hipMemsetAsync(gid + mine, 0xFF, 4 * (mx - mine), st);
+    if (he != hipSuccess) return qb::hip_fail(he, "hipMemsetAsync(pad)");
+  }
+  QB_NCCL(ncclGroupStart(), "ncclGroupStart");
+  QB_NCCL(ncclAllGather(gid, gid_all, mx, ncclUint32, c->nccl, st), "ncclAllGather(gid)");
+  QB_NCCL(ncclAllGather(val, val_all, mx, ncclUint64, c->nccl, st), "ncclAllGather(commit)");
+  QB_NCCL(ncclGroupEnd(), "ncclGroupEnd");
+  return qb_dev_scatter_changed(mx * uint64_t(W), gid_all, val_all, total, commit_all, stream);
+}
+
 // ------------------------------------------------------------- routing ---
 // qb_dev_route_records: the stable partition (qb_route.hip), the per-rank
 // counts all-gathered (with every rank's output capacity, so all ranks take

@@ -181,3 +181,79 @@ def route_partition(cols: Dict[str, torch.Tensor], total: int, world: int):
         off.data_ptr(), ws.data_ptr(), nbytes, stream), "qb_dev_route_partition")
     o = off.cpu().tolist()
     return send, [o[r + 1] - o[r] for r in range(world)]
+
+
+def compact_changed(changed: torch.Tensor, commit: torch.Tensor, g_base: int = 0):
+    """The changed-commit delta of a shard: (global group u32 as int32, new
+    commit) of the groups whose ``changed`` flag (u8) is set, in group order —
+    a group surfaces a Ready when its commit moved (raft/node.go:573,
+    raft/rawnode.go:157).  Device tensors run qb_dev_compact_changed (HIP);
+    host tensors the same compaction in torch."""
+    if changed.numel() != commit.numel():
+        raise ValueError("changed and commit differ in length")
+    if changed.dtype not in (torch.uint8, torch.bool):
+        raise ValueError(f"changed must be uint8/bool, not {changed.dtype}")
+    if commit.dtype not in _WIDE:
+        raise ValueError(f"commit must be int64/uint64, not {commit.dtype}")
+    if g_base + commit.numel() > 0xFFFFFFFF:
+        raise ValueError("global groups must fit uint32")
+    changed = changed.contiguous().view(torch.uint8)
+    commit = commit.contiguous()
+    if commit.device.type != "cuda":
+        idx = torch.nonzero(changed, as_tuple=True)[0]
+        return (idx + g_base).to(torch.int32), commit[idx]
+    from etcd_amd import _lib
+    lib = _lib.load()
+    n = commit.numel()
+    dev = commit.device
+    gid = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(n, 1), dtype=commit.dtype, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    nbytes = lib.qb_compact_changed_workspace_bytes(n)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    _lib.check(lib.qb_dev_compact_changed(n, changed.data_ptr(), commit.data_ptr(), g_base,
+                                          gid.data_ptr(), val.data_ptr(), cnt.data_ptr(),
+                                          ws.data_ptr(), nbytes,
+                                          torch.cuda.current_stream(dev).cuda_stream),
+               "qb_dev_compact_changed")
+    k = int(cnt.item())
+    return gid[:k], val[:k]
+
+
+def allgather_changed(changed: torch.Tensor, commit: torch.Tensor, total: int,
+                      commit_all: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> int:
+    """Apply every rank's changed-commit delta to ``commit_all`` (the
+    node-wide vector the caller keeps across ticks; updated in place) — 12
+    bytes per changed group exchanged instead of allgather_results' whole
+    vectors.  ``changed`` / ``commit``: this rank's shard.
+    Returns the number of changed groups node-wide.  One count exchange, then
+    one padded all-gather per column (padding gid = -1, i.e. UINT32_MAX)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    b, e = shard_range(total, world, rank)
+    if commit.numel() != e - b or changed.numel() != e - b:
+        raise ValueError("local vectors do not match this rank's shard")
+    if commit_all.numel() != total:
+        raise ValueError("commit_all must hold every group")
+    gid, val = compact_changed(changed, commit, b)
+    dev = commit.device
+    n = torch.tensor([gid.numel()], dtype=torch.int64, device=dev)
+    counts = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    mx = max(counts)
+    if mx == 0:
+        return 0
+    pg = torch.full((mx,), -1, dtype=torch.int32, device=dev)
+    pv = torch.zeros(mx, dtype=val.dtype, device=dev)
+    pg[: gid.numel()] = gid
+    pv[: val.numel()] = val
+    lg = [torch.empty_like(pg) for _ in range(world)]
+    lv = [torch.empty_like(pv) for _ in range(world)]
+    dist.all_gather(lg, pg, group=group)
+    dist.all_gather(lv, pv, group=group)
+    g_all, v_all = torch.cat(lg), torch.cat(lv)
+    keep = g_all != -1
+    idx = g_all[keep].to(torch.int64) & 0xFFFFFFFF
+    commit_all[idx] = v_all[keep].to(commit_all.dtype)
+    return sum(counts)

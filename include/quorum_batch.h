@@ -746,6 +746,36 @@ int qb_dev_allgather_results(qb_comm* comm, uint64_t total,
                              uint64_t* commit_all, uint8_t* vote_all,
                              void* workspace, size_t workspace_bytes, void* stream);
 
+/* The changed-commit delta (gather only the groups whose
+ * commit moved).  A group surfaces a Ready when its HardState changed
+ * (raft/node.go:573 newReady, raft/rawnode.go:157 HasReady); in a tick that
+ * is the groups whose maybeCommit advanced (raft.go:585-588) — the tracker
+ * steps' advanced_out.  Device half: the n groups' changed flags (u8, nonzero
+ * = changed) compacted in group order into (g_base + g, commit[g]) pairs;
+ * *out_count (device u64) = pairs written (global groups must fit uint32). */
+size_t qb_compact_changed_workspace_bytes(uint64_t n);
+int qb_dev_compact_changed(uint64_t n, const uint8_t* changed, const uint64_t* commit,
+                           uint64_t g_base, uint32_t* out_gid, uint64_t* out_commit,
+                           uint64_t* out_count, void* workspace, size_t workspace_bytes,
+                           void* stream);
+/* commit_all[gid[i]] = commit[i] for i < m (gid UINT32_MAX or >= total:
+ * skipped, the padding of the exchange below). */
+int qb_dev_scatter_changed(uint64_t m, const uint32_t* gid, const uint64_t* commit, uint64_t total,
+                           uint64_t* commit_all, void* stream);
+size_t qb_allgather_changed_workspace_bytes(uint64_t total, int world);
+/* Collective over the comm: this rank's shard's changed groups (changed_shard
+ * / commit_shard: the shard's local arrays, qb_shard_range) are exchanged and
+ * applied to commit_all[total] (device) on every rank — the caller keeps
+ * commit_all across ticks; a tick moves 12 bytes per changed group instead of
+ * qb_dev_allgather_results' 8 per group.  *changed_total (host) = changed
+ * groups node-wide.  The host waits on the stream once (the exchange size is
+ * data-dependent); a rank's local failure reaches every rank through the
+ * gathered counts, so all return QB_EINVAL together. */
+int qb_dev_allgather_changed(qb_comm* comm, uint64_t total, const uint8_t* changed_shard,
+                             const uint64_t* commit_shard, uint64_t* commit_all,
+                             uint64_t* changed_total, void* workspace, size_t workspace_bytes,
+                             void* stream);
+
 /* Record delivery to the owning shards ("message batches are
  * bucketed by owning shard").  A node's inbound responses arrive at any rank;
  * each record goes to the rank owning its global group, with the group

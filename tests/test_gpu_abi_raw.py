@@ -282,6 +282,69 @@ def test_comm_allgather_world1_raw_abi():
     s.close()
 
 
+@pytest.mark.parametrize("n,frac,base", [(1, 1.0, 0), (4095, 0.5, 7), (1 << 20, 0.01, 123),
+                                          (1000003, 1.0, 0), (5000, 0.0, 9)])
+def test_compact_and_scatter_changed_raw_abi(n, frac, base):
+    """qb_dev_compact_changed: the changed groups in group order as (g_base +
+    g, commit) pairs and the device count; qb_dev_scatter_changed applies them
+    (padding gid UINT32_MAX skipped)."""
+    s = Stream()
+    lib = s.lib
+    rng = np.random.default_rng(n)
+    changed = (rng.random(n) < frac).astype(np.uint8) * rng.integers(1, 256, n).astype(np.uint8)
+    commit = rng.integers(0, 1 << 63, n, dtype=np.int64).astype(np.uint64) | np.uint64(1 << 63)
+    d_ch, d_c = s.up(changed), s.up(commit)
+    gid, val, cnt = s.zeros(4 * n + 8), s.zeros(8 * n + 8), s.zeros(8)
+    need = lib.qb_compact_changed_workspace_bytes(n)
+    ws = s.zeros(need)
+    _lib.check(lib.qb_dev_compact_changed(n, d_ch, d_c, base, gid, val, cnt, ws, need, s.st),
+               "compact")
+    idx = np.nonzero(changed)[0]
+    k = int(s.down(cnt, np.empty(1, np.uint64))[0])
+    assert k == idx.size
+    assert np.array_equal(s.down(gid, np.empty(n + 2, np.uint32))[:k], (idx + base).astype(np.uint32))
+    assert np.array_equal(s.down(val, np.empty(n + 1, np.uint64))[:k], commit[idx])
+    total = n + base
+    out = s.up(np.zeros(total, np.uint64))
+    pad = s.up(np.full(3, 0xFFFFFFFF, np.uint32))
+    _lib.check(lib.qb_dev_scatter_changed(k, gid, val, total, out, s.st), "scatter")
+    _lib.check(lib.qb_dev_scatter_changed(3, pad, val, total, out, s.st), "scatter padding")
+    want = np.zeros(total, np.uint64)
+    want[idx + base] = commit[idx]
+    assert np.array_equal(s.down(out, np.empty(total, np.uint64)), want)
+    s.close()
+
+
+def test_allgather_changed_world1_raw_abi():
+    """qb_dev_allgather_changed on a single-rank communicator over three ticks:
+    commit_all carries every changed group's commit, *changed_total counts
+    them, a tick with nothing changed moves nothing."""
+    s = Stream()
+    lib = s.lib
+    uid = (C.c_char * 128)()
+    _lib.check(lib.qb_comm_get_unique_id(uid), "unique id")
+    comm = C.c_void_p()
+    _lib.check(lib.qb_comm_init(C.byref(comm), 1, 0, uid), "comm init")
+    G = 300007
+    need = lib.qb_allgather_changed_workspace_bytes(G, 1)
+    ws = s.zeros(need)
+    d_all = s.up(np.zeros(G, np.uint64))
+    want = np.zeros(G, np.uint64)
+    rng = np.random.default_rng(5)
+    for frac in (0.2, 0.0, 1.0):
+        changed = (rng.random(G) < frac).astype(np.uint8)
+        commit = rng.integers(0, 1 << 62, G, dtype=np.int64).astype(np.uint64)
+        d_ch, d_c = s.up(changed), s.up(commit)
+        n = C.c_uint64(99)
+        _lib.check(lib.qb_dev_allgather_changed(comm, G, d_ch, d_c, d_all, C.byref(n), ws, need,
+                                                s.st), "allgather changed")
+        want = np.where(changed != 0, commit, want)
+        assert n.value == int(changed.sum())
+        assert np.array_equal(s.down(d_all, np.empty(G, np.uint64)), want)
+    _lib.check(lib.qb_comm_destroy(comm), "comm destroy")
+    s.close()
+
+
 def _route_ref(total, world, grp, cols):
     """Stable partition by owner (shard_range) with rebased groups: the order
     etcd_amd/shard.py:route_records defines."""

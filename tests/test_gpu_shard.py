@@ -221,6 +221,7 @@ def _rccl_comm_world1_worker(rank, world, port, q, total):
         grp = batch.FixedGroups.synth(SEED, 5, total, device=dev)
         c, v = grp.committed_vote()
         gc, gv = comm.allgather_results(c, v, total)      # qb_dev_allgather_results
+        ok_c = bool(torch.equal(gc, c))
         M = 10_000
         gen = torch.Generator(device=dev)
         gen.manual_seed(3)
@@ -233,8 +234,15 @@ def _rccl_comm_world1_worker(rank, world, port, q, total):
         same = all(torch.equal(got[k].to(torch.int64), (cols[k] & 0xFFFFFFFF if k == "group"
                                                          else cols[k]).to(torch.int64))
                    for k in cols)
+        # qb_dev_allgather_changed: the changed groups' commits land in the
+        # node-wide vector (gc, from the full all-gather above)
+        changed = (torch.arange(total, device=dev) % 7 == 3).to(torch.uint8)
+        newc = c + 1000
+        n = comm.allgather_changed(changed, newc, total, gc)
+        torch.cuda.synchronize()
+        delta_ok = n == int(changed.sum()) and bool(torch.equal(gc, torch.where(changed.bool(), newc, c)))
         comm.close()
-        q.put((bool(torch.equal(gc, c)), bool(torch.equal(gv, v)), same, comm.world))
+        q.put((ok_c, bool(torch.equal(gv, v)), same, delta_ok, comm.world))
     finally:
         dist.destroy_process_group()
 
@@ -243,7 +251,8 @@ def _rccl_comm_world1_worker(rank, world, port, q, total):
 def test_rccl_comm_c_abi_world1():
     """etcd_amd.comm.RcclComm — the C ABI's communicator, what bench.py's N > 1
     path times — on a single-rank group: unique id over torch.distributed,
-    qb_comm_init, the all-gather and the record routing (every record stays,
-    in order, an int64 group column converted) against the inputs."""
-    ok_c, ok_v, ok_r, w = _spawn(_rccl_comm_world1_worker, 1, 50_000)
-    assert ok_c and ok_v and ok_r and w == 1
+    qb_comm_init, the all-gather, the record routing (every record stays,
+    in order, an int64 group column converted) and the changed-commit delta
+    gather against the inputs."""
+    ok_c, ok_v, ok_r, ok_d, w = _spawn(_rccl_comm_world1_worker, 1, 50_000)
+    assert ok_c and ok_v and ok_r and ok_d and w == 1

@@ -131,3 +131,66 @@ def test_route_records_by_owning_shard(world):
         assert np.array_equal(got[r][0], np.concatenate(want_g).astype(np.uint32))
         assert np.array_equal(got[r][1], np.concatenate(want_i))
         assert np.array_equal(got[r][2], np.concatenate(want_f))
+
+
+def _delta_inputs(total, tick, frac):
+    """A tick's node-wide changed flags and new commits (the same on every
+    rank: each takes its shard)."""
+    rng = np.random.default_rng(77 + tick)
+    changed = (rng.random(total) < frac).astype(np.uint8)
+    commit = rng.integers(0, 1 << 63, total, dtype=np.int64).astype(np.uint64)
+    commit[:3] = [0, (1 << 64) - 1, 1 << 63]  # the full u64 range travels
+    return changed, commit
+
+
+def _delta_worker(rank, world, port, total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.shard import allgather_changed
+        b, e = shard_range(total, world, rank)
+        commit_all = torch.zeros(total, dtype=torch.int64)
+        seen = []
+        for tick, frac in enumerate((0.3, 0.0, 0.01, 1.0)):
+            changed, commit = _delta_inputs(total, tick, frac)
+            n = allgather_changed(torch.from_numpy(changed[b:e]),
+                                  torch.from_numpy(commit[b:e].view(np.int64)), total, commit_all)
+            seen.append((n, commit_all.numpy().view(np.uint64).copy()))
+        q.put((rank, seen))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 1001), (3, 5000)])
+def test_allgather_changed_keeps_node_wide_commits(world, total):
+    """shard.allgather_changed over gloo: after every tick each rank's
+    node-wide vector equals applying every changed group's new commit (ticks
+    with 30 %, 0 %, 1 % and 100 % of the groups changed, uneven shards)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_delta_worker, args=(r, world, port, total, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = np.zeros(total, np.uint64)
+    for tick, frac in enumerate((0.3, 0.0, 0.01, 1.0)):
+        changed, commit = _delta_inputs(total, tick, frac)
+        want = np.where(changed != 0, commit, want)
+        for r in range(world):
+            n, vec = got[r][tick]
+            assert n == int(changed.sum())
+            assert np.array_equal(vec, want)
+
+
+def test_compact_changed_host():
+    from etcd_amd.shard import compact_changed
+    changed, commit = _delta_inputs(777, 0, 0.2)
+    gid, val = compact_changed(torch.from_numpy(changed), torch.from_numpy(commit.view(np.int64)), 40)
+    idx = np.nonzero(changed)[0]
+    assert np.array_equal(gid.numpy().astype(np.int64), idx + 40)
+    assert np.array_equal(val.numpy().view(np.uint64), commit[idx])
