@@ -642,7 +642,7 @@ def tracker_main(args, world, rank, dev, barrier):
             raise SystemExit("changed-commit delta gather: this shard's commits did not arrive")
     parity = _agree(parity, world, dev)
     if rank != 0:
-        return parity
+        return parity, None
     bpg = TRACKER_BYTES
     if csr:
         # record 21 + match RMW 16 + commit advance: off 4, cfg 4, the voters'
@@ -691,8 +691,7 @@ def tracker_main(args, world, rank, dev, barrier):
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
-    print(json.dumps(out), flush=True)
-    return parity
+    return parity, out
 
 
 # ------------------------------------------------------ multi-GPU helpers ---
@@ -1046,8 +1045,14 @@ def eval_main(args, world, rank, dev, barrier):
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_eval(args.workload, n, args.cpu_seconds)
-        print(json.dumps(out), flush=True)
-    return parity
+        return parity, out
+    return parity, None
+
+
+def run_other(args, world, rank, dev, barrier):
+    """One secondary workload of the default run (its parity, its JSON dict)."""
+    run = tracker_main if args.workload.startswith("tracker") else eval_main
+    return run(args, world, rank, dev, barrier)
 
 
 def parse_args(argv=None):
@@ -1080,6 +1085,8 @@ def parse_args(argv=None):
                     help="CPU baseline budget (split over its legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the post-region oracle check")
+    ap.add_argument("--no-others", action="store_true",
+                    help="the default (configs[1], N = 1) run skips the other BASELINE configs")
     ap.add_argument("--parity-groups", type=int, default=1 << 20,
                     help="tracker workloads: groups of the shard checked against the oracle")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
@@ -1123,15 +1130,36 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if args.workload.startswith("tracker"):
-        parity = tracker_main(args, world, rank, dev, barrier)
-    else:
-        parity = eval_main(args, world, rank, dev, barrier)
+    run = tracker_main if args.workload.startswith("tracker") else eval_main
+    parity, out = run(args, world, rank, dev, barrier)
+    bad = parity is not None and "MISMATCH" in parity
+    if out is not None and world == 1 and args.workload == "fixed" and not args.no_others:
+        # the other BASELINE configs, measured by the same command (so the
+        # driver's own run backs them): configs[2] ragged, configs[3] joint,
+        # configs[4] streaming tracker (fixed and ragged CSR groups) — each at
+        # its full per-GPU size with its own warm-up, K = 20 and parity check
+        out["other_configs"] = {}
+        for wl in ("ragged", "joint", "tracker", "tracker-csr"):
+            sub = argparse.Namespace(**vars(args))
+            sub.workload, sub.steps, sub.warmup, sub.no_cpu_baseline = wl, 20, None, True
+            sub.preroll_ms, sub.settle_ms = min(args.preroll_ms, 200.0), min(args.settle_ms, 1000.0)
+            p2, o2 = run_other(sub, world, rank, dev, barrier)
+            bad |= p2 is not None and "MISMATCH" in p2
+            r = o2["roofline"]
+            out["other_configs"][wl] = {
+                "workload": o2["config"]["workload"], "value": o2["value"], "unit": o2["unit"],
+                "steps": o2["steps"], "warmup": o2["warmup"], "ms_per_step": o2["ms_per_step"],
+                "roofline": {k: r[k] for k in ("achieved", "frac", "traffic", "bytes_per_group",
+                                               "avg_kernel_us", "kernel")},
+                "parity": p2}
+            torch.cuda.empty_cache()
+    if out is not None:
+        print(json.dumps(out), flush=True)
     for c in _COMM:
         c.close()
     if world > 1:
         dist.destroy_process_group()
-    if parity is not None and "MISMATCH" in parity:
+    if bad:
         sys.exit(3)
 
 
