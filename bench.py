@@ -291,6 +291,22 @@ def cpu_baseline_eval(workload: str, n: int, seconds: float):
     for name, f in (("faithful", faithful), ("soa", soa)):
         for th in (1, N):
             legs[f"{name}_{th}t"] = _rate(lambda: f(th), gs, seconds / 4)[0]
+    plumbing = None
+    if workload == "fixed":
+        # configs[0]: BenchmarkMajorityConfig_CommittedIndex (quorum/bench_test.go:
+        # 24-40) — one n-voter config called in a loop, ns/op, faithful C
+        # restatement on 1 thread (the device's ns per group is the line's
+        # avg_kernel_us / groups)
+        iters, lib = 1 << 20, oc.load()
+        while True:
+            t0 = time.perf_counter()
+            lib.orc_bench_plumbing(n, iters, 0x5EED0001)
+            dt = time.perf_counter() - t0
+            if dt >= 0.5:
+                break
+            iters *= 4
+        plumbing = {"voters": n, "cpu_ns_per_op": dt / iters * 1e9,
+                    "reference": "raft/quorum/bench_test.go:24-40 (BASELINE configs[0])"}
     return {
         "value": legs[f"faithful_{N}t"], "unit": "groups/s", "cores": N, "kind": "port",
         "threads": N, "gomaxprocs_equivalent": N, "host": info, "legs": legs,
@@ -300,6 +316,7 @@ def cpu_baseline_eval(workload: str, n: int, seconds: float):
                    f"{info['affinity_cpus']} logical CPUs, cgroup quota {info['cgroup_cpu_quota']}; "
                    f"GOMAXPROCS-equivalent {N}); legs: faithful and SoA restatements at 1 and {N} "
                    f"threads"),
+        **({"configs0_plumbing": plumbing} if plumbing else {}),
     }
 
 
@@ -1049,6 +1066,40 @@ def eval_main(args, world, rank, dev, barrier):
     return parity, None
 
 
+def next_rows():
+    """SURVEY §8f rows and configs[0] (tools/bench_configs.py, GPU side only:
+    one device time per row) for the default run's line: the leader inbox
+    step (4M groups), ReadIndex acks (4M leaders), wire ingest (16M messages,
+    group-row table), a conf change over 8M groups, and the configs[0]
+    plumbing (the faithful C restatement's ns/op beside the device's ns per
+    group).  Their parity is the GPU suite's (tests/test_gpu_leader.py,
+    test_gpu_wire.py, test_gpu_confchange.py: bit-exact vs the oracles)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import bench_configs as bc
+    rows = []
+
+    def report(name, groups, t, algo_bytes, extra=None):
+        d = {"config": name, "per_launch_us": t * 1e6, "units_per_s": groups / t,
+             "algo_bytes_per_unit": algo_bytes / groups, "achieved_GBs": algo_bytes / t / 1e9,
+             "frac": algo_bytes / t / 1e9 / HBM_PEAK_GBS}
+        d.update({k: v for k, v in (extra or {}).items() if k != "cpu_baseline"})
+        rows.append(d)
+    orig, bc.report, bc.GPU_ONLY = bc.report, report, True
+    try:
+        for name, fn in (("leader", lambda: bc.leader_config(1 << 22, 20)),
+                         ("readindex", lambda: bc.readindex_config(1 << 22, 20)),
+                         ("wire", lambda: bc.wire_config(1 << 24, 20, rows=True)),
+                         ("confchange", lambda: bc.confchange_config(1 << 23, 20))):
+            try:
+                fn()
+            except Exception as ex:  # reported; the headline stands
+                rows.append({"config": name, "error": f"{type(ex).__name__}: {ex}"})
+            torch.cuda.empty_cache()
+    finally:
+        bc.report = orig
+    return rows
+
+
 def run_other(args, world, rank, dev, barrier):
     """One secondary workload of the default run (its parity, its JSON dict)."""
     run = tracker_main if args.workload.startswith("tracker") else eval_main
@@ -1143,7 +1194,13 @@ def main():
             sub = argparse.Namespace(**vars(args))
             sub.workload, sub.steps, sub.warmup, sub.no_cpu_baseline = wl, 20, None, True
             sub.preroll_ms, sub.settle_ms = min(args.preroll_ms, 200.0), min(args.settle_ms, 1000.0)
-            p2, o2 = run_other(sub, world, rank, dev, barrier)
+            try:
+                p2, o2 = run_other(sub, world, rank, dev, barrier)
+            except Exception as ex:  # reported in the line; the headline stands
+                out["other_configs"][wl] = {"error": f"{type(ex).__name__}: {ex}"}
+                bad = True
+                torch.cuda.empty_cache()
+                continue
             bad |= p2 is not None and "MISMATCH" in p2
             r = o2["roofline"]
             out["other_configs"][wl] = {
@@ -1153,6 +1210,7 @@ def main():
                                                "avg_kernel_us", "kernel")},
                 "parity": p2}
             torch.cuda.empty_cache()
+        out["next_rows"] = next_rows()
     if out is not None:
         print(json.dumps(out), flush=True)
     for c in _COMM:

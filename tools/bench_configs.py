@@ -272,9 +272,8 @@ def leader_config(G, reps, warm=4, shuffle=True):
     # copied, written) per message; scans 16 B per group.
     algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
     if not shuffle or GPU_ONLY:
-        print(json.dumps({"config": "leader inbox step" + ("" if shuffle else
-                          ", records in group order (lab)"),
-                          "per_launch_us": t * 1e6, "groups_per_s": G / t}), flush=True)
+        report("leader inbox step" + ("" if shuffle else ", records in group order (lab)"), G, t,
+               algo, {"unit": "group-steps/s", "msgs_per_step": msgs})
         return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
     # stepLeader loop one record at a time) on a bounded sample of the same
@@ -334,9 +333,8 @@ def wire_config(M, reps, G=None, rows=False):
     # 1, index/term/hint/log_term 32, status 1, type 1
     algo = nb + M * (8 + 4 + 40) + M * (4 + 1 + 32 + 1 + 1)
     if GPU_ONLY:
-        print(json.dumps({"config": "wire ingest" + (" (group rows)" if rows else ""),
-                          "per_launch_us": t * 1e6,
-                          "messages_per_s": M / t, "frac": algo / t / 8e12}), flush=True)
+        report("wire ingest" + (" (group rows)" if rows else ""), M, t, algo,
+               {"unit": "messages/s", "bytes_per_message": nb / M})
         return
     import time
     Ms = 1 << 22
@@ -393,8 +391,7 @@ def confchange_config(G, reps):
     pr = 29 + 8 * K
     algo = G * (4 + 40 + 8 + 1 + 4 + 9 + 8 + 5 * pr + 4 + 48 + 8 + 6 * pr + 9)
     if GPU_ONLY:
-        print(json.dumps({"config": "conf change", "per_launch_us": tt * 1e6,
-                          "groups_per_s": G / tt, "frac": algo / tt / 8e12}), flush=True)
+        report("conf change", G, tt, algo, {"unit": "groups/s"})
         return
     n = 20000
     trs = []
