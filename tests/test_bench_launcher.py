@@ -92,3 +92,22 @@ def test_route_columns_normalised_or_refused():
                                "index": idx, "term": idx})
     with pytest.raises(ValueError, match="required"):
         shard._device_columns({"group": g64, "flags": torch.zeros(M, dtype=torch.uint8)})
+
+
+def test_default_run_secondary_configs_wiring():
+    """The default (configs[1], N = 1) run also measures configs[2]-[4] and
+    the §8f rows: the flags and the bench_configs entry points next_rows()
+    calls exist with the arguments it passes (the GPU side runs on the box)."""
+    import inspect
+    a = bench.parse_args([])
+    assert a.workload == "fixed" and not a.no_others
+    assert bench.parse_args(["--no-others"]).no_others
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs as bc
+    for name, nargs in (("leader_config", 2), ("readindex_config", 2), ("wire_config", 2),
+                        ("confchange_config", 2)):
+        sig = inspect.signature(getattr(bc, name))
+        required = [p for p in sig.parameters.values() if p.default is inspect.Parameter.empty]
+        assert len(required) == nargs, name
+    assert "rows" in inspect.signature(bc.wire_config).parameters
+    assert callable(bench.next_rows) and callable(bench.run_other)
