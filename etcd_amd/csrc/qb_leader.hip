@@ -992,6 +992,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
   const u32 s0 = live ? A.lg.off[g] : 0u, s1 = live ? A.lg.off[g + 1] : 0u;
   const u32 sb = A.lg.off[g0], span = A.lg.off[gend] - sb;
   const bool staged = span <= kSpanCap;  // workgroup-uniform
+  if (threadIdx.x < 7) lds[threadIdx.x] = 0;  // the stat tally (staged below)
   const bool busy = __syncthreads_or(r1 > r0);
   if (!busy) {
     // No records for any group of the workgroup: only the outputs.
@@ -1025,18 +1026,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
     if (A.stepdown_at) A.stepdown_at[g] = stepdown;
     if (A.gflags) A.gflags[g] = gfl;
   }
-  if (staged) {
-    __syncthreads();
-    for (u32 j = threadIdx.x; j < span; j += kBlock) {
-      const u8 dm = ss.dirty[j];
-      if (!dm) continue;
-      if (dm & kDirtyMatch) U(A.lg.match)[sb + j] = ss.match[j];
-      if (dm & kDirtyNext) U(A.lg.next)[sb + j] = ss.next[j];
-      if (dm & kDirtyIpos) A.lg.infl_pos[sb + j] = ss.ipos[j];
-      if (dm & kDirtySt) A.lg.pstate[sb + j] = ss.st[j];
-    }
-  }
-  // Per-wave sums of per-thread counts, then one flush per block.
+  // Per-wave sums of per-thread counts, staged into LDS before the barrier
+  // the write-back needs anyway and published after it (a flush with two
+  // barriers of its own at the end of the workgroup, as the tracker's K5 had)
   auto wsum = [](u32 v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
@@ -1048,10 +1040,24 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
   tally.t[4] += wsum(n.after);
   tally.t[5] += wsum(n.msgs);
   tally.t[6] += wsum(n.msgs - n.stored);
-  const int slot[7] = {QB_LSTAT_APPLIED, QB_LSTAT_STALE_TERM, QB_LSTAT_HIGHER_TERM,
-                       QB_LSTAT_NON_MEMBER, QB_LSTAT_AFTER_STEPDOWN, QB_LSTAT_MSGS,
-                       QB_LSTAT_MSGS_DROPPED};
-  tally.flush(lds, A.shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+  tally.stage(lds);
+  __syncthreads();
+  {
+    const int slot[7] = {QB_LSTAT_APPLIED, QB_LSTAT_STALE_TERM, QB_LSTAT_HIGHER_TERM,
+                         QB_LSTAT_NON_MEMBER, QB_LSTAT_AFTER_STEPDOWN, QB_LSTAT_MSGS,
+                         QB_LSTAT_MSGS_DROPPED};
+    BlockTally<7>::publish(lds, A.shards + u64(blockIdx.x % 64) * QB_LSTAT_COUNT, slot);
+  }
+  if (staged) {
+    for (u32 j = threadIdx.x; j < span; j += kBlock) {
+      const u8 dm = ss.dirty[j];
+      if (!dm) continue;
+      if (dm & kDirtyMatch) U(A.lg.match)[sb + j] = ss.match[j];
+      if (dm & kDirtyNext) U(A.lg.next)[sb + j] = ss.next[j];
+      if (dm & kDirtyIpos) A.lg.infl_pos[sb + j] = ss.ipos[j];
+      if (dm & kDirtySt) A.lg.pstate[sb + j] = ss.st[j];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ L6 ----
