@@ -751,8 +751,9 @@ int qb_dev_allgather_results(qb_comm* comm, uint64_t total,
  * (raft/node.go:573 newReady, raft/rawnode.go:157 HasReady); in a tick that
  * is the groups whose maybeCommit advanced (raft.go:585-588) — the tracker
  * steps' advanced_out.  Device half: the n groups' changed flags (u8, nonzero
- * = changed) compacted in group order into (g_base + g, commit[g]) pairs;
- * *out_count (device u64) = pairs written (global groups must fit uint32). */
+ * = changed) compacted in group order into (g_base + g, commit[g]) pairs in
+ * out_gid / out_commit (room for n each); *out_count (device u64) = pairs
+ * written (global groups must fit uint32). */
 size_t qb_compact_changed_workspace_bytes(uint64_t n);
 int qb_dev_compact_changed(uint64_t n, const uint8_t* changed, const uint64_t* commit,
                            uint64_t g_base, uint32_t* out_gid, uint64_t* out_commit,
@@ -769,8 +770,11 @@ size_t qb_allgather_changed_workspace_bytes(uint64_t total, int world);
  * commit_all across ticks; a tick moves 12 bytes per changed group instead of
  * qb_dev_allgather_results' 8 per group.  *changed_total (host) = changed
  * groups node-wide.  The host waits on the stream once (the exchange size is
- * data-dependent); a rank's local failure reaches every rank through the
- * gathered counts, so all return QB_EINVAL together. */
+ * data-dependent); a rank's local failure in the compaction reaches every
+ * rank through the gathered counts, so all return QB_EINVAL together.  Every
+ * rank must pass the same total and a large enough workspace: a rank failing
+ * those checks returns before the count all-gather and leaves the others
+ * waiting in it (as qb_dev_route_records). */
 int qb_dev_allgather_changed(qb_comm* comm, uint64_t total, const uint8_t* changed_shard,
                              const uint64_t* commit_shard, uint64_t* commit_all,
                              uint64_t* changed_total, void* workspace, size_t workspace_bytes,
