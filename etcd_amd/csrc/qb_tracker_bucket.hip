@@ -572,6 +572,60 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   }
 }
 
+// K4 for compact records (the tracker steps) in its own kernel: only the
+// staged records and the chunk counters in LDS (33 KB instead of the shared
+// tile's 61 KB) and 512 threads of 8 records, so four parts run per CU
+// instead of two (QB_K4C = 0: the shared kernel above).
+#ifndef QB_K4C
+#define QB_K4C 1
+#endif
+constexpr int kSplitThreads = 512;
+constexpr int kSplitPer = kTile / kSplitThreads;
+__global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
+    Geometry geo, const u32* __restrict__ offsets, const u32* __restrict__ bsum,
+    const u32* __restrict__ pt, Cols in, Cols out, u32* __restrict__ cs) {
+  const u32* pfirst = pt;
+  const u32* part_sb = pt + geo.NSB + 2;
+  const u32 p = blockIdx.x;
+  if (p >= pfirst[geo.NSB]) return;  // fewer parts than the launch bound
+  __shared__ u64 stage[kTile];
+  __shared__ u32 start[kChunksPerSb];
+  __shared__ u32 wsum[kSplitThreads / 64];
+  const u32 sb = part_sb[p];
+  const u32 sb_lo = off_at(offsets, bsum, geo.nbins(), u64(sb) * geo.NT);
+  const u32 sb_hi = off_at(offsets, bsum, geo.nbins(), u64(sb + 1) * geo.NT);
+  const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
+  const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
+  const u32 nrec = hi - lo;
+  u64 vm[kSplitPer];  // loaded together: one round trip
+  u32 vc[kSplitPer];
+#pragma unroll
+  for (int j = 0; j < kSplitPer; ++j) {
+    const u32 k = threadIdx.x + j * kSplitThreads;
+    vm[j] = k < nrec ? in.mr[lo + k] : 0ull;
+    vc[j] = k < nrec ? u32(in.cl[lo + k]) : 0u;
+  }
+  if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
+  __syncthreads();
+  u32 rk[kSplitPer];
+#pragma unroll
+  for (int j = 0; j < kSplitPer; ++j) {
+    const u32 k = threadIdx.x + j * kSplitThreads;
+    rk[j] = k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u;
+  }
+  __syncthreads();
+  tile_scan_bins(start, kChunksPerSb, wsum);
+  if (threadIdx.x <= kChunksPerSb)
+    cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
+        lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
+#pragma unroll
+  for (int j = 0; j < kSplitPer; ++j) {
+    const u32 k = threadIdx.x + j * kSplitThreads;
+    if (k < nrec) stage[start[vc[j]] + rk[j]] = vm[j];
+  }
+  __syncthreads();
+  for (u32 e = threadIdx.x; e < nrec; e += kSplitThreads) out.mr[lo + e] = stage[e];
+}
 
 // ---------------------------------------------------------------- K5 ----
 // Records arrive compact (one u64 each, RecFmt: lg, slot, reject, term,
@@ -903,7 +957,11 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   hipLaunchKernelGGL(k_bk_scatter, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st, geo,
                      rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1);
   QB_CHECK_LAUNCH("k_bk_scatter");
-  hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
+  if (QB_K4C && compact)
+    hipLaunchKernelGGL(k_bk_split_compact, dim3(unsigned(max_parts(geo))), dim3(kSplitThreads), 0,
+                       st, geo, hist, bsum, pt, buf1, buf2, cs);
+  else
+    hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
                        geo, hist, bsum, pt, buf1, buf2, cs);
   QB_CHECK_LAUNCH("k_bk_split");
   return QB_OK;
