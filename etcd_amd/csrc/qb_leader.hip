@@ -286,6 +286,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
 }
 
 constexpr u32 kStageRecs = 1024;  // chunk records placed through LDS
+#ifndef QB_LD_ONEPASS
+#define QB_LD_ONEPASS 1
+#endif
 constexpr u32 kLdsSortMax = 64;   // longer runs are ordered in HBM
 struct ChunkStage {
   u64 mr[kStageRecs];
@@ -316,10 +319,41 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
   cur[t] = 0;
-  for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
-    const u32 total = rt.build(cs, pb, p1, cl);  // synchronises first
-    for (u32 f = t; f < total; f += kBlock)
-      atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
+  // Common case (QB_LD_ONEPASS): one run table and at most kStageRecs
+  // records — each record is loaded once, into registers (kRegRecs per
+  // thread), counted from there and placed from there; otherwise the
+  // records are read twice (count, then place) by the loops below.
+  constexpr u32 kRegRecs = kStageRecs / kBlock;
+  u64 rv[kRegRecs], ri[kRegRecs];
+  u32 rt32[kRegRecs];
+  u32 total1 = 0;
+  const bool one_table = QB_LD_ONEPASS && p1 - p0 <= bk::RunTable::kRuns;  // block-uniform
+  if (one_table) total1 = rt.build(cs, p0, p1, cl);  // synchronises first
+  const bool onepass = one_table && total1 <= kStageRecs;  // block-uniform
+  if (onepass) {
+    u32 b[kRegRecs];
+#pragma unroll
+    for (u32 r = 0; r < kRegRecs; ++r) {
+      const u32 f = t + r * kBlock;
+      b[r] = f < total1 ? rt.locate(f) : 0u;
+    }
+#pragma unroll
+    for (u32 r = 0; r < kRegRecs; ++r) {
+      if (t + r * kBlock < total1) {
+        rv[r] = recs.mr[b[r]];
+        rt32[r] = recs.term32[b[r]];
+        ri[r] = recs.index[b[r]];
+      }
+    }
+#pragma unroll
+    for (u32 r = 0; r < kRegRecs; ++r)
+      if (t + r * kBlock < total1) atomicAdd(&cur[u32(rv[r]) & 1023u], 1u);
+  } else {
+    for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
+      const u32 total = rt.build(cs, pb, p1, cl);  // synchronises first
+      for (u32 f = t; f < total; f += kBlock)
+        atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
+    }
   }
   __syncthreads();
   const u32 x = cur[t];
@@ -343,7 +377,21 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     // is put in batch order there (runs of <= kLdsSortMax), and the chunk
     // is written out with coalesced stores.
     ChunkStage& cs_ = chunk_stage();
-    for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
+    if (onepass) {
+      __syncthreads();  // every group's cur[] start is written
+#pragma unroll
+      for (u32 r = 0; r < kRegRecs; ++r) {
+        if (t + r * kBlock < total1) {
+          const u64 v = rv[r];
+          const u64 term = rt32[r] != bk::kTermEscape ? u64(rt32[r]) : in.term[u32(v >> 32)];
+          const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
+          cs_.mr[e] = v;
+          cs_.term[e] = term;
+          cs_.index[e] = ri[r];
+        }
+      }
+    }
+    for (u32 pb = p0; !onepass && pb < p1; pb += bk::RunTable::kRuns) {
       const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
       for (u32 f = t; f < total; f += kBlock) {
         const u32 b = rt.locate(f);
