@@ -12,7 +12,7 @@ for i in $(seq $rounds); do
         > /tmp/ab_$name.json 2> /tmp/ab_$name.err; then
       python3 -c "import sys,json
 d=json.loads(open('/tmp/ab_$name.json').read().strip().splitlines()[-1]); r=d['roofline']
-print('$name', 'step_us', round(r['avg_kernel_us'],1), 'wall_us', round(d['ms_per_step']*1e3,1), 'frac', round(r['frac'],4), flush=True)"
+print('$name', 'step_us', round(r['avg_kernel_us'],1), 'wall_us', round(d['ms_per_step']*1e3,1), 'frac', round(r['frac'],4), str(d.get('parity',''))[:24], flush=True)"
     else
       echo "$name FAILED rc=$?"; tail -5 /tmp/ab_$name.err
     fi
