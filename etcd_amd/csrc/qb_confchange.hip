@@ -127,12 +127,24 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
 // Replays group g's operation.  On success fills the table/roles of the new
 // config and returns 0; otherwise an error code (the table then holds the
 // old config).  Roles.fresh marks entries whose Progress is (re)created.
+#ifndef QB_CC_PREFETCH
+#define QB_CC_PREFETCH 1
+#endif
 template <int TAB>
 __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autoleave, u64* bad,
                       int* n_old) {
   const u32 s0 = A.off[g], s1 = A.off[g + 1];
   const u32 ns = s1 - s0;
   const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
+  // the first change entry requested with the IDs (QB_CC_PREFETCH): the
+  // apply loop's first iteration then waits on no round trip of its own
+  const u32 k0 = A.cc_off[g], k1 = A.cc_off[g + 1];
+  u64 id0 = 0;
+  u32 ty0 = 0;
+  if (QB_CC_PREFETCH && k0 < k1) {
+    id0 = A.cc_node[k0];
+    ty0 = A.cc_type[k0];
+  }
   r = Roles{};
   for (u32 j = 0; j < ns; ++j) t.id(j) = A.ids[s0 + j];
   r.n = int(ns);
@@ -171,10 +183,10 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
     return QB_CCERR_BAD_OP;
   }
   // apply (confchange.go:151-175)
-  for (u32 k = A.cc_off[g]; k < A.cc_off[g + 1]; ++k) {
-    const u64 id = A.cc_node[k];
+  for (u32 k = k0; k < k1; ++k) {
+    const u64 id = QB_CC_PREFETCH && k == k0 ? id0 : A.cc_node[k];
     if (id == 0) continue;
-    const u32 typ = A.cc_type[k];
+    const u32 typ = QB_CC_PREFETCH && k == k0 ? ty0 : u32(A.cc_type[k]);
     int x = find(t, r.n, id);
     const bool has_pr = x >= 0 && ((r.prs >> x) & 1u);
     if (typ == QB_CC_ADD_NODE || typ == QB_CC_ADD_LEARNER) {
