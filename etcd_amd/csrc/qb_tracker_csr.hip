@@ -65,6 +65,9 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
   geo, recs, pt, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
       stepdown_at, advanced, chunk_slow, any_slow, shards
 
+#ifndef QB_CSR_EARLY
+#define QB_CSR_EARLY 1
+#endif
 // One chunk c (the whole workgroup).
 template <int WMAX, int CAPW, bool NEXT, bool SECOND>
 __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS) {
@@ -108,6 +111,35 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
   const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
+#if QB_CSR_EARLY
+  // The old slot run and the commit inputs depend only on the chunk's first
+  // and last offsets (uniform loads): issued now, in the same round trip as
+  // the offsets and the run table, instead of after the first barrier (one
+  // HBM round trip fewer in front of the record pass).
+  const u32 a0 = off[g0], run = off[g0 + ng] - a0;
+  const bool fits = run <= CAP;
+  u64 old[PER];
+  {
+    const u64* src = run ? match + a0 : group_term + g0;
+    const u32 last = run && fits ? run - 1u : 0u;
+#pragma unroll
+    for (u32 p = 0; p < PER; ++p) {
+      const u32 j = threadIdx.x + p * B;
+      old[p] = src[j < last ? j : last];
+    }
+  }
+  u64 cm[GPT], ts[GPT];
+  u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
+#pragma unroll
+  for (u32 k = 0; k < GPT; ++k) {
+    const u32 lg = threadIdx.x + k * B;
+    const u64 g = g0 + (lg < ng ? lg : ng - 1);
+    cm[k] = committed[g];
+    ts[k] = term_start[g];
+    cf[k] = cfg[g];
+    av[k] = active[g];
+  }
+#endif
   for (u32 k = threadIdx.x; k < CAP; k += B) {
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
@@ -125,13 +157,17 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
   for (u32 k = threadIdx.x; k < CH; k += B) act[k] = 0;
   __syncthreads();
+#if !QB_CSR_EARLY
   const u32 a0 = offs[0], run = offs[CH] - a0;
+#endif
   // A run longer than the buffer: when a second launch exists (CAPW < WMAX)
   // the first defers the chunk to it; otherwise (CAPW == WMAX, and in the
   // second launch) only a table breaking its max_slots bound gets here, and
   // the chunk takes the slow path (exact per-record semantics, global
   // atomics) — no chunk is left deferred without a launch to apply it.
+#if !QB_CSR_EARLY
   const bool fits = run <= CAP;
+#endif
   if constexpr (!SECOND && CAPW < WMAX) {
     if (!fits) {  // block-uniform, before anything is written
       if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
@@ -143,6 +179,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   // (an oversize run stays in HBM: its lanes re-read the first slot; an
   // empty run has no slot to read and reads the chunk's first group term
   // instead — a select, not a branch, which would cost the exact wait counts)
+#if !QB_CSR_EARLY
   u64 old[PER];
   const u64* src = run ? match + a0 : group_term + g0;
   const u32 last = run && fits ? run - 1u : 0u;
@@ -162,6 +199,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     cf[k] = cfg[g];
     av[k] = active[g];
   }
+#endif
   u32 total = rtab.finish(rq);
   __syncthreads();
   constexpr int kRecPer = int(QB_K5_INFLIGHT / B);  // records in flight per workgroup
