@@ -531,6 +531,73 @@ def tracker_parity(tr, csr, snap_host, batches, Gs, threads):
     return tracker_state_mismatches(tr, csr, st, Gs)
 
 
+def _timed(fn, barrier, warm=2, reps=5):
+    """Mean wall ms of fn() over reps calls between barriers (after warm)."""
+    out = None
+    for _ in range(warm):
+        out = fn()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    barrier()
+    return (time.perf_counter() - t0) / reps * 1e3, out
+
+
+def _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen, restore, barrier):
+    """configs[4]'s node-wide exchanges, timed after the region (SURVEY.md
+    §8e): records arriving at any rank delivered to the owning shards
+    (qb_dev_route_records), and the node-wide commit vector kept current by
+    the changed-commit delta (qb_dev_allgather_changed) next to the full
+    all-gather (qb_dev_allgather_results).  Node-wide checks: every record
+    arrives at its owner (count, ownership and a checksum of the global group
+    numbers over all ranks), and the delta-maintained vector equals a fresh
+    full gather of every shard's committed vector after a real tick."""
+    total = world * G
+    ranks = _rccl_ranks(args, world)
+    coll = {}
+    # routing: one batch of G records per rank with global group numbers
+    b = batches[0]
+    gl = torch.randint(0, total, (G,), generator=gen, device=dev, dtype=torch.int64)
+    cols = {"group": gl.to(torch.int32), "flags": b.flags, "index": b.index, "term": b.term}
+    route, route_impl = _router(args, dev)
+    route_ms, got = _timed(lambda: route(cols, total), barrier)
+    coll["route_records"] = {"ms": route_ms, "impl": route_impl, "ranks": world,
+                             "rccl_ranks": ranks, "records_per_rank": G}
+    lg = got["group"].long() & 0xFFFFFFFF
+    sums = torch.tensor([got["group"].numel(), int((lg + rank * G).sum().item()),
+                         int(gl.sum().item()), G], dtype=torch.int64, device=dev)
+    dist.all_reduce(sums)
+    owned = bool((lg < G).all().item())
+    route_ok = _all_ok(owned, world, dev) and int(sums[0].item()) == int(sums[3].item()) \
+        and int(sums[1].item()) == int(sums[2].item())
+    # the changed-commit delta after a real tick, against a full gather
+    gather, gather_impl = _gather(args, dev)
+    vote0 = torch.zeros(G, dtype=torch.uint8, device=dev)
+    adv = torch.zeros(G, dtype=torch.uint8, device=dev)
+    restore()
+    for k in range(W):
+        tr.step(batches[k], reset_stats=False, rearm=False)
+    commit_all, _ = gather(tr.committed, vote0, total)      # the vector before the tick
+    commit_all = commit_all.to(dev).clone()
+    tr.step(batches[W], advanced_out=adv, reset_stats=False, rearm=False)
+    delta, delta_impl = _delta(args, dev)
+    delta_changed = delta(adv, tr.committed, total, commit_all)   # applied once: checked below
+    full_ms, (full_c, _) = _timed(lambda: gather(tr.committed, vote0, total), barrier)
+    delta_ok = _all_ok(torch.equal(commit_all, full_c.to(dev)), world, dev)
+    scratch = commit_all.clone()
+    delta_ms, _ = _timed(lambda: delta(adv, tr.committed, total, scratch), barrier)
+    coll["allgather_changed"] = {"ms": delta_ms, "impl": delta_impl, "ranks": world,
+                                 "rccl_ranks": ranks, "changed_groups": delta_changed}
+    coll["allgather_results"] = {"ms": full_ms, "impl": gather_impl, "ranks": world,
+                                 "rccl_ranks": ranks, "bytes_received_per_rank": 9 * G * (world - 1)}
+    note = ("node-wide: routing delivered every record to its owner (count, ownership, group "
+            "checksum over all ranks)" if route_ok else "MISMATCH in the record routing")
+    note += ("; the delta-maintained commit vector equals a full all-gather after a real tick"
+             if delta_ok else "; MISMATCH between the changed-commit delta and a full all-gather")
+    return route_ms, route_impl, delta_ms, delta_impl, delta_changed, coll, note
+
+
 def tracker_main(args, world, rank, dev, barrier):
     csr = args.workload == "tracker-csr"
     G = args.groups if args.groups != 1 << 20 else 1 << 24
@@ -611,52 +678,15 @@ def tracker_main(args, world, rank, dev, barrier):
                   f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
                   else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
     route_ms = route_impl = delta_ms = delta_impl = delta_changed = None
+    collectives = {}
+    per_rank = _per_rank_values(G * K / elapsed, world)
     if world > 1:
         t = torch.tensor([elapsed, step_s], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_s = (float(x) for x in t.tolist())
-        # records arriving at arbitrary ranks: deliver one batch (G records per
-        # rank, global group numbers over all shards) to the owning ranks,
-        # timed apart — the C ABI's RCCL routing (qb_dev_route_records) on
-        # nccl, torch's all-to-all on a gloo rehearsal
-        b = batches[0]
-        gl = torch.randint(0, world * G, (G,), generator=gen, device=dev, dtype=torch.int64)
-        cols = {"group": gl.to(torch.int32), "flags": b.flags, "index": b.index, "term": b.term}
-        route, route_impl = _router(args, dev)
-        for _ in range(2):
-            got = route(cols, world * G)
-        barrier()
-        tr_ = time.perf_counter()
-        for _ in range(5):
-            got = route(cols, world * G)
-        barrier()
-        route_ms = (time.perf_counter() - tr_) / 5 * 1e3
-        n_in = torch.tensor([got["group"].numel()], dtype=torch.int64, device=dev)
-        dist.all_reduce(n_in)
-        if int(n_in.item()) != world * G:
-            raise SystemExit(f"routing lost records: {int(n_in.item())} of {world * G}")
-        # the changed-commit delta: the node-wide commit vector
-        # kept current from the groups whose commit moved.  A real changed set:
-        # the state replayed to the last warm-up tick, then one tick with
-        # advanced_out (untimed); the exchange is timed apart, like the routing
-        adv = torch.zeros(G, dtype=torch.uint8, device=dev)
-        restore()
-        for k in range(W):
-            tr.step(batches[k], reset_stats=False, rearm=False)
-        tr.step(batches[W], advanced_out=adv, reset_stats=False, rearm=False)
-        commit_all = torch.zeros(world * G, dtype=torch.int64, device=dev)
-        delta, delta_impl = _delta(args, dev)
-        for _ in range(2):
-            delta_changed = delta(adv, tr.committed, world * G, commit_all)
-        barrier()
-        td = time.perf_counter()
-        for _ in range(5):
-            delta_changed = delta(adv, tr.committed, world * G, commit_all)
-        barrier()
-        delta_ms = (time.perf_counter() - td) / 5 * 1e3
-        b0 = rank * G
-        if not torch.equal(commit_all[b0:b0 + G][adv.bool()], tr.committed[adv.bool()]):
-            raise SystemExit("changed-commit delta gather: this shard's commits did not arrive")
+        route_ms, route_impl, delta_ms, delta_impl, delta_changed, collectives, note = \
+            _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen, restore, barrier)
+        parity = (parity or "") + "; " + note
     parity = _agree(parity, world, dev)
     if rank != 0:
         return parity, None
@@ -705,6 +735,8 @@ def tracker_main(args, world, rank, dev, barrier):
         "route_ms": route_ms, "route_impl": route_impl,
         "allgather_changed_ms": delta_ms, "allgather_changed_impl": delta_impl,
         "allgather_changed_groups": delta_changed,
+        "collectives": collectives,
+        "value_per_rank": per_rank,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
@@ -765,6 +797,47 @@ def _agree(parity, world, dev):
     if int(ok.item()) == 0:
         return "MISMATCH on another rank"
     return parity + f" (every one of the {world} ranks)"
+
+
+def _per_rank_values(x: float, world: int):
+    """Every rank's own value (its groups / its own wall time), rank order."""
+    if world == 1:
+        return [float(x)]
+    box = [None] * world
+    dist.all_gather_object(box, float(x))
+    return [float(y) for y in box]
+
+
+def _all_ok(ok: bool, world: int, dev) -> bool:
+    """True iff ``ok`` holds on every rank."""
+    if world == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def _nodewide_eval_parity(args, world, rank, dev, G, B, n, gc, gv, c, v, threads):
+    """The node-wide vectors after the all-gather: on every rank, its own
+    slice equals its own outputs (which it checked bit-exact against the
+    oracle over the whole shard); on rank 0, every rank's slice against the
+    oracle over the first --parity-groups groups of that rank's batch 0 (the
+    counter-based inputs regenerate any sub-range)."""
+    b0 = rank * G
+    own = (torch.equal(gc[b0:b0 + G].to(dev), c) and torch.equal(gv[b0:b0 + G].to(dev), v))
+    ok0 = True
+    Gs = min(G, args.parity_groups)
+    if rank == 0:
+        hc = batch.as_u64(gc)
+        hv = gv.cpu().numpy()
+        for r in range(world):
+            ec, ev_ = eval_oracle(eval_inputs_host(args.workload, n, Gs, (r * B) * G), threads)
+            ok0 &= np.array_equal(hc[r * G:r * G + Gs], ec)
+            ok0 &= np.array_equal(hv[r * G:r * G + Gs], ev_)
+    ok = _all_ok(own and ok0, world, dev)
+    return (f"node-wide all-gather ({world} ranks) bit-exact: each rank's slice = its own checked "
+            f"output, and rank 0 checked the first {Gs} groups of every rank's slice vs the oracle"
+            if ok else "MISMATCH in the node-wide all-gather")
 
 
 # ------------------------------------------------------- evaluation path ---
@@ -964,13 +1037,15 @@ def eval_main(args, world, rank, dev, barrier):
                   else f"MISMATCH in {bad}/{B} batches")
 
     allgather_ms = gather_impl = None
+    collectives = {}
+    per_rank = _per_rank_values(G * K / elapsed, world)
     if world > 1:
         t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s], dtype=torch.float64,
                          device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s = (float(x) for x in t.tolist())
         # node-wide result: all-gather one batch's commit (u64) and vote (u8)
-        # vectors
+        # vectors, timed after the region
         gather, gather_impl = _gather(args, dev)
         c, v = outs[0]
         for _ in range(3):
@@ -982,15 +1057,13 @@ def eval_main(args, world, rank, dev, barrier):
             gc, gv = gather(c, v, world * G)
         barrier()
         allgather_ms = (time.perf_counter() - ta) / reps * 1e3
-        if rank == 0 and not args.no_parity:
-            # the node-wide vector against the oracle over every rank's batch 0
-            ok = True
-            for r in range(world):
-                ec, ev_ = eval_oracle(eval_inputs_host(args.workload, n, G, (r * B) * G), threads)
-                ok &= np.array_equal(batch.as_u64(gc[r * G:(r + 1) * G]), ec)
-                ok &= np.array_equal(gv[r * G:(r + 1) * G].cpu().numpy(), ev_)
-            parity = (parity or "") + ("; node-wide all-gather bit-exact" if ok
-                                       else "; MISMATCH in the node-wide all-gather")
+        collectives["allgather_results"] = {
+            "ms": allgather_ms, "impl": gather_impl, "ranks": world,
+            "rccl_ranks": _rccl_ranks(args, world),
+            "bytes_received_per_rank": 9 * G * (world - 1)}
+        if not args.no_parity:
+            parity = (parity or "") + "; " + _nodewide_eval_parity(
+                args, world, rank, dev, G, B, n, gc, gv, c, v, threads)
     parity = _agree(parity, world, dev)
 
     if rank == 0:
@@ -1059,6 +1132,8 @@ def eval_main(args, world, rank, dev, barrier):
             "mall_warm_kernel_us": warm_kernel_s * 1e6,
             "allgather_ms": allgather_ms,
             "allgather_impl": gather_impl,
+            "collectives": collectives,
+            "value_per_rank": per_rank,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_eval(args.workload, n, args.cpu_seconds)
@@ -1084,20 +1159,86 @@ def next_rows():
              "frac": algo_bytes / t / 1e9 / HBM_PEAK_GBS}
         d.update({k: v for k, v in (extra or {}).items() if k != "cpu_baseline"})
         rows.append(d)
-    orig, bc.report, bc.GPU_ONLY = bc.report, report, True
-    try:
-        for name, fn in (("leader", lambda: bc.leader_config(1 << 22, 20)),
-                         ("readindex", lambda: bc.readindex_config(1 << 22, 20)),
-                         ("wire", lambda: bc.wire_config(1 << 24, 20, rows=True)),
-                         ("confchange", lambda: bc.confchange_config(1 << 23, 20))):
-            try:
-                fn()
-            except Exception as ex:  # reported; the headline stands
-                rows.append({"config": name, "error": f"{type(ex).__name__}: {ex}"})
-            torch.cuda.empty_cache()
-    finally:
-        bc.report = orig
+    kw = {"reporter": report, "gpu_only": True}
+    for name, fn in (("leader", lambda: bc.leader_config(1 << 22, 20, **kw)),
+                     ("readindex", lambda: bc.readindex_config(1 << 22, 20, **kw)),
+                     ("wire", lambda: bc.wire_config(1 << 24, 20, rows=True, **kw)),
+                     ("confchange", lambda: bc.confchange_config(1 << 23, 20, **kw))):
+        try:
+            fn()
+        except Exception as ex:  # reported; the headline stands
+            rows.append({"config": name, "error": f"{type(ex).__name__}: {ex}"})
+        torch.cuda.empty_cache()
     return rows
+
+
+def other_summary(o2, p2):
+    """The other_configs entry of one secondary workload's line."""
+    r = o2["roofline"]
+    d = {"workload": o2["config"]["workload"], "value": o2["value"], "unit": o2["unit"],
+         "n_gpus": o2["n_gpus"], "steps": o2["steps"], "warmup": o2["warmup"],
+         "ms_per_step": o2["ms_per_step"], "value_per_rank": o2.get("value_per_rank"),
+         "roofline": {k: r[k] for k in ("achieved", "frac", "traffic", "bytes_per_group",
+                                        "avg_kernel_us", "kernel")},
+         "parity": p2}
+    if o2.get("collectives"):
+        d["collectives"] = o2["collectives"]
+    return d
+
+
+OTHER_WORKLOADS = ("ragged", "joint", "tracker", "tracker-csr")
+# the node-wide collectives each workload times after its region at N > 1
+COLLECTIVES = {"fixed": ("allgather_results",), "ragged": ("allgather_results",),
+               "joint": ("allgather_results",),
+               "tracker": ("route_records", "allgather_changed", "allgather_results"),
+               "tracker-csr": ("route_records", "allgather_changed", "allgather_results")}
+TOP_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
+            "parity", "rccl_ranks", "value_per_rank")
+
+
+def line_shape_errors(line: dict) -> list:
+    """What the default run's JSON line lacks (tests/test_bench_launcher.py
+    checks committed lines with it): the contract keys, the roofline and CPU
+    baseline at N = 1, and at every N the four other BASELINE configs with a
+    per-rank value each — plus, at N > 1, each workload's timed collectives
+    (ms, implementation, rank count) and node-wide parity."""
+    err = [f"missing {k}" for k in TOP_KEYS if k not in line]
+    n = line.get("n_gpus", 0)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        if k not in line.get("roofline", {}):
+            err.append(f"roofline.{k}")
+    if n == 1 and "cpu_baseline" not in line:
+        err.append("cpu_baseline at N = 1")
+    if len(line.get("value_per_rank") or []) != n:
+        err.append("value_per_rank: one value per rank")
+
+    def colls(where, d, wl):
+        if n <= 1:
+            return
+        for c in COLLECTIVES[wl]:
+            e = (d.get("collectives") or {}).get(c)
+            if not e or not all(k in e for k in ("ms", "impl", "ranks", "rccl_ranks")):
+                err.append(f"{where}: collective {c} (ms, impl, ranks, rccl_ranks)")
+            elif e["ranks"] != n or not e["ms"] or e["ms"] <= 0:
+                err.append(f"{where}: collective {c} ranks / ms")
+        if "node-wide" not in (d.get("parity") or ""):
+            err.append(f"{where}: node-wide parity")
+    colls("headline", line, "fixed")
+    others = line.get("other_configs") or {}
+    for wl in OTHER_WORKLOADS:
+        o = others.get(wl)
+        if not o or "error" in o:
+            err.append(f"other_configs.{wl}: {o.get('error') if o else 'missing'}")
+            continue
+        if len(o.get("value_per_rank") or []) != n or o.get("n_gpus") != n:
+            err.append(f"other_configs.{wl}: n_gpus / value_per_rank")
+        if "MISMATCH" in (o.get("parity") or "MISMATCH"):
+            err.append(f"other_configs.{wl}: parity")
+        colls(f"other_configs.{wl}", o, wl)
+    if "MISMATCH" in (line.get("parity") or ""):
+        err.append("parity")
+    return err
 
 
 def run_other(args, world, rank, dev, barrier):
@@ -1184,32 +1325,32 @@ def main():
     run = tracker_main if args.workload.startswith("tracker") else eval_main
     parity, out = run(args, world, rank, dev, barrier)
     bad = parity is not None and "MISMATCH" in parity
-    if out is not None and world == 1 and args.workload == "fixed" and not args.no_others:
+    if args.workload == "fixed" and not args.no_others:
         # the other BASELINE configs, measured by the same command (so the
-        # driver's own run backs them): configs[2] ragged, configs[3] joint,
-        # configs[4] streaming tracker (fixed and ragged CSR groups) — each at
-        # its full per-GPU size with its own warm-up, K = 20 and parity check
-        out["other_configs"] = {}
-        for wl in ("ragged", "joint", "tracker", "tracker-csr"):
+        # driver's own run backs them, at every N): configs[2] ragged,
+        # configs[3] joint, configs[4] streaming tracker (fixed and ragged CSR
+        # groups) — each at its full per-GPU size with its own warm-up, K = 20,
+        # parity check and (N > 1) its node-wide collectives and checks.  Every
+        # rank runs them (the collectives need all ranks); rank 0 reports.
+        others = {}
+        for wl in OTHER_WORKLOADS:
             sub = argparse.Namespace(**vars(args))
             sub.workload, sub.steps, sub.warmup, sub.no_cpu_baseline = wl, 20, None, True
             sub.preroll_ms, sub.settle_ms = min(args.preroll_ms, 200.0), min(args.settle_ms, 1000.0)
             try:
                 p2, o2 = run_other(sub, world, rank, dev, barrier)
             except Exception as ex:  # reported in the line; the headline stands
-                out["other_configs"][wl] = {"error": f"{type(ex).__name__}: {ex}"}
+                others[wl] = {"error": f"{type(ex).__name__}: {ex}"}
                 torch.cuda.empty_cache()
                 continue
             bad |= p2 is not None and "MISMATCH" in p2
-            r = o2["roofline"]
-            out["other_configs"][wl] = {
-                "workload": o2["config"]["workload"], "value": o2["value"], "unit": o2["unit"],
-                "steps": o2["steps"], "warmup": o2["warmup"], "ms_per_step": o2["ms_per_step"],
-                "roofline": {k: r[k] for k in ("achieved", "frac", "traffic", "bytes_per_group",
-                                               "avg_kernel_us", "kernel")},
-                "parity": p2}
+            if o2 is not None:
+                others[wl] = other_summary(o2, p2)
             torch.cuda.empty_cache()
-        out["next_rows"] = next_rows()
+        if out is not None:
+            out["other_configs"] = others
+            if world == 1:
+                out["next_rows"] = next_rows()
     if out is not None:
         print(json.dumps(out), flush=True)
     for c in _COMM:

@@ -58,6 +58,24 @@ class RcclComm:
             _lib.call("qb_comm_destroy", self._h)
             self._h = C.c_void_p()
 
+    def _shard_len(self, total: int) -> int:
+        from etcd_amd.shard import shard_range
+        b, e = shard_range(total, self.world, self.rank)
+        return e - b
+
+    def _check(self, name: str, t: torch.Tensor, numel: int, sizes) -> None:
+        """The C side reads ``numel`` elements from the raw device pointer: a
+        wrong length, a host tensor or another element size would be an
+        out-of-bounds device read (or a fault inside RCCL), so refuse it."""
+        if t.device.type != "cuda":
+            raise ValueError(f"{name}: a device tensor is required (got {t.device})")
+        if t.element_size() not in sizes:
+            raise ValueError(f"{name}: element size {t.element_size()}, expected {sizes}")
+        if t.numel() != numel:
+            raise ValueError(f"{name}: {t.numel()} elements, expected {numel}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: must be contiguous")
+
     def _workspace(self, nbytes: int) -> torch.Tensor:
         if self._ws is None or self._ws.numel() < nbytes:
             self._ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
@@ -67,11 +85,17 @@ class RcclComm:
                           commit_all: Optional[torch.Tensor] = None,
                           vote_all: Optional[torch.Tensor] = None):
         """Node-wide commit (u64) / vote (u8) vectors from this rank's shard
-        (qb_dev_allgather_results; shard_range order)."""
+        (qb_dev_allgather_results; shard_range order).  ``commit`` / ``vote``
+        hold exactly this rank's shard_range (device, 8-byte / 1-byte)."""
+        n = self._shard_len(total)
+        self._check("commit", commit, n, (8,))
+        self._check("vote", vote, n, (1,))
         if commit_all is None:
             commit_all = torch.empty(total, dtype=torch.int64, device=self.device)
         if vote_all is None:
             vote_all = torch.empty(total, dtype=torch.uint8, device=self.device)
+        self._check("commit_all", commit_all, total, (8,))
+        self._check("vote_all", vote_all, total, (1,))
         need = _lib.fn("qb_allgather_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         _lib.call("qb_dev_allgather_results", self._h, total, commit.data_ptr(), vote.data_ptr(),
@@ -85,12 +109,14 @@ class RcclComm:
         to ``commit_all`` (device, total u64 kept across ticks, updated in
         place).  ``changed`` (u8) / ``commit``: this rank's shard.  Returns the
         number of changed groups node-wide."""
-        if changed.dtype not in (torch.uint8, torch.bool) or commit.element_size() != 8 \
-                or commit_all.element_size() != 8 or commit_all.numel() != total:
-            raise ValueError("allgather_changed: changed u8, commit / commit_all 8-byte, "
-                             "commit_all of length total")
+        if changed.dtype not in (torch.uint8, torch.bool):
+            raise ValueError("allgather_changed: changed must be uint8 / bool")
+        n = self._shard_len(total)
         changed = changed.contiguous().view(torch.uint8)
         commit = commit.contiguous()
+        self._check("changed", changed, n, (1,))
+        self._check("commit", commit, n, (8,))
+        self._check("commit_all", commit_all, total, (8,))
         need = _lib.fn("qb_allgather_changed_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         n = C.c_uint64(0)
@@ -103,12 +129,25 @@ class RcclComm:
                       out_cap: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """This rank's records after delivery (qb_dev_route_records): every
         rank's records for groups of this shard, group rebased to the local
-        index, in (source rank, source position) order."""
+        index, in (source rank, source position) order.  ``out_cap`` must
+        bound the records this rank receives; by default it is the sum of
+        every rank's batch size (all-reduced over torch.distributed when it is
+        initialised — ranks may hold batches of different sizes — else world x
+        this rank's M)."""
         from etcd_amd.shard import _device_columns
         cols = _device_columns(cols)
+        for name, col in cols.items():
+            if col.device.type != "cuda":
+                raise ValueError(f"route_records: column {name!r} must be a device tensor")
         M = cols["group"].numel()
         if out_cap is None:
-            out_cap = self.world * M
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() == self.world:
+                t = torch.tensor([M], dtype=torch.int64,
+                                 device=self.device if dist.get_backend() == "nccl" else "cpu")
+                dist.all_reduce(t)
+                out_cap = int(t.item())
+            else:
+                out_cap = self.world * M
         out = {}
         for name, col in cols.items():
             out[name] = torch.empty(max(out_cap, 1), dtype=col.dtype, device=self.device)

@@ -108,8 +108,6 @@ extern "C" int qb_dev_allgather_results(qb_comm* c, uint64_t total,
                                         void* workspace, size_t workspace_bytes, void* stream) {
   QB_REQUIRE(c, "comm is NULL");
   QB_REQUIRE(commit_all || vote_all, "nothing to gather");
-  QB_REQUIRE(!commit_all || commit_shard, "commit_shard NULL");
-  QB_REQUIRE(!vote_all || vote_shard, "vote_shard NULL");
   if (total == 0) return QB_OK;
   hipStream_t st = qb::as_stream(stream);
   const int W = c->world;
@@ -117,6 +115,9 @@ extern "C" int qb_dev_allgather_results(qb_comm* c, uint64_t total,
   uint64_t b = 0, e = 0;
   shard_range(total, W, c->rank, &b, &e);
   const uint64_t mine = e - b;
+  // (a rank whose shard is empty, total < world, may pass NULL shard vectors)
+  QB_REQUIRE(!commit_all || commit_shard || mine == 0, "commit_shard NULL");
+  QB_REQUIRE(!vote_all || vote_shard || mine == 0, "vote_shard NULL");
   const bool even = total % uint64_t(W) == 0;
   // Even shards gather straight into the caller's vectors; otherwise the
   // padded shards go through the workspace and are compacted by rank.
@@ -197,7 +198,9 @@ extern "C" int qb_dev_allgather_changed(qb_comm* c, uint64_t total, const uint8_
   uint64_t b = 0, e = 0;
   shard_range(total, W, c->rank, &b, &e);
   const uint64_t n = e - b, cap = shard_cap(total, W);
-  QB_REQUIRE(n == 0 || (changed_shard && commit_shard), "changed_shard / commit_shard NULL");
+  // (NULL shard columns are not checked here: qb_dev_compact_changed refuses
+  // them and the refusal travels to every rank as a ~0 count below — an early
+  // return here would leave the other ranks waiting in the count all-gather)
   char* ws = static_cast<char*>(workspace);
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -242,6 +245,29 @@ extern "C" int qb_dev_allgather_changed(qb_comm* c, uint64_t total, const uint8_
   }
   *changed_total = sum;
   if (mx == 0) return QB_OK;
+  if (12 * mx > 8 * cap) {
+    // A skewed tick: the padded pairs (12 B x the largest count) would cost
+    // more than gathering every commit (8 B x the shard cap), so the whole
+    // vector is gathered instead — same result (commit_shard holds every
+    // group's current commit).  Every rank sees the same counts: one choice.
+    const bool even = total % uint64_t(W) == 0;
+    if (even) {
+      QB_NCCL(ncclAllGather(commit_shard, commit_all, cap, ncclUint64, c->nccl, st),
+              "ncclAllGather(commit, full)");
+      return QB_OK;
+    }
+    he = hipMemcpyAsync(val, commit_shard, 8 * n, hipMemcpyDeviceToDevice, st);
+    if (he != hipSuccess) return qb::hip_fail(he, "hipMemcpyAsync(pad)");
+    QB_NCCL(ncclAllGather(val, val_all, cap, ncclUint64, c->nccl, st), "ncclAllGather(commit, full)");
+    for (int r = 0; r < W; ++r) {
+      uint64_t rb = 0, re = 0;
+      shard_range(total, W, r, &rb, &re);
+      he = hipMemcpyAsync(commit_all + rb, val_all + uint64_t(r) * cap, 8 * (re - rb),
+                          hipMemcpyDeviceToDevice, st);
+      if (he != hipSuccess) return qb::hip_fail(he, "hipMemcpyAsync(compact)");
+    }
+    return QB_OK;
+  }
   // this rank's pairs padded to the largest count (gid UINT32_MAX: skipped)
   const uint64_t mine = h[size_t(c->rank)];
   if (mine < mx) {

@@ -738,7 +738,8 @@ int qb_comm_init(qb_comm** out, int world, int rank, const void* id);
 int qb_comm_destroy(qb_comm* comm);
 size_t qb_allgather_workspace_bytes(uint64_t total, int world);
 /* commit_all[total] / vote_all[total] (device; either nullable) receive every
- * rank's shard in rank order.  Collective over the comm, enqueued on stream.
+ * rank's shard in rank order (a rank whose shard is empty, total < world,
+ * may pass NULL shard vectors).  Collective over the comm, enqueued on stream.
  * The workspace (device, qb_allgather_workspace_bytes) is needed only when
  * total % world != 0 (padded shards compacted by rank). */
 int qb_dev_allgather_results(qb_comm* comm, uint64_t total,
@@ -767,14 +768,19 @@ size_t qb_allgather_changed_workspace_bytes(uint64_t total, int world);
 /* Collective over the comm: this rank's shard's changed groups (changed_shard
  * / commit_shard: the shard's local arrays, qb_shard_range) are exchanged and
  * applied to commit_all[total] (device) on every rank — the caller keeps
- * commit_all across ticks; a tick moves 12 bytes per changed group instead of
- * qb_dev_allgather_results' 8 per group.  *changed_total (host) = changed
- * groups node-wide.  The host waits on the stream once (the exchange size is
- * data-dependent); a rank's local failure in the compaction reaches every
- * rank through the gathered counts, so all return QB_EINVAL together.  Every
- * rank must pass the same total and a large enough workspace: a rank failing
- * those checks returns before the count all-gather and leaves the others
- * waiting in it (as qb_dev_route_records). */
+ * commit_all across ticks.  Every rank pads its pairs to the largest
+ * per-rank count C_max, so each rank receives 12 * world * C_max bytes (not
+ * 12 per changed group): a skewed tick (one shard with many commits)
+ * approaches the full gather's cost, and when 12 * C_max exceeds 8 * the
+ * shard size the call is cheaper as qb_dev_allgather_results (it picks that
+ * itself: see below).  *changed_total (host) = changed groups node-wide.  The
+ * host waits on the stream once (the exchange size is data-dependent); a
+ * rank's local failure in the compaction (NULL shard columns included)
+ * reaches every rank through the gathered counts, so all return QB_EINVAL
+ * together.  Every rank must pass the same total, a non-NULL commit_all and a
+ * large enough workspace: a rank failing those checks returns before the
+ * count all-gather and leaves the others waiting in it (as
+ * qb_dev_route_records). */
 int qb_dev_allgather_changed(qb_comm* comm, uint64_t total, const uint8_t* changed_shard,
                              const uint64_t* commit_shard, uint64_t* commit_all,
                              uint64_t* changed_total, void* workspace, size_t workspace_bytes,

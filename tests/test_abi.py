@@ -156,3 +156,25 @@ def test_shard_range_matches_python():
             assert lib.qb_shard_range(total, world, r, C.byref(b), C.byref(e)) == 0
             assert (b.value, e.value) == shard_range(total, world, r)
     assert lib.qb_shard_range(10, 2, 2, C.byref(b), C.byref(e)) == _lib.QB_EINVAL
+
+
+def test_fake_rccl_library_covers_every_rccl_import():
+    """tests/fake_rccl/libqb_fakecomm.so (test-only, the -m gpu
+    test_gpu_comm_fake.py multi-rank tests) defines every nccl* symbol the
+    product library imports from librccl, exports the same qb_* ABI, and
+    does not itself depend on librccl."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prod = os.path.join(root, "etcd_amd", "libquorumbatch.so")
+    fake = os.path.join(root, "tests", "fake_rccl", "libqb_fakecomm.so")
+
+    def syms(path, kind):
+        out = subprocess.run(["nm", "-D", path], capture_output=True, text=True, check=True).stdout
+        return {ln.split()[-1] for ln in out.splitlines() if ln.split()[-2:-1] == [kind]}
+    need = {s for s in syms(prod, "U") if s.startswith("nccl")}
+    assert need, "the product library should import RCCL entry points"
+    have = syms(fake, "T")
+    assert need <= have, need - have
+    assert {s for s in syms(prod, "T") if s.startswith("qb_")} <= have
+    ldd = subprocess.run(["ldd", fake], capture_output=True, text=True).stdout
+    assert "rccl" not in ldd

@@ -111,3 +111,63 @@ def test_default_run_secondary_configs_wiring():
         assert len(required) == nargs, name
     assert "rows" in inspect.signature(bc.wire_config).parameters
     assert callable(bench.next_rows) and callable(bench.run_other)
+
+
+def _synthetic_line(n):
+    """A default-run line of the shape bench.py prints at N ranks."""
+    coll = lambda names: {c: {"ms": 1.0, "impl": "x", "ranks": n, "rccl_ranks": n}  # noqa: E731
+                          for c in names}
+    line = {k: 1 for k in bench.TOP_KEYS}
+    line.update(n_gpus=n, value_per_rank=[1.0] * n, parity="bit-exact",
+                roofline={k: 1 for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")})
+    if n == 1:
+        line["cpu_baseline"] = {}
+    else:
+        line["collectives"] = coll(bench.COLLECTIVES["fixed"])
+        line["parity"] += "; node-wide all-gather bit-exact"
+    line["other_configs"] = {}
+    for wl in bench.OTHER_WORKLOADS:
+        o = {"n_gpus": n, "value_per_rank": [1.0] * n, "parity": "bit-exact"}
+        if n > 1:
+            o["collectives"] = coll(bench.COLLECTIVES[wl])
+            o["parity"] += "; node-wide: ..."
+        line["other_configs"][wl] = o
+    return line
+
+
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_line_shape_check(n):
+    """bench.line_shape_errors accepts a complete line and names what a
+    broken one lacks: at N > 1 every workload (configs[1]-[4]) must carry
+    its timed collectives with their rank counts and a node-wide parity."""
+    line = _synthetic_line(n)
+    assert bench.line_shape_errors(line) == []
+    bad = json.loads(json.dumps(line))
+    del bad["other_configs"]["joint"]
+    assert any("joint" in e for e in bench.line_shape_errors(bad))
+    bad = json.loads(json.dumps(line))
+    bad["value_per_rank"] = [1.0]
+    assert (bench.line_shape_errors(bad) != []) == (n != 1)
+    if n > 1:
+        bad = json.loads(json.dumps(line))
+        del bad["other_configs"]["tracker"]["collectives"]["route_records"]
+        assert any("route_records" in e for e in bench.line_shape_errors(bad))
+        bad = json.loads(json.dumps(line))
+        bad["other_configs"]["tracker-csr"]["parity"] = "bit-exact"
+        assert any("node-wide" in e for e in bench.line_shape_errors(bad))
+
+
+COMMITTED_LINES = [
+    "profiles/r04/multi/bench_n2_gloo_spawned.json",
+]
+
+
+@pytest.mark.parametrize("path", COMMITTED_LINES)
+def test_committed_rehearsal_line_shape(path):
+    """The committed `bench.py --gpus 2 --backend gloo` line (two ranks
+    spawned by bench.py on the one-GPU box, torch gloo collectives standing
+    in for RCCL) has every key the N > 1 contract asks for."""
+    with open(os.path.join(ROOT, path)) as f:
+        line = json.loads([x for x in f.read().splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert bench.line_shape_errors(line) == []

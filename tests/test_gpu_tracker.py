@@ -313,3 +313,55 @@ def test_bench_live_stream_full_size_every_tick(csr):
     tick without active or stats)."""
     from tests.parity_checks import check_tracker_stream
     check_tracker_stream(DEV, csr, 1 << 24, 24)
+
+
+def _escape_value(n):
+    """The compact record's term escape (qb_bucket.h RecFmt): tb = 23 - lgb -
+    slb bits, lgb = log2 of the chunk (512 groups for n <= 8, else 256), slb
+    = 3 for n <= 8 else 4 — all ones is the escape."""
+    lgb = 9 if n <= 8 else 8
+    slb = 3 if n <= 8 else 4
+    return (1 << (23 - lgb - slb)) - 1
+
+
+@pytest.mark.parametrize("n", [5, 9, 16])
+@pytest.mark.parametrize("what", ["term", "index"])
+def test_step_compact_record_escape_boundaries(n, what):
+    """the 8-byte compact record escapes a record whose term does
+    not fit its tb-bit field (term >= escape value) or whose index is >= 2^40.
+    'term': group terms straddle the escape value E (E-3 .. E+3) so a chunk
+    mixes packed records (term E-1 and below) with escaped ones (E and up),
+    equal / stale / higher alike; 'index': small terms, record indexes
+    straddling 2^40, so only the index escapes.  Match, committed, active,
+    stepdown and every stat counter vs the sequential oracle."""
+    G, M = 6000, 12000
+    E = _escape_value(n)
+    rng = np.random.default_rng(E * 31 + n + (what == "index"))
+    st = _random_state(rng, n, G, term_base=E - 5 if what == "term" else 0)
+    if what == "index":
+        shift = np.uint64((1 << 40) - 48)            # last indexes just above 2^40
+        st["match"] = st["match"] % np.uint64(128) + shift
+        st["match"][0] = st["match"].max(axis=0)    # the leader's own match is the last index
+        st["term_start"] = st["term_start"] % np.uint64(128) + shift
+        st["next"] = st["match"] + np.uint64(1)
+        st["last_index"] = st["match"][0].copy()
+        st["committed"][:] = 0
+        oc.commit_all(n, st["match"], st["term_start"], st["committed"])
+    tr = _tracker_from(n, st)
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(3):
+        group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, stale=0.05,
+                                                             higher=0.003)
+        if what == "term":
+            assert (term == E - 1).any() and (term == E).any() and (term >= E + 1).any()
+        else:
+            assert (index < (1 << 40)).any() and (index >= (1 << 40)).any()
+        stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, n, G)
+        got = tr.stats_dict()
+        want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                         "bad_group", "after_stepdown"), stats.tolist()))
+        assert {k: got[k] for k in want} == want
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0

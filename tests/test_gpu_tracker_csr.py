@@ -353,3 +353,60 @@ def test_csr_step_empty_batch_is_commit_advance(kind, G):
     assert np.array_equal(batch.as_u64(tr.match)[: bump.size], bump)
     assert np.array_equal(adv.cpu().numpy().astype(bool), want != st["committed"])
     assert all(v == 0 for v in tr.stats_dict().values())
+
+
+def _csr_escape_value(max_slots):
+    """RecFmt for the CSR step: 512-group chunks (lgb 9), slb = 3 for a slot
+    bound <= 8 else 4 — the term escape is 2047 or 1023."""
+    return (1 << (23 - 9 - (3 if max_slots <= 8 else 4))) - 1
+
+
+@pytest.mark.parametrize("max_slots", [4, 8, 16])
+@pytest.mark.parametrize("what", ["term", "index"])
+def test_csr_step_compact_record_escape_boundaries(max_slots, what):
+    """ADVICE r3, CSR geometry: group terms straddling the escape value of
+    the table's slot bound (packed and escaped records in one chunk), or
+    record indexes straddling 2^40 with small terms; joint configs and
+    learners included."""
+    G, M = 3000, 9000
+    E = _csr_escape_value(max_slots)
+    rng = np.random.default_rng(max_slots * 7 + (what == "index"))
+    lo = 1 if max_slots <= 8 else 9
+    sizes = rng.integers(lo, max_slots + 1, size=G).astype(np.int64)
+    off = np.zeros(G + 1, np.uint32)
+    off[1:] = np.cumsum(sizes).astype(np.uint32)
+    cfg = np.zeros(G, np.uint32)
+    for g in range(G):
+        s = int(sizes[g])
+        vin = int(rng.integers(1, 1 << s)) & ((1 << s) - 1)
+        vout = (int(rng.integers(1, 1 << s)) & ((1 << s) - 1)) if rng.random() < 0.3 else 0
+        cfg[g] = np.uint32(vin | (vout << 16))
+    S = int(off[-1])
+    base = (1 << 40) - 64 if what == "index" else 1 << 30
+    last = (base + rng.integers(0, 100, size=G)).astype(np.uint64)
+    match = np.repeat(last, sizes) - rng.integers(0, 200, size=S).astype(np.uint64)
+    term0 = E - 5 if what == "term" else 0
+    st = {"match": match, "next": match + np.uint64(1), "active": np.zeros(G, np.uint16),
+          "term": (rng.integers(2, 9, size=G) + term0).astype(np.uint64),
+          "term_start": last - rng.integers(0, 300, size=G).astype(np.uint64),
+          "last_index": last, "committed": np.zeros(G, np.uint64),
+          "stepped_down": np.zeros(G, np.uint8)}
+    oc.csr_commit_all(off, cfg, st["match"], st["term_start"], st["committed"])
+    tr = _tracker(off, cfg, st, max_slots=max_slots)
+    assert tr.max_slots == max_slots
+    seq = {k: v.copy() for k, v in st.items()}
+    for _ in range(3):
+        group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, seq, stale=0.05,
+                                                      higher=0.003, nonmember=0.01)
+        if what == "term":
+            assert (term == E - 1).any() and (term == E).any() and (term >= E + 1).any()
+        else:
+            assert (index < (1 << 40)).any() and (index >= (1 << 40)).any()
+        stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, G)
+        want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                         "bad_group", "after_stepdown"), stats.tolist()))
+        assert tr.stats_dict() == want
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0

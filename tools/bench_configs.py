@@ -30,7 +30,7 @@ from etcd_amd.quorum import batch  # noqa: E402
 dev = torch.device("cuda", 0)
 
 
-GPU_ONLY = False
+GPU_ONLY = False  # the command line's --gpu-only (functions take gpu_only= explicitly too)
 
 
 def time_region(fn, reps, warm_s=0.3, regions=5):
@@ -112,7 +112,9 @@ def plumbing_config(reps):
         del fg, c
 
 
-def csr_config(kind, G, reps):
+def csr_config(kind, G, reps, *, reporter=None, gpu_only=None):
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     grp = batch.CsrGroups.synth(0x5EED0003 if kind == "ragged" else 0x5EED0004, kind, G,
                                 device=dev)
     slots = int(grp.off[-1].item())
@@ -121,6 +123,9 @@ def csr_config(kind, G, reps):
     t = time_region(lambda: grp.committed_vote(c, v), reps)
     # off (4) + cfg (4) + votes (4) + match (8 s) + commit (8) + vote (1)
     algo = G * (4 + 4 + 4 + 8 + 1) + 8 * slots + 4
+    if gpu_only:
+        reporter(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G})
+        return
     # CPU beside it: the oracle's SoA C restatement on a bounded sample
     from tests import oracle_c as oc
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -128,13 +133,14 @@ def csr_config(kind, G, reps):
     off, m, cfg, votes = oc.gen_csr(0x5EED0003 if kind == "ragged" else 0x5EED0004, kind, Gs)
     cpu = cpu_rate(lambda: oc.csr_eval(off, m, cfg, votes, threads=threads), Gs)
     cpu1 = cpu_rate(lambda: oc.csr_eval(off, m, cfg, votes), Gs)
-    report(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G,
+    reporter(f"{kind} CSR", G, t, algo, {"mean_slots": slots / G,
            "cpu_baseline": {"value": cpu, "unit": "groups/s", "cores": threads, "kind": "port",
                             "value_1thread": cpu1,
                             "sample": f"{Gs} groups, C SoA restatement (oracle)"}})
 
 
-def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
+def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5, *, reporter=None,
+                   gpu_only=None):
     """Config 5: streaming MsgAppResp batches.  The leader holds E new
     entries per step (its own match, slot 0, is already at the last one);
     batch k acknowledges index last + (k+1)·E − lag (lag < 96) for a random
@@ -143,6 +149,8 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
     replayed would leave the state unchanged after its first application).
     Each timed region restores the start state (untimed), runs warm_steps
     batches, then times `reps` further distinct batches; median of regions."""
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     n = 5
     rng = np.random.default_rng(seed)
     tr = batch.FixedTracker(n, G, dev)
@@ -195,7 +203,7 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
         tr.commit_advance()
 
     t_two = t_apply = t_commit = float("nan")
-    if not GPU_ONLY:  # A/B runs time the bucketed step alone
+    if not gpu_only:  # A/B runs time the bucketed step alone
         t_two = stream_time(two_call)
         t_apply = stream_time(lambda b: tr.apply_appresp(b))
         t_commit = time_region(lambda: tr.commit_advance(), reps)
@@ -213,8 +221,8 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
     algo = G * (21 + 16) + G * 64
     # CPU beside it: the sequential one-record-at-a-time oracle (the Go
     # stepLeader loop restated) on a bounded sample, 1 thread
-    if GPU_ONLY:
-        report("streaming tracker (bucketed step)", G, t, algo, {"unit": "group-steps/s"})
+    if gpu_only:
+        reporter("streaming tracker (bucketed step)", G, t, algo, {"unit": "group-steps/s"})
         return
     from tests import oracle_c as oc
     Gs = 1 << 20
@@ -230,7 +238,7 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
     idx = np.where(lag < lst, lst - lag, np.uint64(0))
     trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
     cpu1 = cpu_rate(lambda: oc.appresp_sequential(n, Gs, (grp_, flg, idx, trm), st), Gs)
-    report("streaming tracker (bucketed step)", G, t, algo,
+    reporter("streaming tracker (bucketed step)", G, t, algo,
            {"two_call_us": t_two * 1e6, "atomic_apply_us": t_apply * 1e6,
             "workload": f"{G} groups x 5 voters, {G} records per step (streaming: {E} new "
                         f"entries per step), 1% stale-term; last step: {applied_last} applied, "
@@ -240,9 +248,11 @@ def tracker_config(G, reps, seed=55, E=64, warm_steps=4, regions=5):
                              "sample": f"{Gs} records on {Gs} groups, sequential C restatement"}})
 
 
-def leader_config(G, reps, warm=4, shuffle=True):
+def leader_config(G, reps, warm=4, shuffle=True, *, reporter=None, gpu_only=None):
     """§8f rows 1-2: the leader inbox step (qb_dev_leader_step) on streaming
     MsgAppResp batches (one per group per step), group-steps/s."""
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     from etcd_amd.quorum.leader import synth_streaming, streaming_inbox
     lg, base = synth_streaming(G, device=dev)
     steps = warm + reps
@@ -271,8 +281,8 @@ def leader_config(G, reps, warm=4, shuffle=True):
     # match/next/pstate/infl_pos written 21 B; messages 40 B x 3 (stored,
     # copied, written) per message; scans 16 B per group.
     algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
-    if not shuffle or GPU_ONLY:
-        report("leader inbox step" + ("" if shuffle else ", records in group order (lab)"), G, t,
+    if not shuffle or gpu_only:
+        reporter("leader inbox step" + ("" if shuffle else ", records in group order (lab)"), G, t,
                algo, {"unit": "group-steps/s", "msgs_per_step": msgs})
         return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
@@ -302,7 +312,7 @@ def leader_config(G, reps, warm=4, shuffle=True):
             if time.perf_counter() - t0 > 6 or n_steps >= 24:
                 break
         cpu[threads] = n_steps * Gs / cpu[threads]
-    report("leader inbox step (streaming MsgAppResp)", G, t, algo,
+    reporter("leader inbox step (streaming MsgAppResp)", G, t, algo,
            {"unit": "group-steps/s", "msgs_per_step": msgs,
             "applied_per_step": st[0] / reps, "inflight_cap": 32, "voters": 5,
             "cpu_baseline": {"value": cpu[16], "unit": "group-steps/s", "cores": 16,
@@ -311,10 +321,12 @@ def leader_config(G, reps, warm=4, shuffle=True):
                                        "C restatement of stepLeader (oracle/leader_oracle.c)"}})
 
 
-def wire_config(M, reps, G=None, rows=False):
+def wire_config(M, reps, G=None, rows=False, *, reporter=None, gpu_only=None):
     """§8f row 3: wire ingest of M gogoproto-encoded responses (MsgAppResp +
     10% MsgHeartbeatResp with read contexts) to M/4 5-voter leaders (G given:
     a development variant with a small, cache-resident group table)."""
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     from etcd_amd.quorum import wire
     from tests import oracle_c as oc
     G = G or M // 4
@@ -332,8 +344,8 @@ def wire_config(M, reps, G=None, rows=False):
     # slot IDs 40 (5 x u64, read once per message); written: group 4, flags
     # 1, index/term/hint/log_term 32, status 1, type 1
     algo = nb + M * (8 + 4 + 40) + M * (4 + 1 + 32 + 1 + 1)
-    if GPU_ONLY:
-        report("wire ingest" + (" (group rows)" if rows else ""), M, t, algo,
+    if gpu_only:
+        reporter("wire ingest" + (" (group rows)" if rows else ""), M, t, algo,
                {"unit": "messages/s", "bytes_per_message": nb / M})
         return
     import time
@@ -347,7 +359,7 @@ def wire_config(M, reps, G=None, rows=False):
             if time.perf_counter() - t0 > 4:
                 break
         cpu[threads] = reps_c * Ms / (time.perf_counter() - t0)
-    report("wire ingest (raftpb.Message -> leader inbox)" + (", group rows" if rows else ""),
+    reporter("wire ingest (raftpb.Message -> leader inbox)" + (", group rows" if rows else ""),
            M, t, algo,
            {"unit": "messages/s", "bytes_per_message": nb / M,
             "input_GBs": nb / t / 1e9,
@@ -357,10 +369,12 @@ def wire_config(M, reps, G=None, rows=False):
                                        "gogoproto Message.Unmarshal + ingest (oracle/wire_oracle.c)"}})
 
 
-def confchange_config(G, reps):
+def confchange_config(G, reps, *, reporter=None, gpu_only=None):
     """§8f row 4: one Changer.Simple(AddLearnerNode) per group over G 5-voter
     groups (Progress carried for 5 slots, initialised for the new one),
     groups/s; CPU beside it: the Python restatement on a small sample."""
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     import time
     from etcd_amd.quorum.confchange import ConfigTable, ADD_LEARNER, SIMPLE
     from oracle import confchange_ref as CC
@@ -390,8 +404,8 @@ def confchange_config(G, reps):
     # 6 x (29 + K*8), err 1, err_id 8
     pr = 29 + 8 * K
     algo = G * (4 + 40 + 8 + 1 + 4 + 9 + 8 + 5 * pr + 4 + 48 + 8 + 6 * pr + 9)
-    if GPU_ONLY:
-        report("conf change", G, tt, algo, {"unit": "groups/s"})
+    if gpu_only:
+        reporter("conf change", G, tt, algo, {"unit": "groups/s"})
         return
     n = 20000
     trs = []
@@ -404,18 +418,20 @@ def confchange_config(G, reps):
     for tr in trs:
         CC.Changer(tr, 100).simple([(CC.ADD_LEARNER, 6)])
     cpu1 = n / (time.perf_counter() - t0)
-    report("conf change (Simple AddLearner, 5 -> 6 slots)", G, tt, algo,
+    reporter("conf change (Simple AddLearner, 5 -> 6 slots)", G, tt, algo,
            {"unit": "groups/s", "cpu_baseline": {
                "value": cpu1, "unit": "groups/s", "cores": 1, "kind": "port",
                "sample": f"{n} groups, Python restatement of confchange.Changer (oracle)"}})
 
 
-def readindex_config(G, reps, Q=4):
+def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
     """§8f row 2: ReadIndex acks — two heartbeat responses per leader carrying
     the latest read context; the quorum releases all Q pending reads
     (MsgReadIndexResp / ReadState).  The read queues are restored before each
     step outside the timed launches (new MsgReadIndex requests are the
     host's).  Also CheckQuorum: QuorumActive over 16M CSR groups."""
+    reporter = reporter or report
+    gpu_only = GPU_ONLY if gpu_only is None else gpu_only
     from etcd_amd.quorum.leader import synth_readindex, readindex_inbox
     lg, last_ctx, pristine = synth_readindex(G, Q, device=dev)
     inboxes = [readindex_inbox(G, last_ctx, device=dev) for _ in range(reps + 2)]
@@ -444,6 +460,13 @@ def readindex_config(G, reps, Q=4):
     grp = batch.CsrGroups.synth(0x5EED0003, "ragged", 1 << 24, device=dev)
     active = torch.randint(-(1 << 15), 1 << 15, (1 << 24,), dtype=torch.int16, device=dev)
     tq = time_region(lambda: grp.quorum_active(active), 20)
+    cq = {"read_queue": Q, "check_quorum_16M_us": tq * 1e6,
+          "check_quorum_groups_per_s": (1 << 24) / tq,
+          "check_quorum_GBs": (1 << 24) * 7 / tq / 1e9}
+    if gpu_only:
+        reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
+                 {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq})
+        return
     # CPU beside it: the C restatement on 1M groups of the same workload
     import time
     from tests import oracle_c as oc
@@ -460,14 +483,12 @@ def readindex_config(G, reps, Q=4):
         t1 = time.perf_counter()
         oc.leader_step(host, lgc.inflight_cap, Q, 0, recc, threads=threads, msg_cap=8 * Gs)
         cpu[threads] = Gs / (time.perf_counter() - t1)
-    report("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
+    reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
            {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps,
             "cpu_baseline": {"value": cpu[16], "unit": "group-steps/s", "cores": 16,
                              "kind": "port", "value_1thread": cpu[1],
                              "sample": f"{Gs} groups, one step, C restatement (oracle)"},
-            "read_queue": Q, "check_quorum_16M_us": tq * 1e6,
-            "check_quorum_groups_per_s": (1 << 24) / tq,
-            "check_quorum_GBs": (1 << 24) * 7 / tq / 1e9})
+            **cq})
 
 
 def main():

@@ -26,10 +26,25 @@ import os
 import numpy as np
 
 
+def base_name(full: str) -> str:
+    """A kernel's unqualified name without template arguments or parameters:
+    "void qb::bk::k_csr_apply<12, 8, false>(...)" -> "k_csr_apply"."""
+    s = full[5:] if full.startswith("void ") else full
+    s = s.replace("(anonymous namespace)::", "")
+    for ch in "<(":
+        i = s.find(ch)
+        if i >= 0:
+            s = s[:i]
+    return s.rsplit("::", 1)[-1].strip()
+
+
 def per_dispatch(path, kernel, counter):
+    """Per-dispatch counter values of the kernels whose base name is exactly
+    ``kernel`` (round 3 matched substrings, so "k_csr_apply" also took
+    k_csr_apply_deferred's dispatches into its median)."""
     vals = {}
     for r in csv.DictReader(open(path)):
-        if kernel not in r.get("Kernel_Name", ""):
+        if base_name(r.get("Kernel_Name", "")) != kernel:
             continue
         if r.get("Counter_Name") != counter:
             continue
@@ -47,15 +62,25 @@ def main():
                          "every listed kernel (a multi-kernel step, one dispatch of each per step)")
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--from-end", action="store_true",
+                    help="take each kernel's LAST --steps dispatches (the tracker bench runs nothing "
+                         "after its region, and its setup dispatches some step kernels once more "
+                         "than the others, which shifts a [W, W+K) window per kernel)")
     ap.add_argument("--key", required=True)
     ap.add_argument("--algo-bytes", type=float, required=True, help="algorithmic bytes/launch")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--source", default=None,
+                    help="where the two CSVs are committed (profiles/rNN/...), stored in the entry")
     a = ap.parse_args()
     fk = wk = 0.0
     per = {}
     for kern in a.kernel.split(","):
-        f = per_dispatch(a.fetch, kern, "FETCH_SIZE")[a.warmup:a.warmup + a.steps]
-        w = per_dispatch(a.write, kern, "WRITE_SIZE")[a.warmup:a.warmup + a.steps]
+        f = per_dispatch(a.fetch, kern, "FETCH_SIZE")
+        w = per_dispatch(a.write, kern, "WRITE_SIZE")
+        if a.from_end:
+            f, w = f[-a.steps:], w[-a.steps:]
+        else:
+            f, w = f[a.warmup:a.warmup + a.steps], w[a.warmup:a.warmup + a.steps]
         if not f or not w:
             raise SystemExit(f"no matching dispatches for {kern}")
         per[kern] = {"read_bytes_corrected": 2.0 * float(np.median(f)) * 1024.0,
@@ -72,8 +97,12 @@ def main():
         "algorithmic_bytes_per_launch": a.algo_bytes,
         "traffic_over_algorithmic": (read_b + write_b) / a.algo_bytes,
         "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; "
-                  "FETCH_SIZE x2 (gfx950 wide-read correction); KiB->bytes x1024",
+                  "FETCH_SIZE x2 (gfx950 wide-read correction); KiB->bytes x1024; kernels "
+                  "matched by exact base name; " + ("last K dispatches of each kernel"
+                                                   if a.from_end else "dispatches [W, W+K)"),
     }
+    if a.source:
+        rec["source"] = a.source
     doc = {}
     if os.path.exists(a.out):
         doc = json.load(open(a.out))

@@ -42,7 +42,8 @@ def summarise(path, filt="", gap_us=50.0):
         for rr in runs:
             span = (en[rr].max() - st[rr].min()) / 1e3
             run_info.append({"dispatches": len(rr), "span_us": round(span, 2),
-                             "interval_us": round(span / len(rr), 3)})
+                             "interval_us": round(span / len(rr), 3),
+                             "mean_dispatch_us": round(float(dur[rr].mean()), 3)})
         out[name] = {
             "dispatches": len(iv),
             "mean_us": round(float(dur.mean()), 3),
