@@ -81,6 +81,8 @@ SIGNATURES = {
     "qb_dev_csr_tally_votes": (_i32, [_u64, _p, _p, _p, _p, _p, _p]),
     "qb_leader_workspace_bytes": (C.c_size_t, [_u64, _u64]),
     "qb_dev_leader_step": (_i32, [_p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, C.c_size_t, _p]),
+    "qb_leader_outbox_workspace_bytes": (C.c_size_t, [_u64, _u64]),
+    "qb_dev_leader_step_outbox": (_i32, [_p, _p, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_dev_ingest_messages": (_i32, [_u64, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p,
                                       _p, _p, _p, _p, _p]),
     "qb_wire_group_rows_bytes": (C.c_size_t, [_u64]),

@@ -9,10 +9,7 @@
 namespace qb {
 namespace bk {
 
-#ifndef QB_KTILE
-#define QB_KTILE 4096
-#endif
-constexpr int kTile = QB_KTILE;      // records per histogram/scatter/split tile
+constexpr int kTile = 4096;          // records per histogram/scatter/split tile
 constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
 using scan::kScanPer;
 constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
@@ -89,65 +86,25 @@ struct RecFmt {
 // 41 -> 55 us with it, so it keeps the linear order.
 constexpr u32 kXcds = 8;
 // interleaved super-buckets (Geometry::il) for the tracker steps
-#ifndef QB_SB_IL
-#define QB_SB_IL 1
-#endif
-constexpr bool kSbIl = QB_SB_IL != 0;
-// K5 write-back granularity (k_bk_apply, k_csr_apply): 0 = changed values
-// only; 1 = committed / active as whole wave segments where any changed; 2 =
-// the slot rows too
-#ifndef QB_K5_FULL
-#define QB_K5_FULL 2
-#endif
-#ifndef QB_CSR_FULL
-#define QB_CSR_FULL 2  // round 3 (compact records): 776 -> 764 us per 16M ragged tick
-#endif
-// Write granule of the whole-segment write-back (QB_K5_FULL / QB_CSR_FULL
-// = 2): a lane stores when any lane of its aligned granule of QB_WB_GRAN
-// 8-byte elements changed (64 = the whole wave segment).
-#ifndef QB_WB_GRAN
-#define QB_WB_GRAN 64
-#endif
-// Whether p holds on any lane of this lane's granule of W consecutive
-// elements, lane l holding element e0 + l (W a power of two < 64; e is this
-// lane's element index, so granules follow the memory alignment); W >= 64:
-// any lane of the wave.
-template <u32 W>
-__device__ __forceinline__ bool granule_any(bool p, u64 e) {
-  const u64 m = __ballot(p);
-  if constexpr (W >= 64) {
-    return m != 0;
-  } else {
-    const int lf = int(threadIdx.x & 63u) - int(e & (W - 1u));  // first lane of the granule
-    const u64 sel = (1ull << W) - 1ull;
-    return (m & (lf >= 0 ? sel << lf : sel >> -lf)) != 0;
-  }
-}
-// Records a K5 workgroup has in flight per pass (both tracker steps).
-#ifndef QB_K5_INFLIGHT
-#define QB_K5_INFLIGHT 1024
-#endif
+constexpr bool kSbIl = true;
+// K5 write-back (k_bk_apply, k_csr_apply): a wave whose 64-element segment
+// of a slot row (or of committed / active) changed anywhere stores the whole
+// segment, unchanged values rewritten, so every written line is whole —
+// faster than storing only the changed lanes although more bytes are
+// written (round 2: -20 us per 16M-group tick; round 3, CSR: -12 us).
+// Narrower granules (32 / 64 bytes) measured +25 us (profiles/r03/k5_variants/).
+__device__ __forceinline__ bool segment_any(bool p) { return __ballot(p) != 0; }
+// Records a K5 workgroup has in flight per pass (both tracker steps);
+// doubling it measured slower (profiles/r03/compact/).
+constexpr u32 kK5Inflight = 1024;
 __device__ __forceinline__ u32 xcd_major() {
   return (blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
 }
 
 // Groups per K5 chunk (one workgroup; its LDS holds n accumulators per group).
-#ifndef QB_CH_NARROW
-#define QB_CH_NARROW 512
-#endif
-#ifndef QB_CH_WIDE
-#define QB_CH_WIDE 256
-#endif
-__host__ __device__ constexpr u32 chunk_groups(u32 n) {
-  return n <= 8 ? u32(QB_CH_NARROW) : u32(QB_CH_WIDE);
-}
+__host__ __device__ constexpr u32 chunk_groups(u32 n) { return n <= 8 ? 512u : 256u; }
 // CSR chunks: the LDS run buffer holds CH * WMAX slots.
-#ifndef QB_CSR_CH_WIDE
-#define QB_CSR_CH_WIDE 512
-#endif
-__host__ __device__ constexpr u32 csr_chunk_groups(u32 wmax) {
-  return wmax <= 8 ? 512u : u32(QB_CSR_CH_WIDE);
-}
+__host__ __device__ constexpr u32 csr_chunk_groups(u32 /*wmax*/) { return 512u; }
 
 struct Geometry {
   u64 G, M;

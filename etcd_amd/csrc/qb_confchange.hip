@@ -127,21 +127,18 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
 // Replays group g's operation.  On success fills the table/roles of the new
 // config and returns 0; otherwise an error code (the table then holds the
 // old config).  Roles.fresh marks entries whose Progress is (re)created.
-#ifndef QB_CC_PREFETCH
-#define QB_CC_PREFETCH 1
-#endif
 template <int TAB>
 __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autoleave, u64* bad,
                       int* n_old) {
   const u32 s0 = A.off[g], s1 = A.off[g + 1];
   const u32 ns = s1 - s0;
   const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
-  // the first change entry requested with the IDs (QB_CC_PREFETCH): the
-  // apply loop's first iteration then waits on no round trip of its own
+  // the first change entry requested with the IDs: the apply loop's first
+  // iteration then waits on no round trip of its own (round 3: 2103 -> 2085 us)
   const u32 k0 = A.cc_off[g], k1 = A.cc_off[g + 1];
   u64 id0 = 0;
   u32 ty0 = 0;
-  if (QB_CC_PREFETCH && k0 < k1) {
+  if (k0 < k1) {
     id0 = A.cc_node[k0];
     ty0 = A.cc_type[k0];
   }
@@ -184,9 +181,9 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
   }
   // apply (confchange.go:151-175)
   for (u32 k = k0; k < k1; ++k) {
-    const u64 id = QB_CC_PREFETCH && k == k0 ? id0 : A.cc_node[k];
+    const u64 id = k == k0 ? id0 : A.cc_node[k];
     if (id == 0) continue;
-    const u32 typ = QB_CC_PREFETCH && k == k0 ? ty0 : u32(A.cc_type[k]);
+    const u32 typ = k == k0 ? ty0 : u32(A.cc_type[k]);
     int x = find(t, r.n, id);
     const bool has_pr = x >= 0 && ((r.prs >> x) & 1u);
     if (typ == QB_CC_ADD_NODE || typ == QB_CC_ADD_LEARNER) {
@@ -313,12 +310,9 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
 constexpr u8 kCarried = 0xFF;
 // A fresh slot (initProgress) is marked kFresh with its group in the new
 // infl_pos; k_cc_copy materialises it.  So every new slot's row is written
-// by the copy kernel, whole lines per wave (QB_CC_FRESH_IN_COPY; 0 = the
-// write pass stores fresh rows itself, scattered partial lines).
+// by the copy kernel, whole lines per wave (round 2: the write pass storing
+// fresh rows itself left scattered partial lines; 2565 -> 2220 us).
 constexpr u8 kFresh = 0xFE;
-#ifndef QB_CC_FRESH_IN_COPY
-#define QB_CC_FRESH_IN_COPY 1
-#endif
 
 template <int TAB>
 __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
@@ -342,7 +336,6 @@ __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
     al = (e >> 16) & 1u;
   }
   u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
-  const u64 last = A.last_index[g];
   auto emit = [&](u32 j, int best) {
     const u32 b = 1u << best;
     if (r.in & b) ncfg_in |= 1u << j;
@@ -354,15 +347,9 @@ __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
     if (carried) {  // carried Progress: k_cc_copy
       A.n_pstate[d] = kCarried;
       A.n_infl_pos[d] = s0 + u32(best);
-    } else if (QB_CC_FRESH_IN_COPY) {  // initProgress (confchange.go:258-281): k_cc_copy
+    } else {  // initProgress (confchange.go:258-281): materialised by k_cc_copy
       A.n_pstate[d] = kFresh;
       A.n_infl_pos[d] = u32(g);
-    } else {  // initProgress (confchange.go:258-281)
-      A.n_match[d] = 0;
-      A.n_next[d] = last;
-      A.n_psnap[d] = 0;
-      A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
-      A.n_infl_pos[d] = 0;
     }
   };
   // Surviving entries in ascending ID order.  The old slots are already
@@ -442,7 +429,7 @@ __global__ __launch_bounds__(256) void k_cc_copy(Args A) {
   const u32 K = A.K;
   for (u64 d = u64(blockIdx.x) * 256 + threadIdx.x; d < end; d += u64(gridDim.x) * 256) {
     const u8 mk = A.n_pstate[d];
-    const bool carried = mk == kCarried, fresh = QB_CC_FRESH_IN_COPY && mk == kFresh;
+    const bool carried = mk == kCarried, fresh = mk == kFresh;
     const u32 src = carried || fresh ? A.n_infl_pos[d] : 0u;
     const bool ok = carried && src < old_total;
     if (ok) {

@@ -44,8 +44,8 @@
 namespace qb {
 namespace ld {
 
-constexpr u32 kFix = 8;         // messages per group kept in the fixed area
-constexpr u32 kChunk = 32;      // messages per overflow chunk
+constexpr u32 kFix = QB_LEADER_OUTBOX_SLOTS;    // messages per group kept in the fixed area
+constexpr u32 kChunk = QB_LEADER_OUTBOX_CHUNK;  // messages per overflow chunk
 constexpr u32 kEmitStage = 1024;  // messages per workgroup staged by k_ld_emit
 constexpr u32 kNone = 0xFFFFFFFFu;
 constexpr u8 kNoSlot = 0xFF;
@@ -78,7 +78,9 @@ struct Carve {
   bk::Geometry geo;
   bk::Carve bcv;
 };
-inline Carve carve(u64 G, u64 M) {
+// outbox: the caller owns the message slots / chunks / counts
+// (qb_dev_leader_step_outbox), so they are not carved.
+inline Carve carve(u64 G, u64 M, bool outbox = false) {
   Carve c{};
   size_t o = 0;
   c.geo = bk::geometry(16, G, M);
@@ -98,13 +100,15 @@ inline Carve carve(u64 G, u64 M) {
   c.rindex = o; o += up256(sizeof(u64) * (M + 1));
   c.rhint = o;  o += up256(sizeof(u64) * (M + 1));
   c.rlt = o;    o += up256(sizeof(u64) * (M + 1));
-  c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
-  c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
-  c.fix = o;    o += up256(sizeof(Msg) * kFix * G);
-  c.chead = o;  o += up256(sizeof(u32) * (G + 1));
-  c.nchunks = M / 8 + 1024;  // 4 spilled messages per record on average
-  c.cnext = o;  o += up256(sizeof(u32) * c.nchunks);
-  c.chunks = o; o += up256(sizeof(Msg) * kChunk * c.nchunks);
+  if (!outbox) {
+    c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
+    c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
+    c.fix = o;    o += up256(sizeof(Msg) * kFix * G);
+    c.chead = o;  o += up256(sizeof(u32) * (G + 1));
+    c.nchunks = M / 8 + 1024;  // 4 spilled messages per record on average
+    c.cnext = o;  o += up256(sizeof(u32) * c.nchunks);
+    c.chunks = o; o += up256(sizeof(Msg) * kChunk * c.nchunks);
+  }
   c.pool = o;   o += up256(sizeof(u32) * 2);
   c.shards = o; o += up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
   c.total = o;
@@ -286,9 +290,6 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
 }
 
 constexpr u32 kStageRecs = 1024;  // chunk records placed through LDS
-#ifndef QB_LD_ONEPASS
-#define QB_LD_ONEPASS 1
-#endif
 constexpr u32 kLdsSortMax = 64;   // longer runs are ordered in HBM
 struct ChunkStage {
   u64 mr[kStageRecs];
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
   const u32 p0 = pt[sb], p1 = pt[sb + 1];
   cur[t] = 0;
-  // Common case (QB_LD_ONEPASS): one run table and at most kStageRecs
+  // Common case (round 3, one pass): one run table and at most kStageRecs
   // records — each record is loaded once, into registers (kRegRecs per
   // thread), counted from there and placed from there; otherwise the
   // records are read twice (count, then place) by the loops below.
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   u64 rv[kRegRecs], ri[kRegRecs];
   u32 rt32[kRegRecs];
   u32 total1 = 0;
-  const bool one_table = QB_LD_ONEPASS && p1 - p0 <= bk::RunTable::kRuns;  // block-uniform
+  const bool one_table = p1 - p0 <= bk::RunTable::kRuns;  // block-uniform
   if (one_table) total1 = rt.build(cs, p0, p1, cl);  // synchronises first
   const bool onepass = one_table && total1 <= kStageRecs;  // block-uniform
   if (onepass) {
@@ -1205,8 +1206,10 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
 // bshards: the bucket pass's shards (bad groups), or null.
 // One wave per counter: lanes sum strided shards, then a shuffle reduction.
 __global__ void k_ld_fold(const u64* __restrict__ shards, const u64* __restrict__ bshards,
-                          u64* __restrict__ stats) {
+                          u64* __restrict__ stats, const u32* __restrict__ pool,
+                          u32* __restrict__ chunks_used) {
   const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (chunks_used && threadIdx.x == 0) *chunks_used = *pool;
   if (k >= QB_LSTAT_COUNT) return;
   u64 s = shards[lane * QB_LSTAT_COUNT + k];
   if (bshards && k == QB_LSTAT_BAD_GROUP)
@@ -1227,42 +1230,36 @@ extern "C" size_t qb_leader_workspace_bytes(uint64_t G, uint64_t M) {
   return ld::carve(G, M).total;
 }
 
-extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
-                                  qb_msg_out* msgs, uint64_t msg_cap, uint64_t* msg_total,
-                                  uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags,
-                                  uint64_t* stats, void* workspace, size_t workspace_bytes,
-                                  void* stream) {
-  QB_REQUIRE(lg && in, "qb_dev_leader_step: lg and in are required");
+extern "C" size_t qb_leader_outbox_workspace_bytes(uint64_t G, uint64_t M) {
+  return ld::carve(G, M, /*outbox=*/true).total;
+}
+
+namespace {
+
+// Where the step leaves its messages: the workspace's k-major area + pool
+// (qb_dev_leader_step, which then compacts them into group order), or the
+// caller's outbox (qb_dev_leader_step_outbox).
+struct MsgSink {
+  ld::Msg* fix;
+  u32* count;
+  u32* chead;
+  u32* cnext;
+  ld::Msg* chunks;
+  u64 nchunks;
+  u32* chunks_used;  // outbox only
+};
+
+int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, const ld::Carve& c,
+                     const MsgSink* sink, qb_msg_out* msgs, uint64_t msg_cap, uint64_t* msg_total,
+                     uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags, uint64_t* stats,
+                     char* ws, hipStream_t st) {
   const u64 G = lg->G, M = in->M;
-  QB_REQUIRE(G < (1ull << 32) && M < (1ull << 32), "qb_dev_leader_step: G and M must be < 2^32");
-  QB_REQUIRE(lg->inflight_cap >= 1 && lg->inflight_cap <= 4096,
-             "qb_dev_leader_step: inflight_cap must be 1..4096");
-  QB_REQUIRE(lg->readq_cap <= QB_LEADER_MAX_READQ, "qb_dev_leader_step: readq_cap must be 0..16");
-  QB_REQUIRE(msg_total && stats, "qb_dev_leader_step: msg_total and stats are required");
-  if (G == 0) return QB_OK;
-  QB_REQUIRE(lg->off && lg->cfg && lg->meta && lg->term && lg->committed && lg->first_index &&
-                 lg->last_index && lg->snap_index && lg->snap_term && lg->max_ents &&
-                 lg->run_start && lg->run_term && lg->match && lg->next &&
-                 lg->pending_snapshot && lg->pstate && lg->infl_pos && lg->infl_buf,
-             "qb_dev_leader_step: a required group/progress array is NULL");
-  QB_REQUIRE(lg->readq_cap == 0 || (lg->rq_ctx && lg->rq_index && lg->rq_meta),
-             "qb_dev_leader_step: read queue arrays are required when readq_cap > 0");
-  QB_REQUIRE(M == 0 || (in->group && in->flags && in->index && in->term),
-             "qb_dev_leader_step: inbox group/flags/index/term are required");
-  QB_REQUIRE(msg_cap == 0 || msgs, "qb_dev_leader_step: msgs is NULL");
-  const ld::Carve c = ld::carve(G, M);
-  QB_REQUIRE(workspace && workspace_bytes >= c.total,
-             "qb_dev_leader_step: workspace needs %zu bytes", c.total);
-  hipStream_t st = as_stream(stream);
-  char* ws = static_cast<char*>(workspace);
   u32* cnt = reinterpret_cast<u32*>(ws + c.cnt);
   u32* bsum = reinterpret_cast<u32*>(ws + c.bsum);
   u32* perm = reinterpret_cast<u32*>(ws + c.perm);
   const ld::RecCols rcols{reinterpret_cast<u8*>(ws + c.rflags), reinterpret_cast<u64*>(ws + c.rterm),
                        reinterpret_cast<u64*>(ws + c.rindex), reinterpret_cast<u64*>(ws + c.rhint),
                        reinterpret_cast<u64*>(ws + c.rlt)};
-  u32* mcnt = reinterpret_cast<u32*>(ws + c.mcnt);
-  u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
   u32* pool = reinterpret_cast<u32*>(ws + c.pool);
   u64* shards = reinterpret_cast<u64*>(ws + c.shards);
   // pool and stat shards are adjacent in the carve: one memset zeroes both
@@ -1322,25 +1319,94 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   A.cnt = cnt;
   A.perm = perm;
   A.rec = rcols;
-  A.mcnt = mcnt;
-  A.fix = reinterpret_cast<ld::Msg*>(ws + c.fix);
-  A.chead = reinterpret_cast<u32*>(ws + c.chead);
-  A.cnext = reinterpret_cast<u32*>(ws + c.cnext);
-  A.chunks = reinterpret_cast<ld::Msg*>(ws + c.chunks);
+  A.mcnt = sink->count;
+  A.fix = sink->fix;
+  A.chead = sink->chead;
+  A.cnext = sink->cnext;
+  A.chunks = sink->chunks;
   A.pool = pool;
-  A.nchunks = c.nchunks;
+  A.nchunks = sink->nchunks;
   A.shards = shards;
   A.stepdown_at = stepdown_at;
   A.gflags = gflags;
   hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
   QB_CHECK_LAUNCH("k_ld_step");
-  scan::launch(mcnt, G, mbsum, st);
-  QB_CHECK_LAUNCH("scan(messages)");
-  hipLaunchKernelGGL(ld::k_ld_emit, dim3(grid_for(G)), dim3(kBlock), 0, st, G, mcnt, A.fix,
-                     A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
-                     msg_cap, msg_off, ld::U(msg_total), shards);
-  QB_CHECK_LAUNCH("k_ld_emit");
-  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64 * QB_LSTAT_COUNT), 0, st, shards, bshards, ld::U(stats));
+  if (msg_total) {  // the group-ordered array: scan of the counts, then the copy
+    u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
+    scan::launch(sink->count, G, mbsum, st);
+    QB_CHECK_LAUNCH("scan(messages)");
+    hipLaunchKernelGGL(ld::k_ld_emit, dim3(grid_for(G)), dim3(kBlock), 0, st, G, sink->count, A.fix,
+                       A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
+                       msg_cap, msg_off, ld::U(msg_total), shards);
+    QB_CHECK_LAUNCH("k_ld_emit");
+  }
+  hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64 * QB_LSTAT_COUNT), 0, st, shards, bshards,
+                     ld::U(stats), pool, sink->chunks_used);
   QB_CHECK_LAUNCH("k_ld_fold");
   return QB_OK;
+}
+
+int leader_check(const qb_leader_groups* lg, const qb_leader_inbox* in, uint64_t* stats) {
+  QB_REQUIRE(lg && in, "qb_dev_leader_step: lg and in are required");
+  const u64 G = lg->G, M = in->M;
+  QB_REQUIRE(G < (1ull << 32) && M < (1ull << 32), "qb_dev_leader_step: G and M must be < 2^32");
+  QB_REQUIRE(lg->inflight_cap >= 1 && lg->inflight_cap <= 4096,
+             "qb_dev_leader_step: inflight_cap must be 1..4096");
+  QB_REQUIRE(lg->readq_cap <= QB_LEADER_MAX_READQ, "qb_dev_leader_step: readq_cap must be 0..16");
+  QB_REQUIRE(stats, "qb_dev_leader_step: stats is required");
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(lg->off && lg->cfg && lg->meta && lg->term && lg->committed && lg->first_index &&
+                 lg->last_index && lg->snap_index && lg->snap_term && lg->max_ents &&
+                 lg->run_start && lg->run_term && lg->match && lg->next &&
+                 lg->pending_snapshot && lg->pstate && lg->infl_pos && lg->infl_buf,
+             "qb_dev_leader_step: a required group/progress array is NULL");
+  QB_REQUIRE(lg->readq_cap == 0 || (lg->rq_ctx && lg->rq_index && lg->rq_meta),
+             "qb_dev_leader_step: read queue arrays are required when readq_cap > 0");
+  QB_REQUIRE(M == 0 || (in->group && in->flags && in->index && in->term),
+             "qb_dev_leader_step: inbox group/flags/index/term are required");
+  return QB_OK;
+}
+
+}  // namespace
+
+extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
+                                  qb_msg_out* msgs, uint64_t msg_cap, uint64_t* msg_total,
+                                  uint32_t* msg_off, uint32_t* stepdown_at, uint8_t* gflags,
+                                  uint64_t* stats, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  QB_REQUIRE(msg_total, "qb_dev_leader_step: msg_total is required");
+  const int rc = leader_check(lg, in, stats);
+  if (rc != QB_OK || lg->G == 0) return rc;
+  QB_REQUIRE(msg_cap == 0 || msgs, "qb_dev_leader_step: msgs is NULL");
+  const ld::Carve c = ld::carve(lg->G, in->M);
+  QB_REQUIRE(workspace && workspace_bytes >= c.total,
+             "qb_dev_leader_step: workspace needs %zu bytes", c.total);
+  char* ws = static_cast<char*>(workspace);
+  const MsgSink sink{reinterpret_cast<ld::Msg*>(ws + c.fix), reinterpret_cast<u32*>(ws + c.mcnt),
+                     reinterpret_cast<u32*>(ws + c.chead), reinterpret_cast<u32*>(ws + c.cnext),
+                     reinterpret_cast<ld::Msg*>(ws + c.chunks), c.nchunks, nullptr};
+  return leader_step_impl(lg, in, c, &sink, msgs, msg_cap, msg_total, msg_off, stepdown_at, gflags,
+                          stats, ws, as_stream(stream));
+}
+
+extern "C" int qb_dev_leader_step_outbox(const qb_leader_groups* lg, const qb_leader_inbox* in,
+                                         const qb_leader_outbox* out, uint32_t* stepdown_at,
+                                         uint8_t* gflags, uint64_t* stats, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
+  QB_REQUIRE(out, "qb_dev_leader_step_outbox: out is required");
+  const int rc = leader_check(lg, in, stats);
+  if (rc != QB_OK || lg->G == 0) return rc;
+  QB_REQUIRE(out->slots && out->count && out->chunk_head && out->chunks_used,
+             "qb_dev_leader_step_outbox: slots, count, chunk_head and chunks_used are required");
+  QB_REQUIRE(out->nchunks == 0 || (out->chunks && out->chunk_next),
+             "qb_dev_leader_step_outbox: chunks / chunk_next are required when nchunks > 0");
+  QB_REQUIRE(out->nchunks < (1ull << 32), "qb_dev_leader_step_outbox: nchunks must be < 2^32");
+  const ld::Carve c = ld::carve(lg->G, in->M, /*outbox=*/true);
+  QB_REQUIRE(workspace && workspace_bytes >= c.total,
+             "qb_dev_leader_step_outbox: workspace needs %zu bytes", c.total);
+  const MsgSink sink{reinterpret_cast<ld::Msg*>(out->slots), out->count, out->chunk_head,
+                     out->chunk_next, reinterpret_cast<ld::Msg*>(out->chunks), out->nchunks,
+                     out->chunks_used};
+  return leader_step_impl(lg, in, c, &sink, nullptr, 0, nullptr, nullptr, stepdown_at, gflags,
+                          stats, static_cast<char*>(workspace), as_stream(stream));
 }

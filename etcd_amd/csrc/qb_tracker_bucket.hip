@@ -187,10 +187,8 @@ __device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec
 // payload then goes register -> LDS -> permuted LDS read -> coalesced store.
 constexpr int kPer = kTile / kPartThreads;  // records per thread
 // Compact records (the tracker steps) go from registers straight to their
-// sorted LDS slot in K3 and K4 (QB_DIRECT; 0 = the permutation walk, A/B).
-#ifndef QB_DIRECT
-#define QB_DIRECT 1
-#endif
+// sorted LDS slot in K3 and K4 (round 3: K3 115 -> 112, K4 65 -> 61 us
+// against the permutation walk the wide columns still use).
 
 // (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs: the
 // direct placement's registers would otherwise leave one)
@@ -265,7 +263,7 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
   }
   __syncthreads();
-  if (QB_DIRECT && out.compact) {
+  if (out.compact) {
     // compact records: bin, rank and the encoded record stay in registers;
     // after the scan each record is stored at its sorted LDS slot with its
     // bin and chunk-low, and the output pass reads the slots in order
@@ -513,7 +511,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
-  if (QB_DIRECT && in.compact) {
+  if (in.compact) {
     // compact records: each record's rank stays in a register and the record
     // goes straight to its sorted LDS slot after the scan, so the output is
     // read in order (no permutation array, no bin / rank stores)
@@ -575,10 +573,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 // K4 for compact records (the tracker steps) in its own kernel: only the
 // staged records and the chunk counters in LDS (33 KB instead of the shared
 // tile's 61 KB) and 512 threads of 8 records, so four parts run per CU
-// instead of two (QB_K4C = 0: the shared kernel above).
-#ifndef QB_K4C
-#define QB_K4C 1
-#endif
+// instead of two (round 3: fixed tick 583.5 -> 572.2 us).
 constexpr int kSplitThreads = 512;
 constexpr int kSplitPer = kTile / kSplitThreads;
 __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
@@ -638,33 +633,18 @@ __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
 // batch in batch order (the exact two-pass form of qb_tracker.hip).
 // LDS: acc_match[n][CH] u64, acc_next[n][CH] u64 (if tracked), gterm[CH] u64,
 // act[CH] u32.
-// K5 threads per workgroup (QB_K5_BLOCK, at most the chunk's group count).
-#ifndef QB_K5_BLOCK
-#define QB_K5_BLOCK 512
-#endif
+// K5 threads per workgroup: 512, at most the chunk's group count (round 2:
+// 512-thread workgroups, one group per thread, -12 us per tick).
 __host__ __device__ constexpr u32 k5_block(int n) {
-  return chunk_groups(u32(n)) < u32(QB_K5_BLOCK) ? chunk_groups(u32(n)) : u32(QB_K5_BLOCK);
+  return chunk_groups(u32(n)) < 512u ? chunk_groups(u32(n)) : 512u;
 }
 
 // SGPR cap: the hardware admits min(8, 800 / (ceil(sgpr / 16) * 16 + 16))
 // waves per SIMD (MI355X_MICROARCH.md, residency), so the compiler's 92
 // SGPRs held K5 at 3 workgroups per CU where its VGPRs and LDS allow 4;
 // capped at 80 (a few SGPRs spill to VGPR lanes): -11 us per 16M-group tick.
-#ifndef QB_K5_SGPR
-#define QB_K5_SGPR 80
-#endif
-#ifndef QB_K5_WAVES
-#define QB_K5_WAVES 0  // 0: the compiler's choice; else a VGPR cap (amdgpu_num_vgpr, A/B knob)
-#endif
 template <int N, bool NEXT>
-__global__ __launch_bounds__(k5_block(N))
-#if QB_K5_WAVES > 0
-__attribute__((amdgpu_num_vgpr(QB_K5_WAVES)))
-#endif
-#if QB_K5_SGPR > 0
-__attribute__((amdgpu_num_sgpr(QB_K5_SGPR)))
-#endif
-void k_bk_apply(
+__global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
     const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
@@ -681,12 +661,9 @@ void k_bk_apply(
   __shared__ u64 gterm[CH];
   __shared__ u32 act[CH];
   __shared__ u32 slow;
-#ifndef QB_K5_REV
-#define QB_K5_REV 1
-#endif
-  // Chunks in reverse order (QB_K5_REV): K4 wrote the last super-buckets
-  // last, so their runs are the ones still in the 256 MB MALL when K5 starts.
-  const u32 c = QB_K5_REV ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
+  // Chunks in reverse order: K4 wrote the last super-buckets last, so their
+  // runs are the ones still in the 256 MB MALL when K5 starts.
+  const u32 c = gridDim.x - 1u - blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   // Load order: the group terms and this chunk's run table first, then the
@@ -736,7 +713,7 @@ void k_bk_apply(
   // loaded before the first is classified.
   u32 total = rt.finish(rq);
   __syncthreads();
-  constexpr int kRecPer = int(QB_K5_INFLIGHT / B);  // records in flight per workgroup
+  constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
   // branch-free (clamped; an empty chunk reads record 0, which exists)
@@ -827,10 +804,8 @@ void k_bk_apply(
     const int slot[3] = {QB_STAT_STALE_TERM, QB_STAT_APPLIED, QB_STAT_REJECTED};
     BlockTally<3>::publish(tl, shard_of(shards), slot);
   }
-  // maybeCommit for every group of the chunk + write-back (coalesced rows).
-  // Write-back granularity (QB_K5_FULL): a store only where the value
-  // changed leaves partially written lines; 2 = a wave whose segment of a
-  // row (or of committed / active) changed anywhere stores the whole segment.
+  // maybeCommit for every group of the chunk + write-back (coalesced rows,
+  // whole wave segments: segment_any, qb_bucket.h).
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
     const u32 lg = threadIdx.x + k * B;
@@ -841,8 +816,7 @@ void k_bk_apply(
       const u64 a = acc_m[s * CH + lg];
       const bool up = live && a > v[k][s];
       if (up) v[k][s] = a;
-      if (QB_K5_FULL >= 2 ? (granule_any<QB_WB_GRAN>(up, g) && live) : up)
-        match[u64(s) * geo.G + g] = v[k][s];
+      if (segment_any(up) && live) match[u64(s) * geo.G + g] = v[k][s];
       if constexpr (NEXT) {
         if (live) {
           u64* q = next + u64(s) * geo.G + g;
@@ -854,11 +828,9 @@ void k_bk_apply(
     const u64 ci = select_quorum<N>(v[k]);
     const bool adv = live && ci > cm[k] && ci >= ts[k];  // log.go:328-334
     const u32 na = live ? act[lg] : 0u;
-    if (QB_K5_FULL >= 1 ? (granule_any<QB_WB_GRAN>(adv, g) && live) : adv)
-      committed[g] = adv ? ci : cm[k];
+    if (segment_any(adv) && live) committed[g] = adv ? ci : cm[k];
     if (advanced && live) advanced[g] = adv ? 1 : 0;
-    if (QB_K5_FULL >= 1 ? (granule_any<4 * QB_WB_GRAN>(na != 0, g) && live) : na != 0)
-      active[g] = u16(av[k] | na);
+    if (segment_any(na != 0) && live) active[g] = u16(av[k] | na);
   }
 }
 
@@ -957,7 +929,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   hipLaunchKernelGGL(k_bk_scatter, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st, geo,
                      rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1);
   QB_CHECK_LAUNCH("k_bk_scatter");
-  if (QB_K4C && compact)
+  if (compact)
     hipLaunchKernelGGL(k_bk_split_compact, dim3(unsigned(max_parts(geo))), dim3(kSplitThreads), 0,
                        st, geo, hist, bsum, pt, buf1, buf2, cs);
   else

@@ -39,16 +39,11 @@ namespace qb {
 namespace bk {
 
 // Threads per workgroup, and LDS slots per group of the first launch's run
-// buffer; compile-time knobs for A/B builds, the defaults are the measured
-// choice.
-#ifndef QB_CSR_BLOCK
-#define QB_CSR_BLOCK 512
-#endif
-#ifndef QB_CSR_CAPW
-#define QB_CSR_CAPW 8
-#endif
+// buffer (the measured choice: round 2, profiles/r02/ab_csr_*.log).
+constexpr u32 kCsrBlock = 512;
+constexpr int kCsrCapW = 8;
 __host__ __device__ constexpr u32 csr_block() {
-  return csr_chunk_groups(16) < u32(QB_CSR_BLOCK) ? csr_chunk_groups(16) : u32(QB_CSR_BLOCK);
+  return csr_chunk_groups(16) < kCsrBlock ? csr_chunk_groups(16) : kCsrBlock;
 }
 constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the first launch
 
@@ -65,9 +60,6 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
   geo, recs, pt, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
       stepdown_at, advanced, chunk_slow, any_slow, shards
 
-#ifndef QB_CSR_EARLY
-#define QB_CSR_EARLY 1
-#endif
 // One chunk c (the whole workgroup).
 template <int WMAX, int CAPW, bool NEXT, bool SECOND>
 __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS) {
@@ -111,7 +103,6 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
   const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
-#if QB_CSR_EARLY
   // The old slot run and the commit inputs depend only on the chunk's first
   // and last offsets (uniform loads): issued now, in the same round trip as
   // the offsets and the run table, instead of after the first barrier (one
@@ -120,6 +111,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   const bool fits = run <= CAP;
   u64 old[PER];
   {
+    // (slots past the run re-read its last slot; an oversize run stays in
+    // HBM: its lanes re-read the first slot; an empty run has no slot and
+    // reads the chunk's first group term instead — a select, not a branch,
+    // which would cost the exact wait counts)
     const u64* src = run ? match + a0 : group_term + g0;
     const u32 last = run && fits ? run - 1u : 0u;
 #pragma unroll
@@ -139,7 +134,6 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     cf[k] = cfg[g];
     av[k] = active[g];
   }
-#endif
   for (u32 k = threadIdx.x; k < CAP; k += B) {
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
@@ -157,52 +151,20 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
   for (u32 k = threadIdx.x; k < CH; k += B) act[k] = 0;
   __syncthreads();
-#if !QB_CSR_EARLY
-  const u32 a0 = offs[0], run = offs[CH] - a0;
-#endif
   // A run longer than the buffer: when a second launch exists (CAPW < WMAX)
   // the first defers the chunk to it; otherwise (CAPW == WMAX, and in the
   // second launch) only a table breaking its max_slots bound gets here, and
   // the chunk takes the slow path (exact per-record semantics, global
   // atomics) — no chunk is left deferred without a launch to apply it.
-#if !QB_CSR_EARLY
-  const bool fits = run <= CAP;
-#endif
   if constexpr (!SECOND && CAPW < WMAX) {
     if (!fits) {  // block-uniform, before anything is written
       if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
       return;
     }
   }
-  // the old slot run (slots past the run re-read its last slot) and the
-  // commit-phase inputs of this thread's groups
-  // (an oversize run stays in HBM: its lanes re-read the first slot; an
-  // empty run has no slot to read and reads the chunk's first group term
-  // instead — a select, not a branch, which would cost the exact wait counts)
-#if !QB_CSR_EARLY
-  u64 old[PER];
-  const u64* src = run ? match + a0 : group_term + g0;
-  const u32 last = run && fits ? run - 1u : 0u;
-#pragma unroll
-  for (u32 p = 0; p < PER; ++p) {
-    const u32 j = threadIdx.x + p * B;
-    old[p] = src[j < last ? j : last];
-  }
-  u64 cm[GPT], ts[GPT];
-  u32 cf[GPT], av[GPT];  // av: RecentActive's read-modify-write reads early
-#pragma unroll
-  for (u32 k = 0; k < GPT; ++k) {
-    const u32 lg = threadIdx.x + k * B;
-    const u64 g = g0 + (lg < ng ? lg : ng - 1);
-    cm[k] = committed[g];
-    ts[k] = term_start[g];
-    cf[k] = cfg[g];
-    av[k] = active[g];
-  }
-#endif
   u32 total = rtab.finish(rq);
   __syncthreads();
-  constexpr int kRecPer = int(QB_K5_INFLIGHT / B);  // records in flight per workgroup
+  constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
   auto load = [&](u32 f0, u32 n) {
@@ -297,10 +259,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       const u64 a = acc[j];
       const bool up = a > old[p];
       if (up) old[p] = a;
-      // QB_CSR_FULL (as QB_K5_FULL): whole wave segments where any slot
-      // changed — neutral in round 2, 12 us faster per 16M-group tick with
-      // the compact records (profiles/r03/k5_variants/)
-      if (QB_CSR_FULL >= 2 ? granule_any<QB_WB_GRAN>(up, a0 + j) : up) match[a0 + j] = old[p];
+      // whole wave segments where any slot changed (segment_any, qb_bucket.h):
+      // neutral in round 2, 12 us faster per 16M-group tick with the compact
+      // records (profiles/r03/k5_variants/)
+      if (segment_any(up)) match[a0 + j] = old[p];
       acc[j] = old[p];
       if constexpr (NEXT) {
         const u64 nn = accn[j];
@@ -327,11 +289,10 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     // log.go:328-334; an empty config's ci = MaxUint64 is past lastIndex,
     // whose term is 0 (log.go:271-273): never committed
     const bool adv = ci != kInf && ci > cm[k] && ci >= ts[k];
-    if (QB_CSR_FULL >= 1 ? granule_any<QB_WB_GRAN>(adv, g) : adv) committed[g] = adv ? ci : cm[k];
+    if (segment_any(adv)) committed[g] = adv ? ci : cm[k];
     if (advanced) advanced[g] = adv ? 1 : 0;
     const u32 na = act[lg];
-    if (QB_CSR_FULL >= 1 ? granule_any<4 * QB_WB_GRAN>(na != 0, g) : na != 0)
-      active[g] = u16(av[k] | na);
+    if (segment_any(na != 0)) active[g] = u16(av[k] | na);
   }
 }
 
@@ -378,7 +339,7 @@ struct CsrStepArgs {
 template <int WMAX, bool SECOND>
 void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                   const CsrStepArgs& a, hipStream_t st) {
-  constexpr int CAPW = SECOND ? WMAX : (WMAX < QB_CSR_CAPW ? WMAX : QB_CSR_CAPW);
+  constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX> : k_csr_apply<WMAX, CAPW, NX>), \
@@ -395,7 +356,7 @@ template <int WMAX>
 void launch_csr_step(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
                      const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
   launch_apply<WMAX, false>(geo, recs, pt, cs, a, st);
-  if constexpr (WMAX > QB_CSR_CAPW) launch_apply<WMAX, true>(geo, recs, pt, cs, a, st);
+  if constexpr (WMAX > kCsrCapW) launch_apply<WMAX, true>(geo, recs, pt, cs, a, st);
   hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
                      CsrLay<WMAX>{a.off, a.cfg}, sa.rg, sa.rf, sa.ri, sa.rt, a.gt, a.ts,
                      a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,

@@ -54,6 +54,16 @@ class LeaderGroupsC(C.Structure):
                           "rq_index", "rq_meta")]
 
 
+OUTBOX_SLOTS = 8    # QB_LEADER_OUTBOX_SLOTS
+OUTBOX_CHUNK = 32   # QB_LEADER_OUTBOX_CHUNK
+
+
+class LeaderOutboxC(C.Structure):
+    """struct qb_leader_outbox (include/quorum_batch.h)."""
+    _fields_ = [("slots", _P), ("count", _P), ("chunk_head", _P), ("chunk_next", _P),
+                ("chunks", _P), ("nchunks", C.c_uint64), ("chunks_used", _P)]
+
+
 class LeaderInboxC(C.Structure):
     """struct qb_leader_inbox."""
     _fields_ = [("M", C.c_uint64)] + [(n, _P) for n in ("group", "flags", "index", "term", "hint",
@@ -198,6 +208,78 @@ class LeaderGroups:
             stepdown_at=_to_np(out["stepdown"], np.uint32, self.G),
             gflags=_to_np(out["gflags"], np.uint8, self.G),
             stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)})
+
+    def step_outbox(self, inbox: LeaderInbox, nchunks: Optional[int] = None,
+                    stats: Optional[torch.Tensor] = None, fetch: bool = True):
+        """One batch through qb_dev_leader_step_outbox: the messages stay in
+        the per-group outbox (8 k-major slots per group + 32-message overflow
+        chunks) the step writes them to.  fetch: a LeaderStepResult with the
+        outbox read back into group order on the host (msg_total = messages
+        stored); else the device outbox dict and stats."""
+        lib = _lib.load()
+        M, G, dev = inbox.M, self.G, self.device
+        need = lib.qb_leader_outbox_workspace_bytes(G, M)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=dev)
+        if nchunks is None:
+            nchunks = M // 8 + 1024
+        ob = self._outbox(nchunks)
+        if stats is None:
+            stats = torch.zeros(8, dtype=torch.int64, device=dev)
+        ls = self._struct()
+        ib = LeaderInboxC(M=M, group=inbox.group.data_ptr(), flags=inbox.flags.data_ptr(),
+                          index=inbox.index.data_ptr(), term=inbox.term.data_ptr(),
+                          hint=inbox.hint.data_ptr(), log_term=inbox.log_term.data_ptr())
+        oc = LeaderOutboxC(slots=ob["slots"].data_ptr(), count=ob["count"].data_ptr(),
+                           chunk_head=ob["chunk_head"].data_ptr(),
+                           chunk_next=ob["chunk_next"].data_ptr() if nchunks else None,
+                           chunks=ob["chunks"].data_ptr() if nchunks else None, nchunks=nchunks,
+                           chunks_used=ob["chunks_used"].data_ptr())
+        _lib.call("qb_dev_leader_step_outbox", C.byref(ls), C.byref(ib), C.byref(oc),
+                  ob["stepdown"].data_ptr(), ob["gflags"].data_ptr(), stats.data_ptr(),
+                  self._ws.data_ptr(), self._ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
+        if not fetch:
+            return ob, stats
+        cnt = _to_np(ob["count"], np.uint32, G).astype(np.int64)
+        slots = ob["slots"].cpu().numpy().view(MSG_DTYPE).reshape(OUTBOX_SLOTS, G)
+        chunks = ob["chunks"].cpu().numpy().view(MSG_DTYPE) if nchunks else None
+        head = _to_np(ob["chunk_head"], np.uint32, G)
+        nxt = _to_np(ob["chunk_next"], np.uint32, nchunks) if nchunks else None
+        off = np.zeros(G + 1, np.int64)
+        off[1:] = np.cumsum(cnt)
+        msgs = np.empty(int(off[-1]), MSG_DTYPE)
+        for k in range(OUTBOX_SLOTS):        # row k of every group with > k messages
+            sel = np.nonzero(cnt > k)[0]
+            msgs[off[sel] + k] = slots[k, sel]
+        for g in np.nonzero(cnt > OUTBOX_SLOTS)[0]:   # the overflow chains (rare)
+            c = int(head[g])
+            for k in range(OUTBOX_SLOTS, int(cnt[g])):
+                j = k - OUTBOX_SLOTS
+                if j and j % OUTBOX_CHUNK == 0:
+                    c = int(nxt[c])
+                msgs[off[g] + k] = chunks[c * OUTBOX_CHUNK + j % OUTBOX_CHUNK]
+        st = stats.cpu().tolist()
+        return LeaderStepResult(
+            msgs=msgs, msg_total=int(off[-1]), msg_off=off.astype(np.uint32),
+            stepdown_at=_to_np(ob["stepdown"], np.uint32, G),
+            gflags=_to_np(ob["gflags"], np.uint8, G),
+            stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)})
+
+    def _outbox(self, nchunks: int):
+        dev, G = self.device, self.G
+        key = ("outbox", nchunks)
+        if getattr(self, "_ob_key", None) != key:
+            self._ob = {"slots": torch.empty(OUTBOX_SLOTS * G * 40, dtype=torch.uint8, device=dev),
+                        "count": torch.zeros(G, dtype=torch.int32, device=dev),
+                        "chunk_head": torch.zeros(G, dtype=torch.int32, device=dev),
+                        "chunk_next": torch.zeros(max(nchunks, 1), dtype=torch.int32, device=dev),
+                        "chunks": torch.empty(max(nchunks, 1) * OUTBOX_CHUNK * 40, dtype=torch.uint8,
+                                              device=dev),
+                        "chunks_used": torch.zeros(1, dtype=torch.int32, device=dev),
+                        "stepdown": torch.zeros(G, dtype=torch.int32, device=dev),
+                        "gflags": torch.zeros(G, dtype=torch.uint8, device=dev)}
+            self._ob_key = key
+        return self._ob
 
     def _outputs(self, msg_cap: int):
         dev = self.device

@@ -573,6 +573,37 @@ int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
                        uint64_t* stats, void* workspace, size_t workspace_bytes,
                        void* stream);
 
+/* The same step with the messages left where the step writes them, in a
+ * per-group outbox — the reference's per-node r.msgs slice (raft.go:393-420
+ * r.send appends to it; Ready.Messages hands it over, node.go:573) as an
+ * 8-message array per group plus an overflow list — instead of one
+ * group-ordered array (qb_dev_leader_step compacts them in a second pass:
+ * a scan of the counts, then every message read and written again).  Group
+ * g's k-th message is slots[k * G + g] for k < QB_LEADER_OUTBOX_SLOTS; the
+ * ones past it continue in QB_LEADER_OUTBOX_CHUNK-message chunks drawn from
+ * chunks[] (chunk c holds chunks[c * 32 .. c * 32 + 31]; chunk_head[g] is
+ * g's first chunk, chunk_next[c] the next), in the order the reference
+ * emits them.  count[g] = messages stored for g (a group whose chunk could
+ * not be drawn — all nchunks used — stops there; the rest is counted in
+ * QB_LSTAT_MSGS_DROPPED); *chunks_used (device u32) = chunks drawn.
+ * stepdown_at / gflags / stats as qb_dev_leader_step. */
+#define QB_LEADER_OUTBOX_SLOTS 8
+#define QB_LEADER_OUTBOX_CHUNK 32
+typedef struct qb_leader_outbox {
+  qb_msg_out* slots;    /* [QB_LEADER_OUTBOX_SLOTS * G], k-major             */
+  uint32_t* count;      /* [G] messages per group                            */
+  uint32_t* chunk_head; /* [G] (meaningful where count > 8)                  */
+  uint32_t* chunk_next; /* [nchunks]                                         */
+  qb_msg_out* chunks;   /* [nchunks * QB_LEADER_OUTBOX_CHUNK]                */
+  uint64_t nchunks;     /* 0: no overflow (messages past the 8th dropped)    */
+  uint32_t* chunks_used; /* device u32                                       */
+} qb_leader_outbox;
+size_t qb_leader_outbox_workspace_bytes(uint64_t G, uint64_t M);
+int qb_dev_leader_step_outbox(const qb_leader_groups* lg, const qb_leader_inbox* in,
+                              const qb_leader_outbox* out, uint32_t* stepdown_at,
+                              uint8_t* gflags, uint64_t* stats, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
 /* ----------------------------------------------------------------------- */
 /* Wire ingest                                       */
 /* ----------------------------------------------------------------------- */

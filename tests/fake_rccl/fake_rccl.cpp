@@ -77,6 +77,13 @@ struct World {
   // point-to-point: mailbox[(s, d, seq)], seq = the k-th send s -> d overall
   std::map<std::tuple<int, int, uint64_t>, Mail> mail;
   std::map<std::pair<int, int>, uint64_t> sent, received;
+  // point-to-point events live as long as the world (a peer may still
+  // enqueue a wait on one after its owner's rank has returned): destroyed
+  // with the last communicator
+  std::vector<hipEvent_t> events;
+  ~World() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
 
   // every rank calls; returns after all n have arrived (a reusable barrier)
   void barrier() {
@@ -115,7 +122,6 @@ constexpr auto kP2pTimeout = std::chrono::seconds(60);
 struct ncclComm {
   std::shared_ptr<World> w;
   int rank;
-  std::vector<hipEvent_t> events;  // this rank's p2p events, freed at destroy
 };
 
 namespace {
@@ -232,8 +238,11 @@ ncclResult_t run_p2p(ncclComm_t c, const std::vector<Op>& ops) {
   if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess)
     return ncclUnhandledCudaError;
-  c->events.push_back(ready);
-  c->events.push_back(done);
+  {
+    std::lock_guard<std::mutex> lk(w.mu);
+    w.events.push_back(ready);
+    w.events.push_back(done);
+  }
   if (hipEventRecord(ready, st) != hipSuccess) return ncclUnhandledCudaError;
   std::vector<std::tuple<int, int, uint64_t>> my_sends, my_recvs;
   {
@@ -353,10 +362,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
-  if (comm) {
-    for (hipEvent_t e : comm->events) (void)hipEventDestroy(e);
-  }
-  delete comm;
+  delete comm;  // the world (and its events) goes with the last communicator
   return ncclSuccess;
 }
 

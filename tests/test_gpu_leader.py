@@ -69,7 +69,7 @@ def test_reference_scenarios_on_device(sc):
 
 
 def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_groups=0,
-          hot_frac=0.0, term_base=0, options=0):
+          hot_frac=0.0, term_base=0, options=0, outbox=False):
     rng = np.random.default_rng(seed)
     groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots, term_base)
     for g in groups:
@@ -77,7 +77,7 @@ def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_gro
     recs = LP.random_records(rng, groups, M, hot_groups=hot_groups, hot_frac=hot_frac)
     eng = _engine(groups, inflight_cap, readq_cap, read_only)
     eng.options = options
-    res = eng.step(_inbox(recs))
+    res = eng.step_outbox(_inbox(recs)) if outbox else eng.step(_inbox(recs))
     orc = copy.deepcopy(groups)
     for g in orc:
         g.msgs = []
@@ -141,6 +141,42 @@ def test_fuzz_atomic_grouping():
     _fuzz(31, G=3000, M=9000, inflight_cap=6, readq_cap=3, max_slots=16, options=1)
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_fuzz_outbox(seed):
+    """qb_dev_leader_step_outbox: the same step with the messages left in the
+    per-group outbox (8 k-major slots + overflow chunks), read back in group
+    order — identical to the oracle (and so to qb_dev_leader_step)."""
+    _fuzz(seed, G=400, M=1500, inflight_cap=3, readq_cap=4, outbox=True)
+
+
+def test_fuzz_outbox_overflow_chunks():
+    """Hot groups emit far more than 8 messages in one batch: the outbox's
+    overflow chains (32-message chunks) hold the rest, in emission order."""
+    _fuzz(41, G=600, M=2000, inflight_cap=6, readq_cap=3, hot_groups=2, hot_frac=0.1, outbox=True)
+    _fuzz(42, G=300, M=5000, inflight_cap=6, readq_cap=3, hot_groups=3, hot_frac=0.5, outbox=True)
+
+
+def test_outbox_without_chunks_keeps_eight_per_group():
+    """nchunks = 0: a group keeps its first 8 messages and the rest is
+    counted as dropped (QB_LSTAT_MSGS_DROPPED), every other output exact."""
+    rng = np.random.default_rng(43)
+    groups = LP.random_groups(rng, 300, 6, 3, 9, 0)
+    recs = LP.random_records(rng, groups, 5000, hot_groups=3, hot_frac=0.5)
+    eng = _engine(groups, 6, 3)
+    res = eng.step_outbox(_inbox(recs), nchunks=0)
+    orc = copy.deepcopy(groups)
+    for g in orc:
+        g.msgs = []
+    L.run_batch(orc, recs)
+    want = []
+    for gi, g in enumerate(orc):
+        want += [(gi,) + m.key() for m in g.msgs[:8]]
+    assert _dev_msgs(res) == want
+    total = sum(len(g.msgs) for g in orc)
+    assert total > len(want)
+    assert res.stats["msgs"] == total and res.stats["msgs_dropped"] == total - len(want)
+
+
 def test_empty_batch_and_truncated_output():
     rng = np.random.default_rng(5)
     groups = LP.random_groups(rng, 50, 4, 2)
@@ -160,9 +196,11 @@ def test_empty_batch_and_truncated_output():
     assert res.stats["msgs_dropped"] == len(om) - cap
 
 
-def test_streaming_workload_vs_c_oracle():
+@pytest.mark.parametrize("outbox", [False, True])
+def test_streaming_workload_vs_c_oracle(outbox):
     """The bench's streaming workload at 1M groups, six consecutive batches,
-    every state array and every message against the C oracle."""
+    every state array and every message against the C oracle (through the
+    group-ordered array and through the outbox)."""
     import torch
     from etcd_amd.quorum.leader import streaming_inbox, synth_streaming
     from tests import oracle_c as oc
@@ -171,7 +209,7 @@ def test_streaming_workload_vs_c_oracle():
     host = {k: v.copy() for k, v in lg.numpy().items()}
     for k in range(6):
         ib = streaming_inbox(G, base, k, device="cuda")
-        res = lg.step(ib, msg_cap=6 * G)
+        res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=6 * G)
         rec = {"group": ib.group.cpu().numpy().view(np.uint32),
                "flags": ib.flags.cpu().numpy(), "index": ib.index.cpu().numpy().view(np.uint64),
                "term": ib.term.cpu().numpy().view(np.uint64),
@@ -189,7 +227,8 @@ def test_streaming_workload_vs_c_oracle():
     torch.cuda.synchronize()
 
 
-def test_readindex_workload_vs_c_oracle():
+@pytest.mark.parametrize("outbox", [False, True])
+def test_readindex_workload_vs_c_oracle(outbox):
     """The ReadIndex bench workload (§8f row 2) at 256K groups: queues,
     released reads and every message against the C oracle."""
     from etcd_amd.quorum.leader import readindex_inbox, synth_readindex
@@ -198,7 +237,7 @@ def test_readindex_workload_vs_c_oracle():
     lg, last_ctx, _ = synth_readindex(G, Q, device="cuda")
     host = {k: v.copy() for k, v in lg.numpy().items()}
     ib = readindex_inbox(G, last_ctx, device="cuda")
-    res = lg.step(ib, msg_cap=8 * G)
+    res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=8 * G)
     rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
            "index": ib.index.cpu().numpy().view(np.uint64),
            "term": ib.term.cpu().numpy().view(np.uint64),

@@ -258,32 +258,50 @@ def leader_config(G, reps, warm=4, shuffle=True, *, reporter=None, gpu_only=None
     steps = warm + reps
     inboxes = [streaming_inbox(G, base, k, device=dev, shuffle=shuffle) for k in range(steps)]
     stats = torch.zeros(8, dtype=torch.int64, device=dev)
-    outs = []
-    for k in range(warm):
-        lg.step(inboxes[k], msg_cap=6 * G, stats=stats, fetch=False)
-    torch.cuda.synchronize()
-    stats.zero_()
     sp = torch.cuda.current_stream(dev).cuda_stream
-    ev = HipEvents(2)
-    ev.record(ev.ev[0], sp)
-    for k in range(warm, steps):
-        lg.step(inboxes[k], msg_cap=6 * G, stats=stats, fetch=False)
-    ev.record(ev.ev[1], sp)
-    torch.cuda.synchronize()
-    t = ev.elapsed_ms(0, 1) / 1e3 / reps
-    ev.close()
-    st = stats.cpu().tolist()
+    snap = {k: v.clone() for k, v in lg.t.items()}
+
+    def timed(step):
+        # the same start state and the same `steps` batches for each form
+        for k_, v_ in snap.items():
+            lg.t[k_].copy_(v_)
+        for k in range(warm):
+            step(inboxes[k])
+        torch.cuda.synchronize()
+        stats.zero_()
+        ev = HipEvents(2)
+        ev.record(ev.ev[0], sp)
+        for k in range(warm, steps):
+            step(inboxes[k])
+        ev.record(ev.ev[1], sp)
+        torch.cuda.synchronize()
+        dt = ev.elapsed_ms(0, 1) / 1e3 / reps
+        ev.close()
+        return dt, stats.cpu().tolist()
+    # the group-ordered array (qb_dev_leader_step: step, scan, copy) and the
+    # per-group outbox the step writes (qb_dev_leader_step_outbox)
+    t_ord, st = timed(lambda ib: lg.step(ib, msg_cap=6 * G, stats=stats, fetch=False))
+    t, st_ob = timed(lambda ib: lg.step_outbox(ib, stats=stats, fetch=False))
+    assert st_ob[6] == st[6], "outbox and ordered forms generated different message counts"
     msgs = st[6] / reps
     # per group-step: record 21 B; group state read 84 B (off 4, cfg 4, meta 4,
     # term/committed/first/last/snap/snap_term/max_ents 56, run 16) + commit
     # and meta written 12 B; 5 slots x (match, next, psnap 24 + pstate 1 +
     # infl_pos 4) read 145 B; the acking follower's freed window entry 8 B and
-    # match/next/pstate/infl_pos written 21 B; messages 40 B x 3 (stored,
-    # copied, written) per message; scans 16 B per group.
-    algo = G * (21 + 84 + 12 + 145 + 8 + 21 + 16) + msgs * 40 * 3
+    # match/next/pstate/infl_pos written 21 B; the record grouping's scan 8 B
+    # per group; messages: the outbox form writes each 40 B message once and
+    # a 4 B count per group; the ordered form stores, re-reads and writes
+    # each (40 B x 3) and scans the counts (8 B per group).
+    base = G * (21 + 84 + 12 + 145 + 8 + 21 + 8)
+    algo = base + G * 4 + msgs * 40
+    algo_ord = base + G * 8 + msgs * 40 * 3
+    ordered = {"ordered_us": t_ord * 1e6, "ordered_algo_bytes": algo_ord,
+               "ordered_frac": algo_ord / t_ord / 1e9 / HBM_PEAK_GBS,
+               "form": "qb_dev_leader_step_outbox (per-group outbox); ordered_* = "
+                       "qb_dev_leader_step (group-ordered array)"}
     if not shuffle or gpu_only:
         reporter("leader inbox step" + ("" if shuffle else ", records in group order (lab)"), G, t,
-               algo, {"unit": "group-steps/s", "msgs_per_step": msgs})
+                 algo, {"unit": "group-steps/s", "msgs_per_step": msgs, **ordered})
         return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
     # stepLeader loop one record at a time) on a bounded sample of the same
@@ -437,25 +455,37 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
     inboxes = [readindex_inbox(G, last_ctx, device=dev) for _ in range(reps + 2)]
     stats = torch.zeros(8, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
-    ev = HipEvents(2)
-    times = []
-    for k in range(reps + 2):
-        for name, t0 in pristine.items():
-            lg.t[name].copy_(t0)
-        if k == 2:
-            stats.zero_()
-        ev.record(ev.ev[0], sp)
-        lg.step(inboxes[k], msg_cap=8 * G, stats=stats, fetch=False)
-        ev.record(ev.ev[1], sp)
-        torch.cuda.synchronize()
-        if k >= 2:
-            times.append(ev.elapsed_ms(0, 1) / 1e3)
-    ev.close()
-    t = float(np.median(times))
-    st = stats.cpu().tolist()
+
+    def timed(step):
+        ev = HipEvents(2)
+        times = []
+        for k in range(reps + 2):
+            for name, t0 in pristine.items():
+                lg.t[name].copy_(t0)
+            if k == 2:
+                stats.zero_()
+            ev.record(ev.ev[0], sp)
+            step(inboxes[k])
+            ev.record(ev.ev[1], sp)
+            torch.cuda.synchronize()
+            if k >= 2:
+                times.append(ev.elapsed_ms(0, 1) / 1e3)
+        ev.close()
+        return float(np.median(times)), stats.cpu().tolist()
+    t_ord, st = timed(lambda ib: lg.step(ib, msg_cap=8 * G, stats=stats, fetch=False))
+    t, st_ob = timed(lambda ib: lg.step_outbox(ib, stats=stats, fetch=False))
+    assert st_ob[6] == st[6], "outbox and ordered forms generated different message counts"
     # per group-step: 2 records 2 x 21 B, group state 84 B, 5 slots x 29 B,
-    # read queue Q x 20 B read + written, Q messages x 40 B x 3
-    algo = G * (42 + 84 + 145 + Q * 20 * 2 + Q * 40 * 3)
+    # read queue Q x 20 B read + written, the grouping scan 8 B; Q messages:
+    # the outbox form 40 B each + a 4 B count per group, the ordered form
+    # 40 B x 3 + the count scan 8 B per group
+    base = G * (42 + 84 + 145 + Q * 20 * 2 + 8)
+    algo = base + G * (4 + Q * 40)
+    algo_ord = base + G * (8 + Q * 40 * 3)
+    ordered = {"ordered_us": t_ord * 1e6, "ordered_algo_bytes": algo_ord,
+               "ordered_frac": algo_ord / t_ord / 1e9 / HBM_PEAK_GBS,
+               "form": "qb_dev_leader_step_outbox (per-group outbox); ordered_* = "
+                       "qb_dev_leader_step (group-ordered array)"}
     # CheckQuorum: QuorumActive over 16M groups (cfg u32 + active u16 -> u8)
     grp = batch.CsrGroups.synth(0x5EED0003, "ragged", 1 << 24, device=dev)
     active = torch.randint(-(1 << 15), 1 << 15, (1 << 24,), dtype=torch.int16, device=dev)
@@ -465,7 +495,8 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
           "check_quorum_GBs": (1 << 24) * 7 / tq / 1e9}
     if gpu_only:
         reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
-                 {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq})
+                 {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq,
+                  **ordered})
         return
     # CPU beside it: the C restatement on 1M groups of the same workload
     import time
@@ -484,7 +515,7 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
         oc.leader_step(host, lgc.inflight_cap, Q, 0, recc, threads=threads, msg_cap=8 * Gs)
         cpu[threads] = Gs / (time.perf_counter() - t1)
     reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
-           {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps,
+           {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **ordered,
             "cpu_baseline": {"value": cpu[16], "unit": "group-steps/s", "cores": 16,
                              "kind": "port", "value_1thread": cpu[1],
                              "sample": f"{Gs} groups, one step, C restatement (oracle)"},
