@@ -698,7 +698,7 @@ def tracker_main(args, world, rank, dev, barrier):
         bpg = 21 + 16 + 4 + 4 + 8 * info["voters_mean"] + 8 + 8 + 8
     key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
     achieved = bpg * G / step_s / 1e9
-    kern = ("k_bk_hist, k_scan_local, k_bk_sums_parts, k_bk_scatter, k_bk_split, "
+    kern = ("memset, k_bk_scatter<true> (reserved regions), k_bk_split_compact, "
             + ("k_csr_apply<WMAX,8,false>, k_csr_apply_deferred, k_bk_slow<CsrLay<WMAX>>" if csr
                else "k_bk_apply<5,false>, k_bk_slow<FixedLay<5>>"))
     out = {

@@ -50,6 +50,10 @@ struct Cols {
   u32 compact;
 };
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
+// chunk_slow values: 1 = slow (k_bk_slow applies the chunk from the batch),
+// 2 = deferred to the CSR step's second launch, 3 = a record of the chunk did
+// not fit its reserved region (K3; K5 then sends the chunk to the slow path)
+constexpr u8 kChunkOverflow = 3;
 __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
@@ -85,6 +89,14 @@ struct RecFmt {
 // us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
 // 41 -> 55 us with it, so it keeps the linear order.
 constexpr u32 kXcds = 8;
+// Reserved regions per super-bucket (the tracker steps' K3): the workgroup
+// on XCD x (blockIdx % 8) draws its runs from region x of each super-bucket,
+// so a region is written by one XCD only and the partial lines at its runs'
+// ends merge in that XCD's L2, and a fill counter takes 1/8 of the atomics.
+// Measured (profiles/r04/tracker/ab_region_shards.log): 8 regions 534-548
+// us per 16M-group tick, 4 / 2 / 1 regions (written by several XCDs)
+// 569-606 us, round 3's scanned offsets 573-576 us.
+constexpr u32 kRegionShards = kXcds;
 // interleaved super-buckets (Geometry::il) for the tracker steps
 constexpr bool kSbIl = true;
 // K5 write-back (k_bk_apply, k_csr_apply): a wave whose 64-element segment
@@ -120,11 +132,19 @@ struct Geometry {
   // run together on one XCD while K5 still walks the state in memory order.
   u32 il;
   RecFmt fmt;  // compact record layout (lg / slot / term bit widths)
+  // Reserved regions (compact records, the tracker steps): super-bucket sb's
+  // records from the tiles of shard x (blockIdx % kRegionShards) go to region
+  // sb * kRegionShards + x of cap records, cut into ppx parts of kTile.
+  u32 cap, ppx;
   __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
   __host__ __device__ u32 sb_of_chunk(u32 c) const {
     return il ? (c & (kXcds - 1u)) | ((c >> 10) << 3) : c >> 7;
   }
   __host__ __device__ u32 cl_of_chunk(u32 c) const { return il ? (c >> 3) & 127u : c & 127u; }
+  // the chunk of super-bucket sb with chunk-low cl (inverse of the two above)
+  __host__ __device__ u32 chunk_of_sb_cl(u32 sb, u32 cl) const {
+    return il ? (sb & (kXcds - 1u)) | (cl << 3) | ((sb >> 3) << 10) : sb * kChunksPerSb + cl;
+  }
   __host__ __device__ u32 sb_of(u32 g) const { return il ? sb_of_chunk(g >> ch_shift) : g >> sb_shift; }
   __host__ __device__ u64 nbins() const { return u64(NSB) * NT; }
   u32 tile_grid() const { return xcd ? (NT + kXcds - 1) / kXcds * kXcds : NT; }
@@ -150,12 +170,25 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   g.fmt.lgb = g.ch_shift;
   g.fmt.slb = n <= 8 ? 3u : 4u;
   g.fmt.tb = kRecHdrBits - 1u - g.fmt.lgb - g.fmt.slb;
+  // reserved regions: twice a region's mean share plus a tile, capped by
+  // what the region's tiles can hold at most (small batches never overflow)
+  // and by the run table's 64 rows per super-bucket
+  const u64 S = kRegionShards;
+  const u64 m = (M + u64(g.NSB) * S - 1) / (u64(g.NSB ? g.NSB : 1) * S);
+  const u64 worst = u64((g.tile_grid() + S - 1) / S) * kTile;
+  u64 cap = (2 * m + 2 * kTile - 1) / kTile * kTile;
+  cap = cap < worst ? cap : worst;
+  const u64 capmax = 64 / S * kTile;  // the run table's 64 rows per super-bucket
+  cap = cap < u64(kTile) ? u64(kTile) : cap > capmax ? capmax : cap;
+  g.cap = u32(cap);
+  g.ppx = g.cap / u32(kTile);
   return g;
 }
 
 // Workspace carve (all offsets 256-byte aligned).
 struct Carve {
-  size_t shards, flags, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, cl, total;
+  size_t shards, flags, counts, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, cl,
+      total;
 };
 // Upper bound on parts: every super-bucket contributes at most one partial.
 inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
@@ -168,18 +201,23 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   size_t o = 0;
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
   c.flags = o;  o += 256;  // u32 words zeroed with the shards (any_slow)
+  // compact: the reserved regions' fill counters, zeroed with the shards
+  c.counts = o;  o += ncols == 1 ? up256(sizeof(u32) * u64(g.NSB) * kRegionShards) : 0;
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
   c.inval = o;  o += up256(sizeof(u32) * 2 * (u64(g.NT) + 2));  // per tile: bad, non-member
   c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
   c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
   // part table: pfirst[NSB+1], part_sb[max_parts], nparts
   c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
-  c.chunk_start = o;  o += up256(sizeof(u32) * max_parts(g) * (kChunksPerSb + 1));
+  // compact: one row per part of the region grid (NSB x 8 x ppx)
+  const u64 nrows = ncols == 1 ? u64(g.NSB) * kRegionShards * g.ppx : max_parts(g);
+  c.chunk_start = o;  o += up256(sizeof(u32) * nrows * (kChunksPerSb + 1));
   // (columns of at least one record: K5's branch-free loads read record 0 of
   // an empty chunk)
-  c.buf1 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
-  c.buf2 = o;  o += ncols * up256(sizeof(u64) * (g.M ? g.M : 1));
-  c.cl = o;  o += ncols == 1 ? up256(g.M ? g.M : 1) : 0;
+  const u64 nrec = ncols == 1 ? u64(g.NSB) * kRegionShards * g.cap : (g.M ? g.M : 1);
+  c.buf1 = o;  o += ncols * up256(sizeof(u64) * nrec);
+  c.buf2 = o;  o += ncols * up256(sizeof(u64) * nrec);
+  c.cl = o;  o += ncols == 1 ? up256(nrec) : 0;
   c.total = o;
   return c;
 }
@@ -250,6 +288,24 @@ struct RunTable {
     const u64 row0 = n ? u64(pb + (r < n ? r : 0u)) * (kChunksPerSb + 1) : 0ull;
     const u32 l = cs[row0 + cl], h = cs[row0 + cl + 1];
     return Regs{l, r < n ? h - l : 0u, n};
+  }
+  // The compact steps' chunk runs: super-bucket sb's parts are rows sb * S *
+  // ppx + r of the region grid (S = kRegionShards), r = x * ppx + j; part j
+  // of region x exists iff j * kTile < its fill (counts, clamped to cap).
+  // Lane r loads its row and its region's count in one round trip (S * ppx
+  // <= 64 rows).
+  __device__ __forceinline__ static Regs issue_regions(const u32* __restrict__ cs,
+                                                       const u32* __restrict__ counts, u32 sb,
+                                                       u32 ppx, u32 cap, u32 cl) {
+    const u32 n = kRegionShards * ppx;
+    const u32 r = threadIdx.x & 63u;
+    const u32 rr = r < n ? r : 0u;
+    const u32 x = rr / ppx, j = rr - x * ppx;
+    const u64 row = (u64(sb) * n + rr) * (kChunksPerSb + 1);
+    const u32 l = cs[row + cl], h = cs[row + cl + 1];
+    u32 fill = counts[sb * kRegionShards + x];
+    fill = fill < cap ? fill : cap;
+    return Regs{l, r < n && j * u32(kTile) < fill ? h - l : 0u, n};
   }
   __device__ __forceinline__ u32 finish(const Regs& q) {
     const u32 r = threadIdx.x & 63u;

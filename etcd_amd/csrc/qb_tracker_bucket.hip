@@ -192,11 +192,15 @@ constexpr int kPer = kTile / kPartThreads;  // records per thread
 
 // (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs: the
 // direct placement's registers would otherwise leave one)
+// RESV: the compact records into reserved regions (the tracker steps); else
+// the scanned offsets (the leader step's wide columns).
+template <bool RESV>
 __global__ __launch_bounds__(kPartThreads)
 __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
-    const u32* __restrict__ bsum, Cols out) {
+    const u32* __restrict__ bsum, Cols out, u32* __restrict__ counts, u64* __restrict__ shards,
+    u8* __restrict__ chunk_slow) {
   extern __shared__ __attribute__((aligned(16))) u32 dyn[];
   u32* start = dyn;               // NSB: count, then local exclusive start
   u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
@@ -260,44 +264,72 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   const u64 nb = geo.nbins();
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     start[b] = 0;
-    gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
+    if constexpr (!RESV) gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
   }
   __syncthreads();
-  if (out.compact) {
+  if (RESV) {
     // compact records: bin, rank and the encoded record stay in registers;
     // after the scan each record is stored at its sorted LDS slot with its
     // bin and chunk-low, and the output pass reads the slots in order
-    u32 bj[kPer], rj[kPer], cj[kPer];
+    u32 bj[kPer], rj[kPer];  // bj: bin | chunk-low << 16
     u64 vj[kPer];
+    u32 nbad = 0, nnon = 0;  // wave-uniform: invalid records (reserved regions)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const u32 k = rk(j);
       const bool ok = g[j] < geo.G && (f[j] & 0x0Fu) < geo.n;  // (k >= nrec has g = ~0)
+      {
+        const bool bad = k < nrec && g[j] >= geo.G;
+        nbad += wave_popc(bad);
+        nnon += wave_popc(k < nrec && !bad && !ok);
+      }
       bj[j] = ok ? geo.sb_of(g[j]) : u32(kNoBin);
       rj[j] = ok ? atomicAdd(&start[bj[j]], 1u) : 0u;
-      cj[j] = geo.cl_of_chunk(geo.chunk_of(g[j]));
+      bj[j] |= geo.cl_of_chunk(geo.chunk_of(g[j])) << 16;
       vj[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j], vt[j],
                              u32(t0 + k));
     }
     __syncthreads();
+    {
+      // reserved regions: this tile's run of super-bucket b goes to region
+      // b * 8 + x (x = the XCD slot, blockIdx % 8) at an offset drawn from
+      // the region's fill counter; invalid records go to the stat shards
+      const u32 x = blockIdx.x % kRegionShards;
+      for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+        const u32 nbin = start[b];
+        if (nbin) gstart[b] = atomicAdd(&counts[b * kRegionShards + x], nbin);  // region-relative
+      }
+      if ((threadIdx.x & 63) == 0 && (nbad | nnon)) {
+        u64* sh = shards + u64(tile % kShards) * QB_STAT_COUNT;
+        if (nbad) atomicAdd(sh + QB_STAT_BAD_GROUP, u64(nbad));
+        if (nnon) atomicAdd(sh + QB_STAT_NON_MEMBER, u64(nnon));
+      }
+    }
     const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (bj[j] == u32(kNoBin)) continue;
-      const u32 e = start[bj[j]] + rj[j];
+      const u32 b = bj[j] & 0xFFFFu;
+      if (b == u32(kNoBin)) continue;
+      const u32 e = start[b] + rj[j];
       L.stage[e] = vj[j];
-      L.bin[e] = u16(bj[j]);
-      L.cl[e] = u8(cj[j]);
+      L.bin[e] = u16(b);
+      L.cl[e] = u8(bj[j] >> 16);
     }
     __syncthreads();
+    const u32 x = blockIdx.x % kRegionShards;
     for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
       const u32 b = L.bin[e];
-      const u32 d = gstart[b] + (e - start[b]);
-      out.mr[d] = L.stage[e];
-      out.cl[d] = L.cl[e];
+      const u32 rel = gstart[b] + (e - start[b]);
+      if (rel < geo.cap) {
+        const u32 d = (b * kRegionShards + x) * geo.cap + rel;
+        out.mr[d] = L.stage[e];
+        out.cl[d] = L.cl[e];
+      } else {  // past the region (a skewed batch): the chunk takes the slow path
+        chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
+      }
     }
     return;
-  }
+  } else {
   if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
     u64 bins = 0, ranks = 0;
     u32 cls = 0;
@@ -385,6 +417,7 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     }
     __syncthreads();
   }
+  }  // !RESV
 }
 
 // --------------------------------------------------------------- K3b ----
@@ -577,21 +610,18 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
 constexpr int kSplitThreads = 512;
 constexpr int kSplitPer = kTile / kSplitThreads;
 __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
-    Geometry geo, const u32* __restrict__ offsets, const u32* __restrict__ bsum,
-    const u32* __restrict__ pt, Cols in, Cols out, u32* __restrict__ cs) {
-  const u32* pfirst = pt;
-  const u32* part_sb = pt + geo.NSB + 2;
+    Geometry geo, const u32* __restrict__ counts, Cols in, Cols out, u32* __restrict__ cs) {
+  // part p = region r's j-th kTile records (the region grid, qb_bucket.h)
   const u32 p = blockIdx.x;
-  if (p >= pfirst[geo.NSB]) return;  // fewer parts than the launch bound
+  const u32 r = p / geo.ppx, j = p - r * geo.ppx;
+  u32 fill = counts[r];
+  fill = fill < geo.cap ? fill : geo.cap;
+  if (j * u32(kTile) >= fill) return;  // no such part this tick
   __shared__ u64 stage[kTile];
   __shared__ u32 start[kChunksPerSb];
   __shared__ u32 wsum[kSplitThreads / 64];
-  const u32 sb = part_sb[p];
-  const u32 sb_lo = off_at(offsets, bsum, geo.nbins(), u64(sb) * geo.NT);
-  const u32 sb_hi = off_at(offsets, bsum, geo.nbins(), u64(sb + 1) * geo.NT);
-  const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
-  const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
-  const u32 nrec = hi - lo;
+  const u32 lo = r * geo.cap + j * u32(kTile);
+  const u32 nrec = fill - j * u32(kTile) < u32(kTile) ? fill - j * u32(kTile) : u32(kTile);
   u64 vm[kSplitPer];  // loaded together: one round trip
   u32 vc[kSplitPer];
 #pragma unroll
@@ -645,7 +675,7 @@ __host__ __device__ constexpr u32 k5_block(int n) {
 // capped at 80 (a few SGPRs spill to VGPR lanes): -11 us per 16M-group tick.
 template <int N, bool NEXT>
 __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) void k_bk_apply(
-    Geometry geo, Cols recs, const u32* __restrict__ pt, const u32* __restrict__ cs,
+    Geometry geo, Cols recs, const u32* __restrict__ counts, const u32* __restrict__ cs,
     const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
@@ -675,7 +705,9 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   // (clamped to the chunk's last group): exact wait counts need straight-line
   // code.
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
-  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  // a record of this chunk that did not fit its reserved region (K3): the
+  // whole chunk goes to the slow path
+  const bool overflow = chunk_slow[c] == kChunkOverflow;
   u64 gtr[GPT];
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
@@ -683,7 +715,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
     gtr[k] = group_term[g0 + (lg < ng ? lg : ng - 1)];
   }
   __shared__ RunTable rt;
-  const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
+  const RunTable::Regs rq = RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl);
   u64 v[GPT][N], cm[GPT], ts[GPT];
   u32 av[GPT];
 #pragma unroll
@@ -705,7 +737,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
     gterm[threadIdx.x + k * B] = gtr[k];
     act[threadIdx.x + k * B] = 0;
   }
-  if (threadIdx.x == 0) slow = 0;
+  if (threadIdx.x == 0) slow = overflow ? 1u : 0u;
   if (threadIdx.x < 3) tl[threadIdx.x] = 0;
   // This chunk's records: one short run per part of its super-bucket,
   // flattened into one index space (RunTable) so every thread has a record
@@ -770,17 +802,11 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
 #pragma unroll
   for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
   apply(0, total);
-  for (u32 pb = p0, f0 = B * kRecPer;;) {
-    for (; f0 < total; f0 += B * kRecPer) {
-      fetch(f0, total);
+  for (u32 f0 = B * kRecPer; f0 < total; f0 += B * kRecPer) {  // (all rows in one table)
+    fetch(f0, total);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
-      apply(f0, total);
-    }
-    pb += RunTable::kRuns;
-    if (pb >= p1) break;
-    total = rt.build(cs, pb, p1, cl);  // more than kRuns parts (synchronises)
-    f0 = 0;
+    for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+    apply(f0, total);
   }
   // the counts are final: staged before the barrier the block takes anyway,
   // published after it (a flush with barriers of its own at the end cost
@@ -848,14 +874,14 @@ struct ApplyArgs {
 };
 
 template <int N>
-void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                   const ApplyArgs& a, hipStream_t st) {
   if (a.next)
-    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
+    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, counts,
                        cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
   else
-    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, pt,
+    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, counts,
                        cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
                        a.chunk_slow, a.any_slow, a.stats);
 }
@@ -873,8 +899,8 @@ void launch_slow(const Geometry& geo, const ApplyArgs& a, const SlowArgs& s, u64
 
 template <int... Ns>
 void dispatch_apply(std::integer_sequence<int, Ns...>, int n, const Geometry& geo, Cols recs,
-                    const u32* pt, const u32* cs, const ApplyArgs& a, hipStream_t st) {
-  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, pt, cs, a, st) : void()), ...);
+                    const u32* counts, const u32* cs, const ApplyArgs& a, hipStream_t st) {
+  ((n == Ns + 1 ? launch_apply<Ns + 1>(geo, recs, counts, cs, a, st) : void()), ...);
 }
 
 template <int... Ns>
@@ -912,6 +938,27 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   u64* zero = reinterpret_cast<u64*>(ws + cv.shards);
   u32* inval = reinterpret_cast<u32*>(ws + cv.inval);
   const u32 nzero = u32((cv.flags + 256 - cv.shards) / sizeof(u64));
+  if (compact) {
+    // Reserved regions (round 4): the stat shards, the flag words and the
+    // regions' fill counters are adjacent in the carve — one memset — and K3
+    // reserves each tile's run of a super-bucket in its XCD slot's region
+    // with one atomic per (tile, super-bucket): no histogram pass, no scan,
+    // no part table (K1, K2 and the sums / parts kernel of round 3)
+    u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
+    hipError_t e = hipMemsetAsync(ws + cv.shards, 0,
+                                  cv.counts + sizeof(u32) * size_t(geo.NSB) * kRegionShards - cv.shards,
+                                  st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
+    if (geo.M == 0) return QB_OK;
+    hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st,
+                       geo, rec_group, rec_flags, rec_index, rec_term, nullptr, nullptr, buf1, counts,
+                       zero, reinterpret_cast<u8*>(ws + cv.chunk_flags));
+    QB_CHECK_LAUNCH("k_bk_scatter");
+    hipLaunchKernelGGL(k_bk_split_compact, dim3(geo.NSB * kRegionShards * geo.ppx), dim3(kSplitThreads), 0,
+                       st, geo, counts, buf1, buf2, cs);
+    QB_CHECK_LAUNCH("k_bk_split_compact");
+    return QB_OK;
+  }
   if (geo.M == 0) {
     hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
     if (e == hipSuccess) e = hipMemsetAsync(zero, 0, sizeof(u64) * nzero, st);
@@ -926,15 +973,12 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   hipLaunchKernelGGL(k_bk_sums_parts, dim3(1), dim3(1024), 0, st, geo, hist, bsum, nblk, pt,
                      inval, zero, nzero);
   QB_CHECK_LAUNCH("k_scan");
-  hipLaunchKernelGGL(k_bk_scatter, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st, geo,
-                     rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1);
+  hipLaunchKernelGGL(k_bk_scatter<false>, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st,
+                     geo, rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1, nullptr, nullptr,
+                     nullptr);
   QB_CHECK_LAUNCH("k_bk_scatter");
-  if (compact)
-    hipLaunchKernelGGL(k_bk_split_compact, dim3(unsigned(max_parts(geo))), dim3(kSplitThreads), 0,
-                       st, geo, hist, bsum, pt, buf1, buf2, cs);
-  else
-    hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
-                       geo, hist, bsum, pt, buf1, buf2, cs);
+  hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
+                     geo, hist, bsum, pt, buf1, buf2, cs);
   QB_CHECK_LAUNCH("k_bk_split");
   return QB_OK;
 }
@@ -1006,7 +1050,7 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
-  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
+  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
   const bk::Cols recs = bk::compact_at(ws + cv.buf2, nullptr);
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
@@ -1026,7 +1070,7 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
                         reinterpret_cast<u8*>(ws + cv.chunk_flags),
                         reinterpret_cast<u32*>(ws + cv.flags),
                         shards};
-  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, pt, cs, a,
+  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, counts, cs, a,
                      st);
   QB_CHECK_LAUNCH("k_bk_apply");
   // chunks flagged slow by K5 (none in the steady state: the launch folds

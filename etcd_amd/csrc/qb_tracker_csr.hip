@@ -49,7 +49,7 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
 
 // CAPW: LDS slots per group; SECOND: the launch for the deferred chunks.
 #define QB_CSR_APPLY_PARAMS                                                                      \
-  Geometry geo, Cols recs, const u32 *__restrict__ pt, const u32 *__restrict__ cs,                \
+  Geometry geo, Cols recs, const u32 *__restrict__ counts, const u32 *__restrict__ cs,            \
       const u64 *__restrict__ rec_index, const u64 *__restrict__ rec_term,                        \
       const u32 *__restrict__ off, const u32 *__restrict__ cfg,                                   \
       const u64 *__restrict__ group_term, const u64 *__restrict__ term_start,                     \
@@ -57,7 +57,7 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
       u64 *__restrict__ committed, u32 *__restrict__ stepdown_at, u8 *__restrict__ advanced,      \
       u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards
 #define QB_CSR_APPLY_ARGS                                                                      \
-  geo, recs, pt, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
+  geo, recs, counts, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
       stepdown_at, advanced, chunk_slow, any_slow, shards
 
 // One chunk c (the whole workgroup).
@@ -80,7 +80,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
-  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  // a record of this chunk that did not fit its reserved region (K3): the
+  // whole chunk goes to the slow path (checked before any deferral)
+  const bool overflow = chunk_slow[c] == kChunkOverflow;
   // Load order: (1) slot offsets, group terms and the run table's rows (the
   // part table by scalar load); (2) the old slot run and the commit inputs;
   // (3) the records.  Vector loads retire in order, so each wait of the
@@ -102,7 +104,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     const u32 k = threadIdx.x + q * B;
     gtr[q] = group_term[g0 + (k < ng ? k : ng - 1)];
   }
-  const RunTable::Regs rq = RunTable::issue(cs, p0, p1, cl);
+  const RunTable::Regs rq = RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl);
   // The old slot run and the commit inputs depend only on the chunk's first
   // and last offsets (uniform loads): issued now, in the same round trip as
   // the offsets and the run table, instead of after the first barrier (one
@@ -138,7 +140,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     acc[k] = 0;
     if constexpr (NEXT) accn[k] = 0;
   }
-  if (threadIdx.x == 0) slow = 0;
+  if (threadIdx.x == 0) slow = overflow ? 1u : 0u;
   if (threadIdx.x < 4) tl[threadIdx.x] = 0;
 #pragma unroll
   for (u32 q = 0; q < OPT; ++q) {
@@ -157,7 +159,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   // the chunk takes the slow path (exact per-record semantics, global
   // atomics) — no chunk is left deferred without a launch to apply it.
   if constexpr (!SECOND && CAPW < WMAX) {
-    if (!fits) {  // block-uniform, before anything is written
+    if (!fits && !overflow) {  // block-uniform, before anything is written
       if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
       return;
     }
@@ -222,17 +224,11 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 #pragma unroll
   for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
   apply(0, total);
-  for (u32 pb = p0, f0 = B * kRecPer;;) {
-    for (; f0 < total; f0 += B * kRecPer) {
-      load(f0, total);
+  for (u32 f0 = B * kRecPer; f0 < total; f0 += B * kRecPer) {  // (all rows in one table)
+    load(f0, total);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
-      apply(f0, total);
-    }
-    pb += RunTable::kRuns;
-    if (pb >= p1) break;
-    total = rtab.build(cs, pb, p1, cl);
-    f0 = 0;
+    for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+    apply(f0, total);
   }
   if (!fits && threadIdx.x == 0) slow = 1;
   tally.stage(tl);  // the counts are final; published after the barrier
@@ -337,13 +333,13 @@ struct CsrStepArgs {
 };
 
 template <int WMAX, bool SECOND>
-void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                   const CsrStepArgs& a, hipStream_t st) {
   constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX> : k_csr_apply<WMAX, CAPW, NX>), \
-                     grid, dim3(csr_block()), 0, st, geo, recs, pt, cs, a.ri, a.rt, a.off, a.cfg,  \
+                     grid, dim3(csr_block()), 0, st, geo, recs, counts, cs, a.ri, a.rt, a.off, a.cfg, \
                      a.gt, a.ts,                                                                   \
                      a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
                      a.any_slow, a.shards)
@@ -353,10 +349,10 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
 }
 
 template <int WMAX>
-void launch_csr_step(const Geometry& geo, Cols recs, const u32* pt, const u32* cs,
+void launch_csr_step(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                      const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
-  launch_apply<WMAX, false>(geo, recs, pt, cs, a, st);
-  if constexpr (WMAX > kCsrCapW) launch_apply<WMAX, true>(geo, recs, pt, cs, a, st);
+  launch_apply<WMAX, false>(geo, recs, counts, cs, a, st);
+  if constexpr (WMAX > kCsrCapW) launch_apply<WMAX, true>(geo, recs, counts, cs, a, st);
   hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
                      CsrLay<WMAX>{a.off, a.cfg}, sa.rg, sa.rf, sa.ri, sa.rt, a.gt, a.ts,
                      a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,
@@ -412,7 +408,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
-  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
+  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
   const bk::Cols buf2 = bk::compact_at(ws + cv.buf2, nullptr);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
@@ -441,10 +437,10 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
                         bk::slow_blocks()};
   u64* stt = reinterpret_cast<u64*>(stats);
   switch (wmax) {
-    case 4: bk::launch_csr_step<4>(geo, buf2, pt, cs, a, sa, stt, st); break;
-    case 8: bk::launch_csr_step<8>(geo, buf2, pt, cs, a, sa, stt, st); break;
-    case 12: bk::launch_csr_step<12>(geo, buf2, pt, cs, a, sa, stt, st); break;
-    default: bk::launch_csr_step<16>(geo, buf2, pt, cs, a, sa, stt, st); break;
+    case 4: bk::launch_csr_step<4>(geo, buf2, counts, cs, a, sa, stt, st); break;
+    case 8: bk::launch_csr_step<8>(geo, buf2, counts, cs, a, sa, stt, st); break;
+    case 12: bk::launch_csr_step<12>(geo, buf2, counts, cs, a, sa, stt, st); break;
+    default: bk::launch_csr_step<16>(geo, buf2, counts, cs, a, sa, stt, st); break;
   }
   QB_CHECK_LAUNCH("k_csr_apply / k_bk_slow");
   return QB_OK;

@@ -365,3 +365,41 @@ def test_step_compact_record_escape_boundaries(n, what):
         assert {k: got[k] for k in want} == want
         tr.stepdown_at.fill_(-1)
         seq["stepped_down"][:] = 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("hot_frac", [1.0, 0.3])
+def test_step_skewed_batch_overflows_reserved_regions(hot_frac):
+    """K3 reserves each super-bucket's records in regions of twice the mean
+    share (qb_bucket.h Geometry::cap); a batch concentrated on one
+    super-bucket (hot_frac of 2M records on the 64K groups of super-bucket 0,
+    the rest uniform) overflows them.  The records that do not fit flag
+    their chunks (kChunkOverflow) and those chunks take the exact slow path:
+    the result is still the sequential oracle's, stats included."""
+    n, G, M = 5, 1 << 20, 1 << 21
+    rng = np.random.default_rng(77)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st, track_next=False)
+    st.pop("next")
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, st, higher=0.0005,
+                                                         nonmember=0.001)
+    hot = rng.random(M) < hot_frac
+    # super-bucket 0 (interleaved): chunks c with c % 8 == 0, c < 1024, 512 groups each
+    c = rng.integers(0, 128, size=M) * 8
+    hg = (c * 512 + rng.integers(0, 512, size=M)).astype(np.uint32)
+    group = np.where(hot, hg, group).astype(np.uint32)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 96, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    u = rng.random(M)
+    term = st["term"][group] - (u < 0.02).astype(np.uint64) + (u > 0.9995).astype(np.uint64)
+    stats = oc.appresp_sequential(n, G, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    assert np.array_equal(batch.as_u64(tr.match), st["match"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+    got = tr.stats_dict()
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert {k: got[k] for k in want} == want

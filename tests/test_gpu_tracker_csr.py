@@ -410,3 +410,33 @@ def test_csr_step_compact_record_escape_boundaries(max_slots, what):
         assert tr.stats_dict() == want
         tr.stepdown_at.fill_(-1)
         seq["stepped_down"][:] = 0
+
+
+@pytest.mark.timeout(300)
+def test_csr_step_skewed_batch_overflows_reserved_regions():
+    """The CSR step with a batch concentrated on one super-bucket (1.5M of 2M
+    records on the groups of super-bucket 0): overflowed chunks take the
+    slow path, the result equals the sequential oracle's."""
+    G, M = 1 << 20, 1 << 21
+    rng = np.random.default_rng(78)
+    off, cfg, sizes, st = _state(rng, "ragged", G)
+    st.pop("next")
+    tr = _tracker(off, cfg, st, track_next=False)
+    group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, higher=0.0005)
+    hot = rng.random(M) < 0.75
+    c = rng.integers(0, 128, size=M) * 8
+    hg = (c * 512 + rng.integers(0, 512, size=M)).astype(np.uint32)
+    group = np.where(hot, hg, group).astype(np.uint32)
+    s_g = sizes[group]
+    slot = (rng.integers(0, 1 << 30, size=M) % np.maximum(s_g, 1)).astype(np.uint8)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 96, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    term = st["term"][group].copy()
+    flags = (slot | (rej.astype(np.uint8) << 7)).astype(np.uint8)
+    stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    _compare(tr, st, G)
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert tr.stats_dict() == want
