@@ -610,7 +610,7 @@ def tracker_main(args, world, rank, dev, barrier):
     tr, batches, info = tracker_setup(G, nb, rank, dev, csr)
     gen = info["gen"]
     snap = {k: getattr(tr, k).clone() for k in TRACKER_STATE}
-    Gs = min(G, args.parity_groups)
+    Gs = G if args.tracker_parity_groups <= 0 else min(G, args.tracker_parity_groups)
     snap_host = tracker_host_state(tr, csr, Gs) if not args.no_parity else None
 
     def restore():
@@ -1279,8 +1279,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-parity", action="store_true", help="skip the post-region oracle check")
     ap.add_argument("--no-others", action="store_true",
                     help="the default (configs[1], N = 1) run skips the other BASELINE configs")
+    ap.add_argument("--tracker-parity-groups", type=int, default=0,
+                    help="tracker workloads: groups of the shard whose final state is checked "
+                         "against the sequential oracle replay of every tick (0 = the whole shard)")
     ap.add_argument("--parity-groups", type=int, default=1 << 20,
-                    help="tracker workloads: groups of the shard checked against the oracle")
+                    help="N > 1, configs[1]-[3]: groups of every rank's slice of the node-wide "
+                         "all-gather that rank 0 checks against the oracle")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--preroll-ms", type=float, default=300.0,
                     help="untimed clock-settle pre-roll before the warm-up steps (wall ms)")
