@@ -254,6 +254,12 @@ def host_cpu_info() -> dict:
     return info
 
 
+def oracle_threads(world: int) -> int:
+    """Host threads for one rank's oracle checks: the CPUs this process may
+    use, shared by the node's ranks (one process per GPU on one node)."""
+    return max(1, host_cpu_info()["threads"] // max(1, world))
+
+
 def _rate(fn, units, seconds):
     """units/s of fn() repeated for >= seconds (at least once)."""
     reps, t0 = 0, time.perf_counter()
@@ -610,7 +616,12 @@ def tracker_main(args, world, rank, dev, barrier):
     tr, batches, info = tracker_setup(G, nb, rank, dev, csr)
     gen = info["gen"]
     snap = {k: getattr(tr, k).clone() for k in TRACKER_STATE}
-    Gs = G if args.tracker_parity_groups <= 0 else min(G, args.tracker_parity_groups)
+    # the whole shard at N = 1; with N ranks sharing the node's CPUs, each
+    # rank checks the first 2M groups of its shard (the GPU suite checks the
+    # full 16M-group stream tick by tick)
+    tpg = args.tracker_parity_groups if args.tracker_parity_groups > 0 else (
+        G if world == 1 else 1 << 21)
+    Gs = min(G, tpg)
     snap_host = tracker_host_state(tr, csr, Gs) if not args.no_parity else None
 
     def restore():
@@ -673,7 +684,7 @@ def tracker_main(args, world, rank, dev, barrier):
     stats = tr.stats_dict()
     parity = None
     if snap_host is not None:
-        bad = tracker_parity(tr, csr, snap_host, batches, Gs, host_cpu_info()["threads"])
+        bad = tracker_parity(tr, csr, snap_host, batches, Gs, oracle_threads(world))
         parity = (f"bit-exact {Gs}/{Gs} groups (first {Gs} of the shard: match, committed, active, "
                   f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
                   else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
@@ -1023,7 +1034,7 @@ def eval_main(args, world, rank, dev, barrier):
     # timed steps; the MALL-warm pass rewrote batch 0 with the same result)
     # against the oracle on the same counter-based inputs
     parity = None
-    threads = host_cpu_info()["threads"]
+    threads = oracle_threads(world)
     if not args.no_parity:
         torch.cuda.synchronize()
         bad = 0
@@ -1281,7 +1292,8 @@ def parse_args(argv=None):
                     help="the default (configs[1], N = 1) run skips the other BASELINE configs")
     ap.add_argument("--tracker-parity-groups", type=int, default=0,
                     help="tracker workloads: groups of the shard whose final state is checked "
-                         "against the sequential oracle replay of every tick (0 = the whole shard)")
+                         "against the sequential oracle replay of every tick (0 = the whole shard "
+                         "at N = 1, the first 2M groups of each rank's shard at N > 1)")
     ap.add_argument("--parity-groups", type=int, default=1 << 20,
                     help="N > 1, configs[1]-[3]: groups of every rank's slice of the node-wide "
                          "all-gather that rank 0 checks against the oracle")

@@ -170,18 +170,25 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   g.fmt.lgb = g.ch_shift;
   g.fmt.slb = n <= 8 ? 3u : 4u;
   g.fmt.tb = kRecHdrBits - 1u - g.fmt.lgb - g.fmt.slb;
-  // reserved regions: twice a region's mean share plus a tile, capped by
-  // what the region's tiles can hold at most (small batches never overflow)
-  // and by the run table's 64 rows per super-bucket
+  // reserved regions: twice a region's mean share plus 256 records, capped
+  // by what the region's tiles can hold at most (a small batch never
+  // overflows) and by the run table's 64 rows per super-bucket
   const u64 S = kRegionShards;
-  const u64 m = (M + u64(g.NSB) * S - 1) / (u64(g.NSB ? g.NSB : 1) * S);
-  const u64 worst = u64((g.tile_grid() + S - 1) / S) * kTile;
-  u64 cap = (2 * m + 2 * kTile - 1) / kTile * kTile;
-  cap = cap < worst ? cap : worst;
+  // a region's mean share for records spread evenly over the groups: the
+  // fullest super-bucket holds mc of the NC chunks (interleaved: a window's
+  // chunks of one XCD, up to 128), and its records split over S regions
+  const u64 mc = il ? (g.NC >= 1024 ? 128u : (g.NC + kXcds - 1) / kXcds)
+                    : (g.NC < kChunksPerSb ? g.NC : kChunksPerSb);
+  const u64 m = g.NC ? (M * mc + u64(g.NC) * S - 1) / (u64(g.NC) * S) : 0;
+  // at most what the region's tiles can hold (and never more than the batch)
+  u64 worst = u64((g.tile_grid() + S - 1) / S) * kTile;
+  worst = worst < M ? worst : M;
+  u64 cap = (2 * m + 256 + 255) / 256 * 256;  // (256-record granules)
+  cap = cap < worst ? cap : (worst + 255) / 256 * 256;
   const u64 capmax = 64 / S * kTile;  // the run table's 64 rows per super-bucket
-  cap = cap < u64(kTile) ? u64(kTile) : cap > capmax ? capmax : cap;
+  cap = cap < 256 ? 256 : cap > capmax ? capmax : cap;
   g.cap = u32(cap);
-  g.ppx = g.cap / u32(kTile);
+  g.ppx = u32((cap + kTile - 1) / kTile);
   return g;
 }
 
