@@ -939,15 +939,17 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   u32* inval = reinterpret_cast<u32*>(ws + cv.inval);
   const u32 nzero = u32((cv.flags + 256 - cv.shards) / sizeof(u64));
   if (compact) {
-    // Reserved regions (round 4): the stat shards, the flag words and the
-    // regions' fill counters are adjacent in the carve — one memset — and K3
-    // reserves each tile's run of a super-bucket in its XCD slot's region
-    // with one atomic per (tile, super-bucket): no histogram pass, no scan,
-    // no part table (K1, K2 and the sums / parts kernel of round 3)
+    // Reserved regions (round 4): the stat shards, the flag words, the
+    // regions' fill counters and the chunk flags are adjacent in the carve —
+    // one memset — and K3 reserves each tile's run of a super-bucket in its
+    // XCD slot's region with one atomic per (tile, super-bucket): no histogram
+    // pass, no scan, no part table (K1, K2 and the sums / parts kernel of
+    // round 3).  The chunk flags must start at 0 here: K3 marks overflowing
+    // chunks kChunkOverflow and K5 reads that mark before writing the flag
+    // (a fresh workspace holds garbage; a stale mark would send a chunk to
+    // the slow path and reset its groups' stepdown_at).
     u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-    hipError_t e = hipMemsetAsync(ws + cv.shards, 0,
-                                  cv.counts + sizeof(u32) * size_t(geo.NSB) * kRegionShards - cv.shards,
-                                  st);
+    hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.chunk_flags + size_t(geo.NC) + 1 - cv.shards, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
     if (geo.M == 0) return QB_OK;
     hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st,

@@ -278,6 +278,49 @@ def test_pipelined_bucket_apply_equals_step():
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill", [0x01, 0x03, 0xFF])
+def test_garbage_workspace_sends_no_chunk_to_the_slow_path(fill):
+    """A workspace fresh from the allocator holds garbage; the chunk flags in it
+    (K3 marks overflowing chunks, K5 reads the mark) must not survive into the
+    tick.  With step-down markers kept from an earlier tick (rearm=False) and a
+    batch with no higher term, a chunk wrongly sent to the slow path would
+    reset its groups' markers: every marker must stay, and the state must
+    equal a step over a zeroed workspace."""
+    import torch
+    from etcd_amd.quorum import batch as qb
+    dev = torch.device("cuda", 0)
+    n, G, M = 5, 200_003, 150_000
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    trs = []
+    for _ in range(2):
+        tr = qb.FixedTracker(n, G, dev)
+        gen.manual_seed(7)
+        tr.match.copy_(torch.randint(0, 1 << 20, (n, G), generator=gen, device=dev))
+        tr.term.fill_(7)
+        tr.term_start.copy_(torch.randint(0, 1 << 19, (G,), generator=gen, device=dev))
+        tr.commit_advance()
+        tr.stepdown_at.copy_(torch.randint(0, 1 << 30, (G,), generator=gen, device=dev,
+                                           dtype=torch.int32))
+        trs.append(tr)
+    grp = torch.randint(0, G, (M,), generator=gen, device=dev, dtype=torch.int32)
+    slot = torch.randint(0, n, (M,), generator=gen, device=dev, dtype=torch.int32)
+    idx = torch.randint(0, 1 << 21, (M,), generator=gen, device=dev)
+    trm = torch.where(torch.rand(M, generator=gen, device=dev) < 0.05, 6, 7).to(torch.int64)
+    bt = qb.AppRespBatch(grp, slot.to(torch.uint8), idx, trm)
+    markers = trs[0].stepdown_at.clone()
+    for tr, byte in zip(trs, (0x00, fill)):
+        ws = tr.workspace(M)
+        ws.fill_(byte)
+        tr.bucket(bt, ws)
+        tr.apply_bucketed(bt, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(trs[1].stepdown_at, markers)
+    for name in ("match", "committed", "active", "stepdown_at", "stats"):
+        assert torch.equal(getattr(trs[0], name), getattr(trs[1], name)), name
+
+
 def test_stepdown_entry_rule_check_and_rearm():
     """The bucketed step's entry rule (stepdown_at all UINT32_MAX) is checked
     on request (qb_dev_stepdown_check_armed); the Python step re-arms by
