@@ -1,6 +1,7 @@
 // qb_bucket.h — device bucketing of record batches by group (shared by the
-// bucketed tracker step and the leader step): per-tile LDS counting sorts
-// into super-buckets, then into chunks of CH groups.
+// bucketed tracker steps and the leader step): per-tile LDS counting sorts
+// into reserved regions of super-buckets, then into chunks of CH groups
+// (DESIGN.md §3.3, §3.3e).
 #pragma once
 
 #include "qb_common.h"
@@ -9,22 +10,20 @@
 namespace qb {
 namespace bk {
 
-constexpr int kTile = 4096;          // records per histogram/scatter/split tile
+constexpr int kTile = 4096;          // records per scatter / split tile
 constexpr int kChunksPerSb = 128;    // chunks per super-bucket (7 bits)
-using scan::kScanPer;
 constexpr int kShards = 256;         // stat counter shards (one 64-byte line each)
 
 // Bucketed record payload, structure of arrays, so every scatter store is
 // one contiguous wave-wide write.  Two forms:
 //
-// Wide (the leader step): three u64 columns of M — index, term, and
-//   mr = meta | ridx << 32 with
+// Wide (the leader step): three columns — index (u64), term32 (u32, in a
+//   u64 column's space) and mr = meta | ridx << 32 with
 //   meta = lg (bits 0-9) | chunk-low (10-16) | record flags byte (17-24:
 //          slot 17-20, kind 21-22, no-progress 23, reject 24),
 //   ridx = batch index of the record (step-down ordering).
-//   term32 (optional, in the term column's space): the term as u32, or
-//   kTermEscape when it does not fit, in which case the consumer reads the
-//   full term from the original batch by ridx.
+//   term32: the term as u32, or kTermEscape when it does not fit, in which
+//   case the consumer reads the full term from the original batch by ridx.
 //
 // Compact (the tracker steps, Cols::compact): ONE u64 per record through
 // both levels — what K5 needs and nothing else — plus a u8 chunk-low column
@@ -52,8 +51,22 @@ struct Cols {
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
 // chunk_slow values: 1 = slow (k_bk_slow applies the chunk from the batch),
 // 2 = deferred to the CSR step's second launch, 3 = a record of the chunk did
-// not fit its reserved region (K3; K5 then sends the chunk to the slow path)
+// not fit its reserved region (K3; K5 then sends the chunk to the slow path).
+// Wide records (the leader step) that do not fit go to the overflow area
+// (Ovf) instead, and K3 sets the chunk's flag to 1.
 constexpr u8 kChunkOverflow = 3;
+// Wide records that did not fit their reserved region (a batch concentrated
+// on a few super-buckets), appended in any order with their chunk; the
+// leader's chunk placement (k_ld_chunk_runs) adds a flagged chunk's records
+// from here.  Exact always, slower only for such batches.
+struct Ovf {
+  u32* total;    // records appended (the carve's flag word 1)
+  u32* cnt;      // [NC] records per chunk
+  u64* mr;       // [M] the three wide columns and the chunk
+  u64* index;
+  u32* term32;
+  u32* chunk;
+};
 __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
@@ -89,7 +102,7 @@ struct RecFmt {
 // us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
 // 41 -> 55 us with it, so it keeps the linear order.
 constexpr u32 kXcds = 8;
-// Reserved regions per super-bucket (the tracker steps' K3): the workgroup
+// Reserved regions per super-bucket (K3, both record forms): the workgroup
 // on XCD x (blockIdx % 8) draws its runs from region x of each super-bucket,
 // so a region is written by one XCD only and the partial lines at its runs'
 // ends merge in that XCD's L2, and a fill counter takes 1/8 of the atomics.
@@ -132,9 +145,9 @@ struct Geometry {
   // run together on one XCD while K5 still walks the state in memory order.
   u32 il;
   RecFmt fmt;  // compact record layout (lg / slot / term bit widths)
-  // Reserved regions (compact records, the tracker steps): super-bucket sb's
-  // records from the tiles of shard x (blockIdx % kRegionShards) go to region
-  // sb * kRegionShards + x of cap records, cut into ppx parts of kTile.
+  // Reserved regions: super-bucket sb's records from the tiles of shard x
+  // (blockIdx % kRegionShards) go to region sb * kRegionShards + x of cap
+  // records, cut into ppx parts of kTile.
   u32 cap, ppx;
   __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
   __host__ __device__ u32 sb_of_chunk(u32 c) const {
@@ -176,12 +189,16 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   const u64 S = kRegionShards;
   // a region's mean share for records spread evenly over the groups: the
   // fullest super-bucket holds mc of the NC chunks (interleaved: a window's
-  // chunks of one XCD, up to 128), and its records split over S regions
+  // chunks of one XCD, up to 128), and the region gets the records of its
+  // XCD slot's tiles, at most tps of the NT (tps = NT / S once NT >= S; a
+  // batch of fewer tiles puts a whole tile's share in one region)
   const u64 mc = il ? (g.NC >= 1024 ? 128u : (g.NC + kXcds - 1) / kXcds)
                     : (g.NC < kChunksPerSb ? g.NC : kChunksPerSb);
-  const u64 m = g.NC ? (M * mc + u64(g.NC) * S - 1) / (u64(g.NC) * S) : 0;
+  const u64 tps = (g.tile_grid() + S - 1) / S;
+  const u64 den = u64(g.NC) * (g.NT ? g.NT : 1);
+  const u64 m = g.NC ? (M * mc * tps + den - 1) / den : 0;
   // at most what the region's tiles can hold (and never more than the batch)
-  u64 worst = u64((g.tile_grid() + S - 1) / S) * kTile;
+  u64 worst = tps * kTile;
   worst = worst < M ? worst : M;
   u64 cap = (2 * m + 256 + 255) / 256 * 256;  // (256-record granules)
   cap = cap < worst ? cap : (worst + 255) / 256 * 256;
@@ -192,41 +209,53 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   return g;
 }
 
-// Workspace carve (all offsets 256-byte aligned).
+// Workspace carve (all offsets 256-byte aligned).  [shards, zero_end) is
+// zeroed by one memset per call (bucket_records).
 struct Carve {
-  size_t shards, flags, counts, chunk_flags, inval, hist, bsum, parts, chunk_start, buf1, buf2, cl,
+  size_t shards, flags, counts, chunk_flags, ovf_cnt, zero_end, chunk_start, buf1, buf2, cl, ovf,
       total;
+  u64 nrec;  // records per column of buf1 / buf2 (the region grid)
 };
-// Upper bound on parts: every super-bucket contributes at most one partial.
-inline u64 max_parts(const Geometry& g) { return (g.M + kTile - 1) / kTile + g.NSB; }
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
-// ncols = 3: index, term and mr move with the records; ncols = 1: only mr
-// (callers that read the payload from the original batch by ridx, and the
-// compact form, whose u8 chunk-low column rides in the carve's cl area).
+// ncols = 3: the wide form (index, term32, mr; the leader step) with its
+// overflow area; ncols = 1: the compact form, whose u8 chunk-low column rides
+// in the carve's cl area (the tracker steps).
 inline Carve carve(const Geometry& g, int ncols = 3) {
   Carve c{};
   size_t o = 0;
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
-  c.flags = o;  o += 256;  // u32 words zeroed with the shards (any_slow)
-  // compact: the reserved regions' fill counters, zeroed with the shards
-  c.counts = o;  o += ncols == 1 ? up256(sizeof(u32) * u64(g.NSB) * kRegionShards) : 0;
+  c.flags = o;  o += 256;  // u32 words: any_slow (0), Ovf::total (1), slow-path barrier (16..)
+  c.counts = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards);  // region fills
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
-  c.inval = o;  o += up256(sizeof(u32) * 2 * (u64(g.NT) + 2));  // per tile: bad, non-member
-  c.hist = o;  o += up256(sizeof(u32) * (g.nbins() + 1));
-  c.bsum = o;  o += up256(sizeof(u32) * ((g.nbins() + kScanPer) / kScanPer + 1));
-  // part table: pfirst[NSB+1], part_sb[max_parts], nparts
-  c.parts = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 2 + max_parts(g)));
-  // compact: one row per part of the region grid (NSB x 8 x ppx)
-  const u64 nrows = ncols == 1 ? u64(g.NSB) * kRegionShards * g.ppx : max_parts(g);
+  c.ovf_cnt = o;  o += ncols == 3 ? up256(sizeof(u32) * (u64(g.NC) + 1)) : 0;
+  c.zero_end = o;
+  // one row per part of the region grid (NSB x 8 x ppx)
+  const u64 nrows = u64(g.NSB) * kRegionShards * g.ppx;
   c.chunk_start = o;  o += up256(sizeof(u32) * nrows * (kChunksPerSb + 1));
   // (columns of at least one record: K5's branch-free loads read record 0 of
   // an empty chunk)
-  const u64 nrec = ncols == 1 ? u64(g.NSB) * kRegionShards * g.cap : (g.M ? g.M : 1);
+  c.nrec = u64(g.NSB) * kRegionShards * g.cap;
+  const u64 nrec = c.nrec ? c.nrec : 1;
   c.buf1 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.buf2 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.cl = o;  o += ncols == 1 ? up256(nrec) : 0;
+  // wide: the overflow area, M records (mr, index, term32, chunk)
+  const u64 M1 = g.M ? g.M : 1;
+  c.ovf = o;  o += ncols == 3 ? 2 * up256(sizeof(u64) * M1) + 2 * up256(sizeof(u32) * M1) : 0;
   c.total = o;
   return c;
+}
+inline Ovf ovf_at(char* ws, const Carve& c, const Geometry& g) {
+  const u64 M1 = g.M ? g.M : 1;
+  char* b = ws + c.ovf;
+  Ovf v{};
+  v.total = reinterpret_cast<u32*>(ws + c.flags) + 1;
+  v.cnt = reinterpret_cast<u32*>(ws + c.ovf_cnt);
+  v.mr = reinterpret_cast<u64*>(b);
+  v.index = reinterpret_cast<u64*>(b + up256(sizeof(u64) * M1));
+  v.term32 = reinterpret_cast<u32*>(b + 2 * up256(sizeof(u64) * M1));
+  v.chunk = reinterpret_cast<u32*>(b + 2 * up256(sizeof(u64) * M1) + up256(sizeof(u32) * M1));
+  return v;
 }
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
@@ -242,61 +271,23 @@ inline Cols compact_at(char* base, char* cl) {
 }
 
 
-// Run table of one chunk: the chunk's run in each of up to kRuns parts,
-// with an inclusive prefix of run lengths so flattened record f maps to a
-// buffer index by binary search.
+// Run table of one chunk: the chunk's run in each of up to kRuns parts of
+// its super-bucket's regions, with an inclusive prefix of run lengths so
+// flattened record f maps to a buffer index by binary search.
 struct RunTable {
   static constexpr u32 kRuns = 64;
   u32 lo[kRuns];
   u32 pre[kRuns + 1];
   u32 nr;
-  // Every thread calls; returns the number of records in parts [pb, min(p1, pb+kRuns)).
-  __device__ __forceinline__ u32 build(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
-    __syncthreads();  // earlier readers of the table are done
-    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
-    if (threadIdx.x < 64) {  // one wave: inclusive scan of the run lengths
-      const u32 r = threadIdx.x;
-      u32 l = 0, len = 0;
-      if (r < n) {
-        const u64 row = u64(pb + r) * (kChunksPerSb + 1) + cl;
-        l = cs[row];
-        len = cs[row + 1] - l;
-      }
-      u32 x = len;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = u32(__shfl_up(int(x), o, 64));
-        if (r >= u32(o)) x += y;
-      }
-      if (r < n) {
-        lo[r] = l;
-        pre[r + 1] = x;
-      }
-      if (r == 0) {
-        pre[0] = 0;
-        nr = n;
-      }
-    }
-    __syncthreads();
-    return pre[n];
-  }
-  // build() in two halves, for a caller that wants the run table's loads in
-  // flight ahead of its own bulk loads (vector loads retire in order, so a
-  // wait for loads issued after the bulk would wait for the bulk too):
-  // issue() loads lane r's run (every wave, branch-free: an empty table reads
-  // row 0 and counts nothing); finish() scans the lengths and wave 0 publishes
-  // the table.  The caller synchronises before locate().
+  // issue_regions() loads lane r's run (every wave, branch-free: a row past
+  // the table reads row 0 and counts nothing); finish() scans the lengths and
+  // wave 0 publishes the table.  The caller synchronises before locate().
+  // (Two halves, so a caller can keep the table's loads in flight ahead of
+  // its own bulk loads: vector loads retire in order.)
   struct Regs {
     u32 l, len, n;
   };
-  __device__ __forceinline__ static Regs issue(const u32* __restrict__ cs, u32 pb, u32 p1, u32 cl) {
-    const u32 n = p1 - pb < kRuns ? p1 - pb : kRuns;
-    const u32 r = threadIdx.x & 63u;
-    const u64 row0 = n ? u64(pb + (r < n ? r : 0u)) * (kChunksPerSb + 1) : 0ull;
-    const u32 l = cs[row0 + cl], h = cs[row0 + cl + 1];
-    return Regs{l, r < n ? h - l : 0u, n};
-  }
-  // The compact steps' chunk runs: super-bucket sb's parts are rows sb * S *
+  // A chunk's runs: super-bucket sb's parts are rows sb * S *
   // ppx + r of the region grid (S = kRegionShards), r = x * ppx + j; part j
   // of region x exists iff j * kTile < its fill (counts, clamped to cap).
   // Lane r loads its row and its region's count in one round trip (S * ppx
@@ -359,22 +350,22 @@ struct RunTable {
   }
 };
 
-// K1-K4 of the bucketed pipeline: records (any order) -> buf2 holds each
-// chunk's records as one run per part of its super-bucket; pt / cs describe
-// the parts and the chunk runs inside them (RunTable reads them).  Records
-// with group >= G are dropped and counted into shards[QB_STAT_BAD_GROUP], and
-// with n < 16 those with slot >= n into shards[QB_STAT_NON_MEMBER].
-// rec_index == rec_term == nullptr buckets the mr column alone (carve with
-// ncols = 1).  term32: the term column moves as u32 (term_to32), 4 bytes
-// per record less through both levels; read it with Cols::term32.  compact
-// (carve with ncols = 1): the 8-byte compact record (RecFmt) through both
-// levels, chunk-low in the carve's cl bytes between them.
-// K2 zeroes [cv.shards, cv.flags + 256) (stat shards and flag words) before
-// anything counts into them, so the caller needs no memset; K2's add-back is folded into its readers
-// (the hist array keeps per-4096 local scans, see off_at).
+// K3-K4 of the bucketed pipeline: records (any order) -> buf2 holds each
+// chunk's records as one run per part of its super-bucket's reserved regions;
+// counts (region fills) and cs (chunk run starts per part) describe them
+// (RunTable::issue_regions reads them).  One memset zeroes [cv.shards,
+// cv.zero_end) first: stat shards, flag words, region fills, chunk flags
+// (and the wide form's per-chunk overflow counts).  Records with group >= G
+// are dropped and counted into shards[QB_STAT_BAD_GROUP], and with n < 16
+// those with slot >= n into shards[QB_STAT_NON_MEMBER].  compact (carve with
+// ncols = 1): the 8-byte compact record (RecFmt) through both levels,
+// chunk-low in the carve's cl bytes between them; a record past its region
+// marks its chunk kChunkOverflow.  Otherwise (carve with ncols = 3) the wide
+// columns (index, term32, mr); a record past its region goes to the overflow
+// area (ovf_at) and its chunk is flagged 1.
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32 = false, bool compact = false);
+                   hipStream_t st, bool compact);
 
 
 }  // namespace bk

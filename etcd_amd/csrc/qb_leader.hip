@@ -16,9 +16,10 @@
 //   responseToReadIndexReq                raft.go:1737-1752
 //
 // Pipeline:
-//   L1 bucket        bk::bucket_records (qb_bucket.h) sorts the records'
-//                    batch indexes into chunks of 256 groups through LDS
-//                    counting sorts (bad groups counted)
+//   L1 bucket        bk::bucket_records (qb_bucket.h) sorts the records
+//                    (wide columns) into chunks of 256 groups through LDS
+//                    counting sorts into reserved regions (bad groups
+//                    counted; a skewed batch's excess to the overflow area)
 //   L2 k_ld_chunk_total + scan  records per chunk -> each chunk's base
 //   L3 k_ld_chunk_runs  per chunk: LDS count per group, block scan (writes
 //                    the per-group run starts), LDS-atomic scatter of the
@@ -273,18 +274,26 @@ __global__ __launch_bounds__(kBlock) void k_ld_gather(u64 G, qb_leader_inbox in,
 }
 
 // --------------------------------------------------------- L2 / L3 (bk) ----
-// Records of chunk c: the sum of its runs over the parts of its super-bucket.
+// Records of chunk c: the sum of its runs over the parts of its super-bucket's
+// regions (a part exists iff j * kTile < its region's fill), plus the chunk's
+// records in the overflow area.
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
-                                                           const u32* __restrict__ pt,
+                                                           const u32* __restrict__ counts,
                                                            const u32* __restrict__ cs,
+                                                           const u32* __restrict__ ovf_cnt,
                                                            u32* __restrict__ ctot) {
   const u32 c = blockIdx.x * kBlock + threadIdx.x;
   if (c >= geo.NC) return;
-  const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
-  u32 s = 0;
-  for (u32 p = pt[sb], p1 = pt[sb + 1]; p < p1; ++p) {
-    const u64 row = u64(p) * (bk::kChunksPerSb + 1) + cl;
-    s += cs[row + 1] - cs[row];
+  const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
+  const u32 nrow = bk::kRegionShards * geo.ppx;
+  u32 s = ovf_cnt[c];
+  for (u32 x = 0; x < bk::kRegionShards; ++x) {
+    u32 fill = counts[sb * bk::kRegionShards + x];
+    fill = fill < geo.cap ? fill : geo.cap;
+    for (u32 j = 0; j < geo.ppx && j * u32(bk::kTile) < fill; ++j) {
+      const u64 row = (u64(sb) * nrow + x * geo.ppx + j) * (bk::kChunksPerSb + 1) + cl;
+      s += cs[row + 1] - cs[row];
+    }
   }
   ctot[c] = s;
 }
@@ -305,10 +314,14 @@ __device__ __forceinline__ ChunkStage& chunk_stage() {
 // chunk's records per group in LDS, scan the counts (cnt[g] = the group's
 // run start, cnt[G] = all valid records), then place every record's batch
 // index in its group's run with an LDS cursor.  Order inside a run is
-// arbitrary; the step sorts each run.
+// arbitrary; the step sorts each run.  The chunk's records are its runs in
+// the parts of its super-bucket's regions (one run table) and, for a chunk
+// flagged by K3 (a skewed batch), its records in the overflow area.
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::Cols recs,
-                                                          const u32* __restrict__ pt,
+                                                          const u32* __restrict__ counts,
                                                           const u32* __restrict__ cs,
+                                                          const u8* __restrict__ chunk_flags,
+                                                          bk::Ovf ovf,
                                                           const u32* __restrict__ cbase,
                                                           u32* __restrict__ cnt,
                                                           u32* __restrict__ perm,
@@ -317,20 +330,21 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   __shared__ u32 cur[kCh];
   __shared__ u32 wsum[kBlock / 64];
   const u32 c = blockIdx.x, t = threadIdx.x;
-  const u32 sb = c / bk::kChunksPerSb, cl = c % bk::kChunksPerSb;
-  const u32 p0 = pt[sb], p1 = pt[sb + 1];
+  const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   cur[t] = 0;
-  // Common case (round 3, one pass): one run table and at most kStageRecs
+  const bk::RunTable::Regs rq = bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl);
+  const u32 total1 = rt.finish(rq);  // the region records (workgroup-uniform)
+  // overflow records of this chunk (K3 flagged it): the area is scanned
+  const u32 novf = chunk_flags[c] ? *ovf.total : 0u;  // workgroup-uniform
+  __syncthreads();  // the run table is published
+  // Common case (round 3, one pass): no overflow and at most kStageRecs
   // records — each record is loaded once, into registers (kRegRecs per
   // thread), counted from there and placed from there; otherwise the
   // records are read twice (count, then place) by the loops below.
   constexpr u32 kRegRecs = kStageRecs / kBlock;
   u64 rv[kRegRecs], ri[kRegRecs];
   u32 rt32[kRegRecs];
-  u32 total1 = 0;
-  const bool one_table = p1 - p0 <= bk::RunTable::kRuns;  // block-uniform
-  if (one_table) total1 = rt.build(cs, p0, p1, cl);  // synchronises first
-  const bool onepass = one_table && total1 <= kStageRecs;  // block-uniform
+  const bool onepass = novf == 0 && total1 <= kStageRecs;  // block-uniform
   if (onepass) {
     u32 b[kRegRecs];
 #pragma unroll
@@ -350,11 +364,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     for (u32 r = 0; r < kRegRecs; ++r)
       if (t + r * kBlock < total1) atomicAdd(&cur[u32(rv[r]) & 1023u], 1u);
   } else {
-    for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
-      const u32 total = rt.build(cs, pb, p1, cl);  // synchronises first
-      for (u32 f = t; f < total; f += kBlock)
-        atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
-    }
+    for (u32 f = t; f < total1; f += kBlock) atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
+    for (u32 o = t; o < novf; o += kBlock)
+      if (ovf.chunk[o] == c) atomicAdd(&cur[u32(ovf.mr[o]) & 1023u], 1u);
   }
   __syncthreads();
   const u32 x = cur[t];
@@ -373,38 +385,43 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   if (c + 1 == geo.NC && t == 0) cnt[geo.G] = cbase[geo.NC];
   cur[t] = start;
   const u32 ntot = cbase[c + 1] - base;  // workgroup-uniform
+  __syncthreads();  // every group's cur[] start is written
+  // the chunk's records one at a time (region runs, then overflow): the full
+  // term (a kTermEscape term32 is read from the batch by ridx)
+  auto each = [&](auto&& fn) {
+    for (u32 f = t; f < total1; f += kBlock) {
+      const u32 b = rt.locate(f);
+      fn(recs.mr[b], recs.term32[b], recs.index[b]);
+    }
+    for (u32 o = t; o < novf; o += kBlock)
+      if (ovf.chunk[o] == c) fn(ovf.mr[o], ovf.term32[o], ovf.index[o]);
+  };
+  auto full_term = [&](u64 v, u32 t32) -> u64 {
+    return t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
+  };
   if (ntot <= kStageRecs) {
     // Common case: the chunk's records are placed in LDS, each group's run
     // is put in batch order there (runs of <= kLdsSortMax), and the chunk
     // is written out with coalesced stores.
     ChunkStage& cs_ = chunk_stage();
     if (onepass) {
-      __syncthreads();  // every group's cur[] start is written
 #pragma unroll
       for (u32 r = 0; r < kRegRecs; ++r) {
         if (t + r * kBlock < total1) {
           const u64 v = rv[r];
-          const u64 term = rt32[r] != bk::kTermEscape ? u64(rt32[r]) : in.term[u32(v >> 32)];
           const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
           cs_.mr[e] = v;
-          cs_.term[e] = term;
+          cs_.term[e] = full_term(v, rt32[r]);
           cs_.index[e] = ri[r];
         }
       }
-    }
-    for (u32 pb = p0; !onepass && pb < p1; pb += bk::RunTable::kRuns) {
-      const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
-      for (u32 f = t; f < total; f += kBlock) {
-        const u32 b = rt.locate(f);
-        const u64 v = recs.mr[b];
-        const u32 t32 = recs.term32[b];  // kTermEscape: the full term from the batch
-        const u64 term = t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
-        const u64 index = recs.index[b];
+    } else {
+      each([&](u64 v, u32 t32, u64 index) {
         const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
         cs_.mr[e] = v;
-        cs_.term[e] = term;
+        cs_.term[e] = full_term(v, t32);
         cs_.index[e] = index;
-      }
+      });
     }
     __syncthreads();
     if (x > 1 && x <= kLdsSortMax) {
@@ -440,27 +457,19 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     if (x > kLdsSortMax) gather_run(in, perm, base + start, x, rc);
     return;
   }
-  for (u32 pb = p0; pb < p1; pb += bk::RunTable::kRuns) {
-    const u32 total = rt.build(cs, pb, p1, cl);  // also orders cur[] writes
-    for (u32 f = t; f < total; f += kBlock) {
-      const u32 b = rt.locate(f);
-      const u64 v = recs.mr[b];
-      const u32 t32 = recs.term32[b];
-      const u64 term = t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
-      const u64 index = recs.index[b];
-      const u32 k = base + atomicAdd(&cur[u32(v) & 1023u], 1u);
-      const u32 i = u32(v >> 32);
-      const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
-      perm[k] = i;
-      rc.flags[k] = fl;
-      rc.term[k] = term;
-      rc.index[k] = index;
-      if (fl & QB_REC_REJECT) {
-        rc.hint[k] = in.hint ? in.hint[i] : 0ull;
-        rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
-      }
+  each([&](u64 v, u32 t32, u64 index) {
+    const u32 k = base + atomicAdd(&cur[u32(v) & 1023u], 1u);
+    const u32 i = u32(v >> 32);
+    const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
+    perm[k] = i;
+    rc.flags[k] = fl;
+    rc.term[k] = full_term(v, t32);
+    rc.index[k] = index;
+    if (fl & QB_REC_REJECT) {
+      rc.hint[k] = in.hint ? in.hint[i] : 0ull;
+      rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
     }
-  }
+  });
   // A group with several records: its run (placed in arbitrary order) is
   // put in batch order and its fields gathered again in that order.
   __syncthreads();  // the chunk's runs are complete (workgroup-visible)
@@ -1273,22 +1282,24 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
     char* bws = ws + c.bkt;
     bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);
     u32* ctot = reinterpret_cast<u32*>(ws + c.ctot);
-    const u32* pt = reinterpret_cast<const u32*>(bws + c.bcv.parts);
+    const u32* counts = reinterpret_cast<const u32*>(bws + c.bcv.counts);
     const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
+    const bk::Ovf ovf = bk::ovf_at(bws, c.bcv, c.geo);
     // bucket_records zeroes bshards itself (before its first count)
     const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags,
                                       ld::U(in->index), ld::U(in->term), bshards, st,
-                                      /*term32=*/true);
+                                      /*compact=*/false);
     if (rc != QB_OK) return rc;
     hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, st, c.geo, pt, cs, ctot);
+                       dim3(kBlock), 0, st, c.geo, counts, cs, ovf.cnt, ctot);
     QB_CHECK_LAUNCH("k_ld_chunk_total");
     scan::launch(ctot, c.geo.NC, reinterpret_cast<u32*>(ws + c.cbsum), st);
     QB_CHECK_LAUNCH("scan(chunks)");
-    bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, M, 3);
+    bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, c.bcv.nrec, 3);
     b2.term32 = reinterpret_cast<u32*>(b2.term);
     hipLaunchKernelGGL(ld::k_ld_chunk_runs, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo,
-                       b2, pt, cs, ctot, cnt, perm, *in, rcols);
+                       b2, counts, cs, reinterpret_cast<const u8*>(bws + c.bcv.chunk_flags), ovf,
+                       ctot, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");
   } else {
     u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);

@@ -10,17 +10,15 @@
 //   raft.maybeCommit / raftLog.maybeCommit  raft.go:585-588, log.go:328-334
 //
 // Pipeline (records are any-order; M ~ G at the BASELINE config 5):
-//   K1 k_bk_hist     per tile of kTile records: LDS histogram over super-
-//                    buckets (kChunksPerSb chunks of CH groups each); invalid
-//                    records (group >= G, slot >= n) are counted and dropped
-//   K2 k_scan_*      exclusive scan of the bin-major [super-bucket][tile]
-//                    histogram (three small kernels)
-//   K3 k_bk_scatter  per tile: counting sort by super-bucket in LDS; every
-//                    payload column is loaded coalesced into LDS, permuted
-//                    there and written out as per-bucket contiguous runs
-//   K3b k_bk_parts   cut every super-bucket into parts of <= kTile records
-//   K4 k_bk_split    per part: the same LDS counting sort by chunk, written
-//                    in place (same range), plus the part's chunk run starts
+//   memset           stat shards, flag words, region fills, chunk flags
+//   K3 k_bk_scatter  per tile: counting sort by super-bucket in LDS; each
+//                    super-bucket's run reserves its place in the region of
+//                    this workgroup's XCD slot with one atomic and is written
+//                    there contiguously; invalid records (group >= G, slot >=
+//                    n) are counted and dropped (round 4: no histogram pass,
+//                    no scan, no part table — DESIGN.md §3.3e)
+//   K4 k_bk_split_*  per part of a region: the same LDS counting sort by
+//                    chunk, written in place, plus the part's chunk run starts
 //   K5 k_bk_apply<N> one workgroup per chunk of CH groups (its records are
 //                    one short run per part of its super-bucket): classify (term
 //                    filter, step-down ordering via an LDS atomic min of the
@@ -33,88 +31,6 @@
 
 namespace qb {
 namespace bk {
-
-// ---------------------------------------------------------------- K1 ----
-// Invalid records (group >= G, slot >= n) are counted per tile into inval[2
-// * tile + {0, 1}] with plain stores; k_bk_sums_parts adds them to the stat
-// shards after zeroing those (so the step needs no memset).
-// (100 SGPRs hold it at 6 of its 256-thread blocks per CU by the residency
-// rule; capping them at 80 for 8 blocks measured neutral: not kept)
-__global__ __launch_bounds__(kBlock) void k_bk_hist(Geometry geo, const u32* __restrict__ rg,
-                                                    const u8* __restrict__ rf,
-                                                    u32* __restrict__ hist,
-                                                    u32* __restrict__ inval) {
-  extern __shared__ __attribute__((aligned(16))) u32 lh[];  // NSB counters
-  __shared__ u32 tl[2];
-  const u32 tile = geo.tile();
-  if (tile >= geo.NT) return;  // XCD-major grid is rounded up to a multiple of kXcds
-  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) lh[b] = 0;
-  __syncthreads();
-  const u64 t0 = u64(tile) * kTile;
-  // The tile's group / flag loads are all issued before the first LDS
-  // atomic (a load -> use loop waited one HBM round trip per iteration).
-  constexpr int kHistPer = kTile / kBlock;
-  u32 gg[kHistPer];
-  u32 ff[kHistPer];
-  u32 valid = 0;  // bit k: record k of this thread exists
-  // A full tile of aligned columns is read 4 records per lane (16-byte
-  // group and 4-byte flag loads: 5 load instructions instead of 32); the
-  // histogram does not depend on which thread counts which record.
-  const bool vec = t0 + kTile <= geo.M && (reinterpret_cast<uintptr_t>(rg) & 15u) == 0 &&
-                   (reinterpret_cast<uintptr_t>(rf) & 3u) == 0;
-  if (vec) {
-#pragma unroll
-    for (int q = 0; q < kHistPer / 4; ++q) {
-      const u64 i = t0 + u64(q) * (4 * kBlock) + 4u * threadIdx.x;
-      const uint4 gv = *reinterpret_cast<const uint4*>(rg + i);
-      const u32 fv = *reinterpret_cast<const u32*>(rf + i);
-      gg[4 * q] = gv.x;
-      gg[4 * q + 1] = gv.y;
-      gg[4 * q + 2] = gv.z;
-      gg[4 * q + 3] = gv.w;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ff[4 * q + r] = (fv >> (8 * r)) & 0xFFu;
-    }
-    valid = (1u << kHistPer) - 1u;
-  } else {
-#pragma unroll
-    for (int k = 0; k < kHistPer; ++k) {
-      const u64 i = t0 + u64(k) * kBlock + threadIdx.x;
-      const bool in = i < geo.M;
-      gg[k] = in ? rg[i] : 0xFFFFFFFFu;
-      ff[k] = in ? rf[i] : 0u;
-      valid |= u32(in) << k;
-    }
-  }
-  if (threadIdx.x < 2) tl[threadIdx.x] = 0;
-  u32 nbad = 0, nnon = 0;  // wave-uniform counts
-#pragma unroll
-  for (int k = 0; k < kHistPer; ++k) {
-    const u32 g = gg[k];
-    const bool in = (valid >> k) & 1u, bad = in && g >= geo.G;
-    const bool non = in && !bad && (ff[k] & 0x0Fu) >= geo.n;
-    if (in && !bad && !non) atomicAdd(&lh[geo.sb_of(g)], 1u);
-    nbad += wave_popc(bad);
-    nnon += wave_popc(non);
-  }
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) {
-    if (nbad) atomicAdd(&tl[0], nbad);
-    if (nnon) atomicAdd(&tl[1], nnon);
-  }
-  for (u32 b = threadIdx.x; b < geo.NSB; b += kBlock) hist[u64(b) * geo.NT + tile] = lh[b];
-  __syncthreads();
-  if (threadIdx.x < 2) inval[2 * tile + threadIdx.x] = tl[threadIdx.x];
-}
-
-// K2: scan::k_scan_local (qb_scan.h) leaves per-4096 local exclusive scans in
-// hist; k_bk_sums_parts scans the block sums and derives the parts.  The
-// add-back pass is folded into the readers: offset i = hist[i] + bsum[i/4096]
-// (off_at), and hist[nbins] = total.
-__device__ __forceinline__ u32 off_at(const u32* __restrict__ hist, const u32* __restrict__ bsum,
-                                      u64 nb, u64 i) {
-  return i < nb ? hist[i] + bsum[i / kScanPer] : hist[nb];
-}
 
 // ------------------------------------------------ LDS tile partition ----
 // Counting sort of one tile (<= kTile records) by a small key, in LDS.  The
@@ -180,30 +96,32 @@ __device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec
 }
 
 // ---------------------------------------------------------------- K3 ----
-// Level 1: one block per tile of the original records; bins = super-buckets;
-// each bin's run goes to gstart[bin] (from the level-1 scan).  Every global
-// load of the tile (group, flags and both payload columns) is issued before
-// the first LDS step, so the loads overlap each other and the ranking; the
-// payload then goes register -> LDS -> permuted LDS read -> coalesced store.
+// Level 1: one block per tile of the original records; bins = super-buckets.
+// Every global load of the tile (group, flags and both payload columns) is
+// issued before the first LDS step, so the loads overlap each other and the
+// ranking.  Each super-bucket's run of the tile reserves its place in region
+// b * 8 + x (x = the XCD slot, blockIdx % 8) with one returning atomic on the
+// region's fill counter; what does not fit (a skewed batch) is marked (the
+// compact form: the chunk goes to the slow path) or appended to the overflow
+// area (the wide form).  Invalid records go to the stat shards.
 constexpr int kPer = kTile / kPartThreads;  // records per thread
-// Compact records (the tracker steps) go from registers straight to their
-// sorted LDS slot in K3 and K4 (round 3: K3 115 -> 112, K4 65 -> 61 us
-// against the permutation walk the wide columns still use).
-
-// (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs: the
-// direct placement's registers would otherwise leave one)
-// RESV: the compact records into reserved regions (the tracker steps); else
-// the scanned offsets (the leader step's wide columns).
-template <bool RESV>
+// (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs)
+// COMPACT: the 8-byte records (the tracker steps) go from registers straight
+// to their sorted LDS slot (round 3: K3 115 -> 112 us against the
+// permutation walk); else the wide columns (the leader step) move through
+// the permutation walk, one column at a time.
+struct NoOvf {};
+template <bool COMPACT>
 __global__ __launch_bounds__(kPartThreads)
 __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
-    const u64* __restrict__ ri, const u64* __restrict__ rt, const u32* __restrict__ offsets,
-    const u32* __restrict__ bsum, Cols out, u32* __restrict__ counts, u64* __restrict__ shards,
-    u8* __restrict__ chunk_slow) {
+    const u64* __restrict__ ri, const u64* __restrict__ rt, Cols out, u32* __restrict__ counts,
+    u64* __restrict__ shards, u8* __restrict__ chunk_slow,
+    std::conditional_t<COMPACT, NoOvf, Ovf> ovf) {
   extern __shared__ __attribute__((aligned(16))) u32 dyn[];
   u32* start = dyn;               // NSB: count, then local exclusive start
-  u32* gstart = dyn + geo.NSB;    // NSB: global start of (bin, tile)
+  u32* gstart = dyn + geo.NSB;    // NSB: the run's offset in its region
+  u32* obase = dyn + 2 * geo.NSB; // NSB (wide): overflow slot of region offset 0
   __shared__ TileLds L;
   const u32 tile = geo.tile();
   if (tile >= geo.NT) return;
@@ -233,6 +151,8 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     g[3] = gv.w;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) f[j] = (fv >> (8 * j)) & 0xFFu;
+    // (ri is never null; the guard stays because without it the compiler's
+    // allocation of the compact form spills 4 VGPRs instead of 1)
     if (ri) {
       const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ri + i);
       const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(ri + i + 2);
@@ -261,51 +181,58 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
       vt[j] = (in && ri) ? rt[t0 + k] : 0ull;
     }
   }
-  const u64 nb = geo.nbins();
-  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
-    start[b] = 0;
-    if constexpr (!RESV) gstart[b] = off_at(offsets, bsum, nb, u64(b) * geo.NT + tile);
-  }
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) start[b] = 0;
   __syncthreads();
-  if (RESV) {
-    // compact records: bin, rank and the encoded record stay in registers;
-    // after the scan each record is stored at its sorted LDS slot with its
-    // bin and chunk-low, and the output pass reads the slots in order
-    u32 bj[kPer], rj[kPer];  // bj: bin | chunk-low << 16
-    u64 vj[kPer];
-    u32 nbad = 0, nnon = 0;  // wave-uniform: invalid records (reserved regions)
+  // bj: bin | chunk-low << 16 (kNoBin for an invalid record), rj: its rank;
+  // compact: vj the encoded record (computed in the same pass, so the raw
+  // columns die early: two 1024-thread blocks per CU hold <= 64 VGPRs)
+  u32 bj[kPer], rj[kPer];
+  u64 vj[kPer];
+  u32 nbad = 0, nnon = 0;  // wave-uniform: invalid records
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = rk(j);
-      const bool ok = g[j] < geo.G && (f[j] & 0x0Fu) < geo.n;  // (k >= nrec has g = ~0)
-      {
-        const bool bad = k < nrec && g[j] >= geo.G;
-        nbad += wave_popc(bad);
-        nnon += wave_popc(k < nrec && !bad && !ok);
+  for (int j = 0; j < kPer; ++j) {
+    const u32 k = rk(j);
+    const bool ok = g[j] < geo.G && (f[j] & 0x0Fu) < geo.n;  // (k >= nrec has g = ~0)
+    {
+      const bool bad = k < nrec && g[j] >= geo.G;
+      nbad += wave_popc(bad);
+      nnon += wave_popc(k < nrec && !bad && !ok);
+    }
+    bj[j] = ok ? geo.sb_of(g[j]) : u32(kNoBin);
+    rj[j] = ok ? atomicAdd(&start[bj[j]], 1u) : 0u;
+    if constexpr (!COMPACT) {
+      if (k < nrec) {
+        L.bin[k] = u16(bj[j]);
+        L.rank[k] = u16(rj[j]);
       }
-      bj[j] = ok ? geo.sb_of(g[j]) : u32(kNoBin);
-      rj[j] = ok ? atomicAdd(&start[bj[j]], 1u) : 0u;
-      bj[j] |= geo.cl_of_chunk(geo.chunk_of(g[j])) << 16;
+    }
+    bj[j] |= geo.cl_of_chunk(geo.chunk_of(g[j])) << 16;
+    if constexpr (COMPACT)
       vj[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j], vt[j],
                              u32(t0 + k));
-    }
-    __syncthreads();
-    {
-      // reserved regions: this tile's run of super-bucket b goes to region
-      // b * 8 + x (x = the XCD slot, blockIdx % 8) at an offset drawn from
-      // the region's fill counter; invalid records go to the stat shards
-      const u32 x = blockIdx.x % kRegionShards;
-      for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
-        const u32 nbin = start[b];
-        if (nbin) gstart[b] = atomicAdd(&counts[b * kRegionShards + x], nbin);  // region-relative
-      }
-      if ((threadIdx.x & 63) == 0 && (nbad | nnon)) {
-        u64* sh = shards + u64(tile % kShards) * QB_STAT_COUNT;
-        if (nbad) atomicAdd(sh + QB_STAT_BAD_GROUP, u64(nbad));
-        if (nnon) atomicAdd(sh + QB_STAT_NON_MEMBER, u64(nnon));
+  }
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+    const u32 nbin = start[b];
+    if (!nbin) continue;
+    const u32 gs = atomicAdd(&counts[b * kRegionShards + blockIdx.x % kRegionShards], nbin);
+    gstart[b] = gs;  // region-relative
+    if constexpr (!COMPACT) {
+      if (gs + nbin > geo.cap) {  // the run's tail goes to the overflow area
+        const u32 lo = gs > geo.cap ? gs : geo.cap;
+        obase[b] = atomicAdd(ovf.total, gs + nbin - lo) - lo;
       }
     }
-    const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
+  }
+  if ((threadIdx.x & 63) == 0 && (nbad | nnon)) {
+    u64* sh = shards + u64(tile % kShards) * QB_STAT_COUNT;
+    if (nbad) atomicAdd(sh + QB_STAT_BAD_GROUP, u64(nbad));
+    if (nnon) atomicAdd(sh + QB_STAT_NON_MEMBER, u64(nnon));
+  }
+  const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
+  if constexpr (COMPACT) {
+    // after the scan each record is stored at its sorted LDS slot with its
+    // bin and chunk-low, and the output pass reads the slots in order
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const u32 b = bj[j] & 0xFFFFu;
@@ -330,249 +257,97 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     }
     return;
   } else {
-  if (vec) {  // a lane's 4 consecutive bins / ranks go out as one 8-byte LDS store each
-    u64 bins = 0, ranks = 0;
-    u32 cls = 0;
+    tile_perm(L, start, nrec);
+    const u32 x = blockIdx.x % kRegionShards;
+    // three columns, one at a time: index, term32, mr = meta | ridx << 32
+    for (int col = 0; col < 3; ++col) {
+      u64 v[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      u32 b = kNoBin, r = 0;
-      if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
-        b = geo.sb_of(g[j]);
-        r = atomicAdd(&start[b], 1u);
+      for (int j = 0; j < kPer; ++j) {
+        const u32 k = rk(j);
+        if (col == 0) {
+          v[j] = vi[j];
+        } else if (col == 1) {
+          v[j] = vt[j];
+        } else {
+          const u32 meta = (g[j] & (geo.CH - 1u)) | ((bj[j] >> 16) << 10) | ((f[j] & 0xFFu) << 17);
+          v[j] = u64(meta) | (u64(u32(t0 + k)) << 32);
+        }
       }
-      bins |= u64(b) << (16 * j);
-      ranks |= u64(r & 0xFFFFu) << (16 * j);
-      cls |= geo.cl_of_chunk(geo.chunk_of(g[j])) << (8 * j);
-    }
-    *reinterpret_cast<u64*>(&L.bin[4u * threadIdx.x]) = bins;
-    *reinterpret_cast<u64*>(&L.rank[4u * threadIdx.x]) = ranks;
-    if (out.compact) *reinterpret_cast<u32*>(&L.cl[4u * threadIdx.x]) = cls;
-  } else {
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = rk(j);
-      if (k >= nrec) continue;
-      u16 b = kNoBin;
-      if (g[j] < geo.G && (f[j] & 0x0Fu) < geo.n) {
-        b = u16(geo.sb_of(g[j]));
-        L.rank[k] = u16(atomicAdd(&start[b], 1u));
-        L.cl[k] = u8(geo.cl_of_chunk(geo.chunk_of(g[j])));
-      }
-      L.bin[k] = b;
-    }
-  }
-  __syncthreads();
-  const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
-  tile_perm(L, start, nrec);
-  // wide: three payload columns, index, term, mr = meta | ridx << 32;
-  // compact: one, the 8-byte record (RecFmt), plus the chunk-low bytes
-  for (int col = out.compact ? 2 : ri ? 0 : 2; col < 3; ++col) {
-    u64 v[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = rk(j);
-      if (col == 0) {
-        v[j] = vi[j];
-      } else if (col == 1) {
-        v[j] = vt[j];
-      } else if (out.compact) {
-        v[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j],
-                              vt[j], u32(t0 + k));
+      if (vec) {  // two 16-byte LDS stores per lane (8-byte stores at a 32-byte stride conflict)
+        *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x]) = ulonglong2{v[0], v[1]};
+        *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x + 2]) = ulonglong2{v[2], v[3]};
       } else {
-        const u32 chunk = geo.chunk_of(g[j]);
-        const u32 meta = (g[j] & (geo.CH - 1u)) | (geo.cl_of_chunk(chunk) << 10) |
-                         ((f[j] & 0xFFu) << 17);
-        v[j] = u64(meta) | (u64(u32(t0 + k)) << 32);
-      }
-    }
-    if (vec) {  // two 16-byte LDS stores per lane (8-byte stores at a 32-byte stride conflict)
-      *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x]) = ulonglong2{v[0], v[1]};
-      *reinterpret_cast<ulonglong2*>(&L.stage[4u * threadIdx.x + 2]) = ulonglong2{v[2], v[3]};
-    } else {
 #pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        if (rk(j) < nrec) L.stage[rk(j)] = v[j];
-    }
-    __syncthreads();
-    u64* dst = col == 0 ? out.index : col == 1 ? out.term : out.mr;
-    if (col == 1 && out.term32) {
+        for (int j = 0; j < kPer; ++j)
+          if (rk(j) < nrec) L.stage[rk(j)] = v[j];
+      }
+      __syncthreads();
       for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
         const u32 k = L.perm[e];
         const u32 b = L.bin[k];
-        out.term32[gstart[b] + (e - start[b])] = term_to32(L.stage[k]);
+        const u32 rel = gstart[b] + (e - start[b]);
+        const u64 val = L.stage[k];
+        if (rel < geo.cap) {
+          const u32 d = (b * kRegionShards + x) * geo.cap + rel;
+          if (col == 0) out.index[d] = val;
+          else if (col == 1) out.term32[d] = term_to32(val);
+          else out.mr[d] = val;
+        } else {  // past the region: the overflow area, the chunk flagged
+          const u32 o = obase[b] + rel;
+          if (col == 0) {
+            ovf.index[o] = val;
+          } else if (col == 1) {
+            ovf.term32[o] = term_to32(val);
+          } else {
+            const u32 c = geo.chunk_of_sb_cl(b, (u32(val) >> 10) & 127u);
+            ovf.mr[o] = val;
+            ovf.chunk[o] = c;
+            chunk_slow[c] = 1;
+            atomicAdd(&ovf.cnt[c], 1u);
+          }
+        }
       }
-    } else if (out.compact) {
-      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
-        const u32 k = L.perm[e];
-        const u32 d = gstart[L.bin[k]] + (e - start[L.bin[k]]);
-        dst[d] = L.stage[k];
-        out.cl[d] = L.cl[k];
-      }
-    } else {
-      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
-        const u32 k = L.perm[e];
-        const u32 b = L.bin[k];
-        dst[gstart[b] + (e - start[b])] = L.stage[k];
-      }
-    }
-    __syncthreads();
-  }
-  }  // !RESV
-}
-
-// --------------------------------------------------------------- K3b ----
-// One block: exclusive scan of the per-4096 scan-block sums (bsum, in
-// place; hist[nbins] = total), then the parts: super-bucket sb (records
-// [lo, hi) of buf1) is cut into ceil((hi - lo) / kTile) parts.  pfirst[sb] =
-// first part of sb, part_sb[p] = its super-bucket, nparts = pfirst[NSB].
-// It also writes the stat shards / flag words ([zero, zero + nzero) u64):
-// zero, except K1's invalid-record counts (inval) in shard 0.
-__global__ __launch_bounds__(1024) void k_bk_sums_parts(Geometry geo, u32* __restrict__ hist,
-                                                        u32* __restrict__ bsum, u32 nblk,
-                                                        u32* __restrict__ pt,
-                                                        const u32* __restrict__ inval,
-                                                        u64* __restrict__ zero, u32 nzero) {
-  __shared__ u32 sh[1024 + 32];
-  __shared__ u32 red[2][16];
-  // K1's per-tile (bad, non-member) pairs: 16-byte loads issued before the
-  // block-sum scan so their latency overlaps it (the carve pads inval to
-  // whole 16-byte pieces; pieces past 2 * NT are masked)
-  const u32 ne = 2 * geo.NT, nq = (ne + 3) / 4;
-  const uint4* iv4 = reinterpret_cast<const uint4*>(inval);
-  u32 nbad = 0, nnon = 0;
-  for (u32 q0 = 0; q0 < nq; q0 += 4 * 1024) {
-    uint4 v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const u32 q = q0 + u32(r) * 1024 + threadIdx.x;
-      v[r] = q < nq ? iv4[q] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const u32 e = 4 * (q0 + u32(r) * 1024 + threadIdx.x);
-      if (e < ne) nbad += v[r].x, nnon += v[r].y;
-      if (e + 2 < ne) nbad += v[r].z, nnon += v[r].w;
+      __syncthreads();
     }
   }
-  const u64 nb = geo.nbins();
-  u32 carry = 0;
-  for (u32 base = 0; base < nblk; base += 1024) {
-    const u32 i = base + threadIdx.x;
-    const u32 v = i < nblk ? bsum[i] : 0u;
-    u32 total;
-    const u32 ex = scan::block_exclusive_scan_1024(v, sh, &total);
-    if (i < nblk) bsum[i] = ex + carry;
-    carry += total;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) hist[nb] = carry;
-  // stat shards / flag words start at zero, except shard 0's invalid counts
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    nbad += __shfl_xor(nbad, o, 64);
-    nnon += __shfl_xor(nnon, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = nbad;
-    red[1][threadIdx.x >> 6] = nnon;
-  }
-  __syncthreads();
-  u64 tb = 0, tn = 0;
-  for (u32 w = 0; w < blockDim.x / 64; ++w) tb += red[0][w], tn += red[1][w];
-  for (u32 k = threadIdx.x; k < nzero; k += blockDim.x)
-    zero[k] = k == QB_STAT_BAD_GROUP ? tb : k == QB_STAT_NON_MEMBER ? tn : 0ull;
-  __threadfence_block();
-  __syncthreads();  // this block's bsum / hist[nb] stores are visible to it
-  u32* pfirst = pt;                  // NSB + 1
-  u32* part_sb = pt + geo.NSB + 2;   // max_parts
-  __shared__ u32 cnt[4096];
-  __shared__ u32 wsum[16];
-  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
-    const u32 n = off_at(hist, bsum, nb, u64(b + 1) * geo.NT) - off_at(hist, bsum, nb, u64(b) * geo.NT);
-    cnt[b] = (n + kTile - 1) / kTile;
-  }
-  __syncthreads();
-  const u32 total = tile_scan_bins(cnt, geo.NSB, wsum);
-  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
-    pfirst[b] = cnt[b];
-    const u32 n = (b + 1 < geo.NSB ? cnt[b + 1] : total) - cnt[b];
-    for (u32 q = 0; q < n; ++q) part_sb[cnt[b] + q] = b;
-  }
-  if (threadIdx.x == 0) pfirst[geo.NSB] = total;
 }
 
 // ---------------------------------------------------------------- K4 ----
-// Level 2: one block per part; counting sort of the part by chunk-low,
-// written to the SAME range of buf2; cs[p][c] = first record of chunk-low c
-// in part p (cs[p][128] = part end).
-__global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
-                                                           const u32* __restrict__ offsets,
-                                                           const u32* __restrict__ bsum,
-                                                           const u32* __restrict__ pt, Cols in,
-                                                           Cols out, u32* __restrict__ cs) {
-  const u32* pfirst = pt;
-  const u32* part_sb = pt + geo.NSB + 2;
+// Level 2 over the region grid: part p = region r's j-th kTile records
+// (p = r * ppx + j; a part past its region's fill exits after one load); a
+// counting sort of the part by chunk-low, written to the SAME range of buf2;
+// cs[p][c] = first record of chunk-low c in part p (cs[p][128] = part end).
+// The wide columns (the leader step) move through the permutation walk.
+__global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
+                                                                const u32* __restrict__ counts,
+                                                                Cols in, Cols out,
+                                                                u32* __restrict__ cs) {
   const u32 p = blockIdx.x;
-  if (p >= pfirst[geo.NSB]) return;  // fewer parts than the launch bound
+  const u32 r = p / geo.ppx, j0 = p - r * geo.ppx;
+  u32 fill = counts[r];
+  fill = fill < geo.cap ? fill : geo.cap;
+  if (j0 * u32(kTile) >= fill) return;  // no such part this call
   __shared__ TileLds L;
   __shared__ u32 start[kChunksPerSb];
-  const u32 sb = part_sb[p];
-  const u32 sb_lo = off_at(offsets, bsum, geo.nbins(), u64(sb) * geo.NT);
-  const u32 sb_hi = off_at(offsets, bsum, geo.nbins(), u64(sb + 1) * geo.NT);
-  const u32 lo = sb_lo + (p - pfirst[sb]) * u32(kTile);
-  const u32 hi = sb_hi - lo < u32(kTile) ? sb_hi : lo + u32(kTile);
-  const u32 nrec = hi - lo;
+  const u32 lo = r * geo.cap + j0 * u32(kTile);
+  const u32 nrec = fill - j0 * u32(kTile) < u32(kTile) ? fill - j0 * u32(kTile) : u32(kTile);
   // The payload columns are loaded now, with mr, and held in registers.
-  u64 vi[kPer], vt[kPer];
-  if (in.index) {
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = threadIdx.x + j * kPartThreads;
-      vi[j] = k < nrec ? in.index[lo + k] : 0ull;
-      vt[j] = k >= nrec     ? 0ull
-              : in.term32   ? u64(in.term32[lo + k])
-                            : in.term[lo + k];
-    }
-  }
-  u64 vm[kPer];  // loaded together: one round trip, not one per record
-  u32 vc[kPer];  // compact: the chunk-low bytes
+  u64 vi[kPer], vt[kPer], vm[kPer];  // loaded together: one round trip
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
+    vi[j] = k < nrec ? in.index[lo + k] : 0ull;
+    vt[j] = k < nrec ? u64(in.term32[lo + k]) : 0ull;
     vm[j] = k < nrec ? in.mr[lo + k] : 0ull;
-    vc[j] = k < nrec && in.compact ? u32(in.cl[lo + k]) : 0u;
   }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
-  if (in.compact) {
-    // compact records: each record's rank stays in a register and the record
-    // goes straight to its sorted LDS slot after the scan, so the output is
-    // read in order (no permutation array, no bin / rank stores)
-    u32 rk[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = threadIdx.x + j * kPartThreads;
-      rk[j] = k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u;
-    }
-    __syncthreads();
-    tile_scan_bins(start, kChunksPerSb, L.wsum);
-    if (threadIdx.x <= kChunksPerSb)
-      cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
-          lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const u32 k = threadIdx.x + j * kPartThreads;
-      if (k < nrec) L.stage[start[vc[j]] + rk[j]] = vm[j];
-    }
-    __syncthreads();
-    for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[e];
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
     if (k >= nrec) continue;
-    const u16 b = u16(in.compact ? vc[j] : (u32(vm[j]) >> 10) & 127u);
+    const u16 b = u16((u32(vm[j]) >> 10) & 127u);
     L.bin[k] = b;
     L.rank[k] = u16(atomicAdd(&start[b], 1u));
     L.stage[k] = vm[j];
@@ -585,19 +360,18 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split(Geometry geo,
   tile_perm(L, start, nrec);
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
   __syncthreads();
-  for (int col = in.index ? 0 : 2; col < 2; ++col) {
-    u64* dst = col == 0 ? out.index : out.term;
+  for (int col = 0; col < 2; ++col) {
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const u32 k = threadIdx.x + j * kPartThreads;
       if (k < nrec) L.stage[k] = col == 0 ? vi[j] : vt[j];
     }
     __syncthreads();
-    if (col == 1 && out.term32) {
+    if (col == 1) {
       for (u32 e = threadIdx.x; e < nrec; e += blockDim.x)
         out.term32[lo + e] = u32(L.stage[L.perm[e]]);
     } else {
-      for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) dst[lo + e] = L.stage[L.perm[e]];
+      for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.index[lo + e] = L.stage[L.perm[e]];
     }
     __syncthreads();
   }
@@ -921,67 +695,45 @@ namespace bk {
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool term32, bool compact) {
-  u32* hist = reinterpret_cast<u32*>(ws + cv.hist);
-  u32* bsum = reinterpret_cast<u32*>(ws + cv.bsum);
+                   hipStream_t st, bool compact) {
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
-  u32* pt = reinterpret_cast<u32*>(ws + cv.parts);
-  const int ncols = !rec_index || compact ? 1 : 3;
-  Cols buf1 = compact ? compact_at(ws + cv.buf1, ws + cv.cl) : cols_at(ws + cv.buf1, geo.M, ncols);
-  Cols buf2 = compact ? compact_at(ws + cv.buf2, nullptr) : cols_at(ws + cv.buf2, geo.M, ncols);
-  if (term32 && ncols == 3) {
-    buf1.term32 = reinterpret_cast<u32*>(buf1.term);
-    buf2.term32 = reinterpret_cast<u32*>(buf2.term);
-  }
-  const size_t lds_bins = sizeof(u32) * geo.NSB;
-  // k_bk_sums_parts zeroes the stat shards and flag words: [cv.shards, cv.flags + 256)
-  u64* zero = reinterpret_cast<u64*>(ws + cv.shards);
-  u32* inval = reinterpret_cast<u32*>(ws + cv.inval);
-  const u32 nzero = u32((cv.flags + 256 - cv.shards) / sizeof(u64));
+  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
+  u8* chunk_flags = reinterpret_cast<u8*>(ws + cv.chunk_flags);
+  // Reserved regions (round 4): the stat shards, the flag words, the
+  // regions' fill counters, the chunk flags (and the wide form's per-chunk
+  // overflow counts) are adjacent in the carve — one memset — and K3 reserves
+  // each tile's run of a super-bucket in its XCD slot's region with one
+  // atomic per (tile, super-bucket): no histogram pass, no scan, no part
+  // table (K1, K2 and the sums / parts kernel of round 3).  The chunk flags
+  // must start at 0: K3 marks overflowing chunks and their readers test the
+  // mark (a fresh workspace holds garbage; a stale mark would send a tracker
+  // chunk to the slow path and reset its groups' stepdown_at).
+  hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.zero_end - cv.shards, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
+  if (geo.M == 0) return QB_OK;
+  const unsigned kparts = geo.NSB * kRegionShards * geo.ppx;
   if (compact) {
-    // Reserved regions (round 4): the stat shards, the flag words, the
-    // regions' fill counters and the chunk flags are adjacent in the carve —
-    // one memset — and K3 reserves each tile's run of a super-bucket in its
-    // XCD slot's region with one atomic per (tile, super-bucket): no histogram
-    // pass, no scan, no part table (K1, K2 and the sums / parts kernel of
-    // round 3).  The chunk flags must start at 0 here: K3 marks overflowing
-    // chunks kChunkOverflow and K5 reads that mark before writing the flag
-    // (a fresh workspace holds garbage; a stale mark would send a chunk to
-    // the slow path and reset its groups' stepdown_at).
-    u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-    hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.chunk_flags + size_t(geo.NC) + 1 - cv.shards, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
-    if (geo.M == 0) return QB_OK;
-    hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st,
-                       geo, rec_group, rec_flags, rec_index, rec_term, nullptr, nullptr, buf1, counts,
-                       zero, reinterpret_cast<u8*>(ws + cv.chunk_flags));
+    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl), buf2 = compact_at(ws + cv.buf2, nullptr);
+    hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads),
+                       2 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
+                       buf1, counts, shards, chunk_flags, NoOvf{});
     QB_CHECK_LAUNCH("k_bk_scatter");
-    hipLaunchKernelGGL(k_bk_split_compact, dim3(geo.NSB * kRegionShards * geo.ppx), dim3(kSplitThreads), 0,
-                       st, geo, counts, buf1, buf2, cs);
+    hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts), dim3(kSplitThreads), 0, st, geo, counts, buf1,
+                       buf2, cs);
     QB_CHECK_LAUNCH("k_bk_split_compact");
     return QB_OK;
   }
-  if (geo.M == 0) {
-    hipError_t e = hipMemsetAsync(pt, 0, sizeof(u32) * (size_t(geo.NSB) + 1), st);
-    if (e == hipSuccess) e = hipMemsetAsync(zero, 0, sizeof(u64) * nzero, st);
-    return e == hipSuccess ? QB_OK : hip_fail(e, "hipMemsetAsync(parts)");
-  }
-  hipLaunchKernelGGL(k_bk_hist, dim3(geo.tile_grid()), dim3(kBlock), lds_bins, st, geo, rec_group,
-                     rec_flags, hist, inval);
-  QB_CHECK_LAUNCH("k_bk_hist");
-  const u64 nb = geo.nbins();
-  const u32 nblk = u32((nb + kScanPer - 1) / kScanPer);
-  hipLaunchKernelGGL(scan::k_scan_local, dim3(nblk), dim3(1024), 0, st, hist, nb, bsum);
-  hipLaunchKernelGGL(k_bk_sums_parts, dim3(1), dim3(1024), 0, st, geo, hist, bsum, nblk, pt,
-                     inval, zero, nzero);
-  QB_CHECK_LAUNCH("k_scan");
-  hipLaunchKernelGGL(k_bk_scatter<false>, dim3(geo.tile_grid()), dim3(kPartThreads), 2 * lds_bins, st,
-                     geo, rec_group, rec_flags, rec_index, rec_term, hist, bsum, buf1, nullptr, nullptr,
-                     nullptr);
+  // wide: index, term32 (in a u64 column's space) and mr
+  Cols buf1 = cols_at(ws + cv.buf1, cv.nrec, 3), buf2 = cols_at(ws + cv.buf2, cv.nrec, 3);
+  buf1.term32 = reinterpret_cast<u32*>(buf1.term);
+  buf2.term32 = reinterpret_cast<u32*>(buf2.term);
+  hipLaunchKernelGGL(k_bk_scatter<false>, dim3(geo.tile_grid()), dim3(kPartThreads),
+                     3 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term, buf1,
+                     counts, shards, chunk_flags, ovf_at(ws, cv, geo));
   QB_CHECK_LAUNCH("k_bk_scatter");
-  hipLaunchKernelGGL(k_bk_split, dim3(unsigned(max_parts(geo))), dim3(kPartThreads), 0, st,
-                     geo, hist, bsum, pt, buf1, buf2, cs);
-  QB_CHECK_LAUNCH("k_bk_split");
+  hipLaunchKernelGGL(k_bk_split_wide, dim3(kparts), dim3(kPartThreads), 0, st, geo, counts, buf1, buf2,
+                     cs);
+  QB_CHECK_LAUNCH("k_bk_split_wide");
   return QB_OK;
 }
 
@@ -1025,11 +777,11 @@ extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
   const int rc = fixed_tracker_check(n, G, M, workspace, workspace_bytes, &geo, &cv);
   if (rc != QB_OK) return rc;
   char* ws = static_cast<char*>(workspace);
-  // the stat shards and the flag words start at zero (K2 writes them)
+  // (bucket_records zeroes the stat shards and the flag words itself)
   return bk::bucket_records(geo, cv, ws, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
                             reinterpret_cast<const u64*>(rec_term),
                             reinterpret_cast<u64*>(ws + cv.shards), as_stream(stream),
-                            /*term32=*/false, /*compact=*/true);
+                            /*compact=*/true);
 }
 
 extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,

@@ -415,7 +415,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
   {
     const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags, ri, rtm, shards, st,
-                                      /*term32=*/false, /*compact=*/true);
+                                      /*compact=*/true);
     if (rc != QB_OK) return rc;
   }
   const bk::CsrStepArgs a{ri,

@@ -96,7 +96,7 @@ struct CsrLay {
 // Grid barrier over the co-resident blocks of k_bk_slow (MI355X_MICROARCH.md
 // "barrier-counter": lane-0 release fence before the arrive, relaxed poll,
 // acquire fence after).  ctr starts at 0 (zeroed with the stat shards by
-// k_bk_sums_parts); barrier k waits for k * gridDim.x arrivals.
+// bucket_records' memset); barrier k waits for k * gridDim.x arrivals.
 __device__ __forceinline__ void grid_barrier(u32* ctr, u32 target) {
   __syncthreads();
   if (threadIdx.x == 0) {

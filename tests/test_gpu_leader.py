@@ -228,6 +228,53 @@ def test_streaming_workload_vs_c_oracle(outbox):
 
 
 @pytest.mark.parametrize("outbox", [False, True])
+def test_skewed_batch_overflows_reserved_regions(outbox):
+    """A batch concentrated on two super-buckets (the first 65536 of 1M
+    groups) plus 10 % of the rest: their runs outgrow the reserved regions
+    (capacity ~2x an even share), the excess goes to the overflow area and
+    the flagged chunks collect it — every state array and message against
+    the C oracle, the bucketing's bad-group count included."""
+    import torch
+    from etcd_amd.quorum.leader import LeaderInbox, streaming_inbox, synth_streaming
+    from tests import oracle_c as oc
+    G = 1 << 20
+    lg, base = synth_streaming(G, device="cuda")
+    host = {k: v.copy() for k, v in lg.numpy().items()}
+    full = streaming_inbox(G, base, 0, device="cuda")
+    col = {n: getattr(full, n).cpu().numpy() for n in ("group", "flags", "index", "term", "hint",
+                                                       "log_term")}
+    grp = col["group"].view(np.uint32)
+    rng = np.random.default_rng(5)
+    keep = (grp < 65536) | (rng.random(grp.size) < 0.1)
+    keep[:64] = True
+    grp = grp.copy()
+    grp[:64] = G + 7  # a few bad groups, counted by the bucketing
+    flags = col["flags"][keep]
+    ib = LeaderInbox.from_numpy(grp[keep], flags & 0x0F, (flags >> 4) & 3,
+                                col["index"].view(np.uint64)[keep], col["term"].view(np.uint64)[keep],
+                                reject=(flags & 0x80) != 0, hint=col["hint"].view(np.uint64)[keep],
+                                log_term=col["log_term"].view(np.uint64)[keep])
+    M = int(keep.sum())
+    assert M > 150_000
+    res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=6 * M)
+    rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
+           "index": ib.index.cpu().numpy().view(np.uint64),
+           "term": ib.term.cpu().numpy().view(np.uint64),
+           "hint": ib.hint.cpu().numpy().view(np.uint64),
+           "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
+    msgs, total, sd, gf, stats = oc.leader_step(host, 32, 0, 0, rec, threads=16, msg_cap=6 * M)
+    dev = lg.numpy()
+    for name in host:
+        assert np.array_equal(dev[name], host[name]), name
+    assert res.msg_total == total
+    assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))
+    assert np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)
+    assert res.stats["applied"] == int(stats[0]) == M - 64
+    assert res.stats["bad_group"] == 64
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("outbox", [False, True])
 def test_readindex_workload_vs_c_oracle(outbox):
     """The ReadIndex bench workload (§8f row 2) at 256K groups: queues,
     released reads and every message against the C oracle."""
