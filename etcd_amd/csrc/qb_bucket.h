@@ -313,14 +313,19 @@ struct RunTable {
       const u32 y = u32(__shfl_up(int(x), o, 64));
       if (r >= u32(o)) x += y;
     }
+    // only the non-empty runs enter the table (a region's part past its fill
+    // or without this chunk's records counts nothing): the binary searches
+    // of locate() go over fewer rows
+    const u64 ne = __ballot(r < q.n && q.len != 0);
+    const u32 k = u32(__popcll(ne & ((1ull << r) - 1ull)));
     if (threadIdx.x < 64) {
-      if (r < q.n) {
-        lo[r] = q.l;
-        pre[r + 1] = x;
+      if ((ne >> r) & 1ull) {
+        lo[k] = q.l;
+        pre[k + 1] = x;
       }
       if (r == 0) {
         pre[0] = 0;
-        nr = q.n;
+        nr = u32(__popcll(ne));
       }
     }
     return u32(__shfl(int(x), 63, 64));  // lengths past n are 0
