@@ -332,11 +332,11 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   const u32 c = blockIdx.x, t = threadIdx.x;
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   cur[t] = 0;
-  const bk::RunTable::Regs rq = bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl);
-  const u32 total1 = rt.finish(rq);  // the region records (workgroup-uniform)
+  if (t < 64) rt.finish(bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl));  // wave 0
   // overflow records of this chunk (K3 flagged it): the area is scanned
   const u32 novf = chunk_flags[c] ? *ovf.total : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published
+  const u32 total1 = rt.pre[rt.nr];  // the region records (workgroup-uniform)
   // Common case (round 3, one pass): no overflow and at most kStageRecs
   // records — each record is loaded once, into registers (kRegRecs per
   // thread), counted from there and placed from there; otherwise the
