@@ -110,6 +110,11 @@ constexpr u32 kXcds = 8;
 // us per 16M-group tick, 4 / 2 / 1 regions (written by several XCDs)
 // 569-606 us, round 3's scanned offsets 573-576 us.
 constexpr u32 kRegionShards = kXcds;
+// Rows of a chunk's run table (RunTable): kRegionShards regions x up to 32
+// parts of kTile per super-bucket, so a region holds up to 131072 records
+// (batches of up to ~8 records per group per call before the reserved
+// regions overflow; round 4 started with 64 rows, i.e. ~2 per group).
+constexpr u32 kMaxRows = 256;
 // interleaved super-buckets (Geometry::il) for the tracker steps
 constexpr bool kSbIl = true;
 // K5 write-back (k_bk_apply, k_csr_apply): a wave whose 64-element segment
@@ -185,7 +190,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   g.fmt.tb = kRecHdrBits - 1u - g.fmt.lgb - g.fmt.slb;
   // reserved regions: twice a region's mean share plus 256 records, capped
   // by what the region's tiles can hold at most (a small batch never
-  // overflows) and by the run table's 64 rows per super-bucket
+  // overflows) and by the run table's kMaxRows rows per super-bucket
   const u64 S = kRegionShards;
   // a region's mean share for records spread evenly over the groups: the
   // fullest super-bucket holds mc of the NC chunks (interleaved: a window's
@@ -202,7 +207,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   worst = worst < M ? worst : M;
   u64 cap = (2 * m + 256 + 255) / 256 * 256;  // (256-record granules)
   cap = cap < worst ? cap : (worst + 255) / 256 * 256;
-  const u64 capmax = 64 / S * kTile;  // the run table's 64 rows per super-bucket
+  const u64 capmax = kMaxRows / S * kTile;  // the run table's rows per super-bucket
   cap = cap < 256 ? 256 : cap > capmax ? capmax : cap;
   g.cap = u32(cap);
   g.ppx = u32((cap + kTile - 1) / kTile);
@@ -274,8 +279,15 @@ inline Cols compact_at(char* base, char* cl) {
 // Run table of one chunk: the chunk's run in each of up to kRuns parts of
 // its super-bucket's regions, with an inclusive prefix of run lengths so
 // flattened record f maps to a buffer index by binary search.
-struct RunTable {
-  static constexpr u32 kRuns = 64;
+// Lane r's row of a run table (RunTableT::issue_regions).
+struct RunRegs {
+  u32 l, len, n;
+};
+// R rows of LDS (kMaxRows for the MANY instantiations, 64 otherwise: the
+// common kernels keep their LDS and so their occupancy).
+template <u32 R>
+struct RunTableT {
+  static constexpr u32 kRuns = R;
   u32 lo[kRuns];
   u32 pre[kRuns + 1];
   u32 nr;
@@ -284,51 +296,72 @@ struct RunTable {
   // wave 0 publishes the table.  The caller synchronises before locate().
   // (Two halves, so a caller can keep the table's loads in flight ahead of
   // its own bulk loads: vector loads retire in order.)
-  struct Regs {
-    u32 l, len, n;
-  };
-  // A chunk's runs: super-bucket sb's parts are rows sb * S *
-  // ppx + r of the region grid (S = kRegionShards), r = x * ppx + j; part j
-  // of region x exists iff j * kTile < its fill (counts, clamped to cap).
-  // Lane r loads its row and its region's count in one round trip (S * ppx
-  // <= 64 rows).
+  using Regs = RunRegs;
+  // A chunk's runs: super-bucket sb's parts are rows sb * S * ppx + rr of the
+  // region grid (S = kRegionShards), rr = x * ppx + j; part j of region x
+  // exists iff j * kTile < its fill (counts, clamped to cap).
+  __device__ __forceinline__ static void row_run(const u32* __restrict__ cs,
+                                                 const u32* __restrict__ counts, u32 sb, u32 ppx,
+                                                 u32 cap, u32 cl, u32 n, u32 rr_in, u32& l,
+                                                 u32& len) {
+    const bool in = rr_in < n;
+    const u32 rr = in ? rr_in : 0u;
+    const u32 x = rr / ppx, j = rr - x * ppx;
+    const u64 row = (u64(sb) * n + rr) * (kChunksPerSb + 1);
+    l = cs[row + cl];
+    const u32 h = cs[row + cl + 1];
+    u32 fill = counts[sb * kRegionShards + x];
+    fill = fill < cap ? fill : cap;
+    len = in && j * u32(kTile) < fill ? h - l : 0u;
+  }
+  // Lane r loads row r and its region's count in one round trip.
   __device__ __forceinline__ static Regs issue_regions(const u32* __restrict__ cs,
                                                        const u32* __restrict__ counts, u32 sb,
                                                        u32 ppx, u32 cap, u32 cl) {
     const u32 n = kRegionShards * ppx;
-    const u32 r = threadIdx.x & 63u;
-    const u32 rr = r < n ? r : 0u;
-    const u32 x = rr / ppx, j = rr - x * ppx;
-    const u64 row = (u64(sb) * n + rr) * (kChunksPerSb + 1);
-    const u32 l = cs[row + cl], h = cs[row + cl + 1];
-    u32 fill = counts[sb * kRegionShards + x];
-    fill = fill < cap ? fill : cap;
-    return Regs{l, r < n && j * u32(kTile) < fill ? h - l : 0u, n};
+    Regs q;
+    q.n = n;
+    row_run(cs, counts, sb, ppx, cap, cl, n, threadIdx.x & 63u, q.l, q.len);
+    return q;
   }
-  __device__ __forceinline__ u32 finish(const Regs& q) {
+  // Only the non-empty runs enter the table (a region's part past its fill
+  // or without this chunk's records counts nothing), so the binary searches
+  // of locate() go over fewer rows.  Returns the chunk's record count (every
+  // lane).  MANY = false: up to 64 rows (8 parts per region), one pass from
+  // the registers issue_regions() filled.  MANY = true (a batch of several
+  // records per group: more than 8 parts per region, many_rows()): 64 rows
+  // per pass, the rows past the first 64 loaded here.  The kernels are
+  // instantiated for both, so the common one keeps its registers.
+  __host__ __device__ static constexpr bool many_rows(u32 ppx) { return kRegionShards * ppx > 64; }
+  template <bool MANY>
+  __device__ __forceinline__ u32 finish(const Regs& q, const u32* __restrict__ cs,
+                                        const u32* __restrict__ counts, u32 sb, u32 ppx, u32 cap,
+                                        u32 cl) {
     const u32 r = threadIdx.x & 63u;
-    u32 x = q.len;
+    u32 carry = 0, kb = 0;
+    for (u32 p0 = 0; p0 < (MANY ? q.n : 1u); p0 += 64) {
+      u32 l = q.l, len = q.len;
+      if (MANY && p0) row_run(cs, counts, sb, ppx, cap, cl, q.n, p0 + r, l, len);
+      u32 x = len;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const u32 y = u32(__shfl_up(int(x), o, 64));
-      if (r >= u32(o)) x += y;
-    }
-    // only the non-empty runs enter the table (a region's part past its fill
-    // or without this chunk's records counts nothing): the binary searches
-    // of locate() go over fewer rows
-    const u64 ne = __ballot(r < q.n && q.len != 0);
-    const u32 k = u32(__popcll(ne & ((1ull << r) - 1ull)));
-    if (threadIdx.x < 64) {
-      if ((ne >> r) & 1ull) {
-        lo[k] = q.l;
-        pre[k + 1] = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = u32(__shfl_up(int(x), o, 64));
+        if (r >= u32(o)) x += y;
       }
-      if (r == 0) {
-        pre[0] = 0;
-        nr = u32(__popcll(ne));
+      const u64 ne = __ballot(len != 0);
+      const u32 k = kb + u32(__popcll(ne & ((1ull << r) - 1ull)));
+      if (threadIdx.x < 64 && ((ne >> r) & 1ull)) {
+        lo[k] = l;
+        pre[k + 1] = carry + x;
       }
+      carry += u32(__shfl(int(x), 63, 64));
+      kb += u32(__popcll(ne));
     }
-    return u32(__shfl(int(x), 63, 64));  // lengths past n are 0
+    if (threadIdx.x == 0) {
+      pre[0] = 0;
+      nr = kb;
+    }
+    return carry;
   }
   __device__ __forceinline__ u32 locate(u32 f) const {
     u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
@@ -340,9 +373,10 @@ struct RunTable {
     return lo[a] + (f - pre[a]);
   }
   // locate() unrolled for a caller in straight-line code (no loop: exact
-  // wait counts); nr <= kRuns = 64.
+  // wait counts) for tables of at most 64 runs; MANY takes the loop.
+  template <bool MANY>
   __device__ __forceinline__ u32 locate_fixed(u32 f) const {
-    static_assert(kRuns == 64, "six halvings");
+    if constexpr (MANY) return locate(f);
     const u32 n = nr;
     u32 a = 0;
 #pragma unroll
@@ -354,6 +388,9 @@ struct RunTable {
     return lo[a] + (f - pre[a]);
   }
 };
+using RunTable = RunTableT<kMaxRows>;
+template <bool MANY>
+using RunTableOf = RunTableT<MANY ? kMaxRows : 64u>;
 
 // K3-K4 of the bucketed pipeline: records (any order) -> buf2 holds each
 // chunk's records as one run per part of its super-bucket's reserved regions;

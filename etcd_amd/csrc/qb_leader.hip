@@ -317,6 +317,7 @@ __device__ __forceinline__ ChunkStage& chunk_stage() {
 // arbitrary; the step sorts each run.  The chunk's records are its runs in
 // the parts of its super-bucket's regions (one run table) and, for a chunk
 // flagged by K3 (a skewed batch), its records in the overflow area.
+template <bool MANY>
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::Cols recs,
                                                           const u32* __restrict__ counts,
                                                           const u32* __restrict__ cs,
@@ -326,13 +327,15 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
                                                           u32* __restrict__ cnt,
                                                           u32* __restrict__ perm,
                                                           qb_leader_inbox in, RecCols rc) {
-  __shared__ bk::RunTable rt;
+  __shared__ bk::RunTableOf<MANY> rt;
   __shared__ u32 cur[kCh];
   __shared__ u32 wsum[kBlock / 64];
   const u32 c = blockIdx.x, t = threadIdx.x;
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   cur[t] = 0;
-  if (t < 64) rt.finish(bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl));  // wave 0
+  if (t < 64)  // wave 0
+    rt.template finish<MANY>(bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl), cs,
+                             counts, sb, geo.ppx, geo.cap, cl);
   // overflow records of this chunk (K3 flagged it): the area is scanned
   const u32 novf = chunk_flags[c] ? *ovf.total : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published
@@ -1297,9 +1300,13 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
     QB_CHECK_LAUNCH("scan(chunks)");
     bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, c.bcv.nrec, 3);
     b2.term32 = reinterpret_cast<u32*>(b2.term);
-    hipLaunchKernelGGL(ld::k_ld_chunk_runs, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo,
-                       b2, counts, cs, reinterpret_cast<const u8*>(bws + c.bcv.chunk_flags), ovf,
-                       ctot, cnt, perm, *in, rcols);
+    const u8* cfl = reinterpret_cast<const u8*>(bws + c.bcv.chunk_flags);
+    if (bk::RunTable::many_rows(c.geo.ppx))
+      hipLaunchKernelGGL(ld::k_ld_chunk_runs<true>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
+                         counts, cs, cfl, ovf, ctot, cnt, perm, *in, rcols);
+    else
+      hipLaunchKernelGGL(ld::k_ld_chunk_runs<false>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
+                         counts, cs, cfl, ovf, ctot, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");
   } else {
     u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);

@@ -447,7 +447,7 @@ __host__ __device__ constexpr u32 k5_block(int n) {
 // waves per SIMD (MI355X_MICROARCH.md, residency), so the compiler's 92
 // SGPRs held K5 at 3 workgroups per CU where its VGPRs and LDS allow 4;
 // capped at 80 (a few SGPRs spill to VGPR lanes): -11 us per 16M-group tick.
-template <int N, bool NEXT>
+template <int N, bool NEXT, bool MANY>
 __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) void k_bk_apply(
     Geometry geo, Cols recs, const u32* __restrict__ counts, const u32* __restrict__ cs,
     const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
     const u32 lg = threadIdx.x + k * B;
     gtr[k] = group_term[g0 + (lg < ng ? lg : ng - 1)];
   }
-  __shared__ RunTable rt;
+  __shared__ RunTableOf<MANY> rt;
   const RunTable::Regs rq = RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl);
   u64 v[GPT][N], cm[GPT], ts[GPT];
   u32 av[GPT];
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   // flattened into one index space (RunTable) so every thread has a record
   // in flight at once; kRecPer records per thread, both columns of each
   // loaded before the first is classified.
-  u32 total = rt.finish(rq);
+  u32 total = rt.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
   __syncthreads();
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
       const u32 f = f0 + u32(r) * B + threadIdx.x;
-      ix[r] = tot ? rt.locate_fixed(f < tot ? f : tot - 1) : 0u;
+      ix[r] = tot ? rt.template locate_fixed<MANY>(f < tot ? f : tot - 1) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
@@ -647,20 +647,24 @@ struct ApplyArgs {
   u64* stats;
 };
 
+template <int N, bool MANY>
+void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
+                       const ApplyArgs& a, hipStream_t st) {
+  if (a.next)
+    hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
+                       counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats);
+  else
+    hipLaunchKernelGGL((k_bk_apply<N, false, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
+                       counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats);
+}
 template <int N>
 void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                   const ApplyArgs& a, hipStream_t st) {
-  if (a.next)
-    hipLaunchKernelGGL((k_bk_apply<N, true>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, counts,
-                       cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
-                       a.chunk_slow, a.any_slow, a.stats);
-  else
-    hipLaunchKernelGGL((k_bk_apply<N, false>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs, counts,
-                       cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown, a.adv,
-                       a.chunk_slow, a.any_slow, a.stats);
+  if (RunTable::many_rows(geo.ppx)) launch_apply_rows<N, true>(geo, recs, counts, cs, a, st);
+  else launch_apply_rows<N, false>(geo, recs, counts, cs, a, st);
 }
-
-
 
 template <int N>
 void launch_slow(const Geometry& geo, const ApplyArgs& a, const SlowArgs& s, u64* stats,

@@ -61,7 +61,7 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
       stepdown_at, advanced, chunk_slow, any_slow, shards
 
 // One chunk c (the whole workgroup).
-template <int WMAX, int CAPW, bool NEXT, bool SECOND>
+template <int WMAX, int CAPW, bool NEXT, bool SECOND, bool MANY>
 __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS) {
   constexpr u32 CH = csr_chunk_groups(WMAX);
   constexpr u32 B = csr_block();
@@ -75,7 +75,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   __shared__ u32 act[CH];
   __shared__ u32 slow;
   __shared__ u32 tl[4];
-  __shared__ RunTable rtab;
+  __shared__ RunTableOf<MANY> rtab;
   BlockTally<4> tally;  // stale, applied, rejected, non-member
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
@@ -164,7 +164,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
       return;
     }
   }
-  u32 total = rtab.finish(rq);
+  u32 total = rtab.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
   __syncthreads();
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
@@ -174,7 +174,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) {
       const u32 f = f0 + u32(r) * B + threadIdx.x;
-      ix[r] = n ? rtab.locate_fixed(f < n ? f : n - 1) : 0u;
+      ix[r] = n ? rtab.template locate_fixed<MANY>(f < n ? f : n - 1) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
@@ -292,9 +292,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
 }
 
-template <int WMAX, int CAPW, bool NEXT>
+template <int WMAX, int CAPW, bool NEXT, bool MANY>
 __global__ __launch_bounds__(csr_block()) void k_csr_apply(QB_CSR_APPLY_PARAMS) {
-  csr_apply_chunk<WMAX, CAPW, NEXT, false>(blockIdx.x, QB_CSR_APPLY_ARGS);
+  csr_apply_chunk<WMAX, CAPW, NEXT, false, MANY>(blockIdx.x, QB_CSR_APPLY_ARGS);
 }
 
 // The deferred chunks: a workgroup per kDeferSpan consecutive chunks reads
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply(QB_CSR_APPLY_PARAMS) 
 // chunk cost ~25 us even with nothing deferred: every one of them reserved
 // the big buffer's LDS).
 constexpr u32 kDeferSpan = 64;
-template <int WMAX, int CAPW, bool NEXT>
+template <int WMAX, int CAPW, bool NEXT, bool MANY>
 __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY_PARAMS) {
   __shared__ u64 mask;
   const u32 c0 = blockIdx.x * kDeferSpan;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY
   __syncthreads();
   for (u64 m = mask; m; m &= m - 1) {  // block-uniform
     __syncthreads();  // the previous chunk's readers of the LDS state are done
-    csr_apply_chunk<WMAX, CAPW, NEXT, true>(c0 + u32(__builtin_ctzll(m)), QB_CSR_APPLY_ARGS);
+    csr_apply_chunk<WMAX, CAPW, NEXT, true, MANY>(c0 + u32(__builtin_ctzll(m)), QB_CSR_APPLY_ARGS);
   }
 }
 
@@ -332,13 +332,14 @@ struct CsrStepArgs {
   u64* shards;
 };
 
-template <int WMAX, bool SECOND>
-void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
-                  const CsrStepArgs& a, hipStream_t st) {
+template <int WMAX, bool SECOND, bool MANY>
+void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
+                       const CsrStepArgs& a, hipStream_t st) {
   constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
 #define QB_CSR_LAUNCH(NX)                                                                       \
-  hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX> : k_csr_apply<WMAX, CAPW, NX>), \
+  hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX, MANY>                        \
+                             : k_csr_apply<WMAX, CAPW, NX, MANY>),                                 \
                      grid, dim3(csr_block()), 0, st, geo, recs, counts, cs, a.ri, a.rt, a.off, a.cfg, \
                      a.gt, a.ts,                                                                   \
                      a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
@@ -346,6 +347,12 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* 
   if (a.next) QB_CSR_LAUNCH(true);
   else QB_CSR_LAUNCH(false);
 #undef QB_CSR_LAUNCH
+}
+template <int WMAX, bool SECOND>
+void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
+                  const CsrStepArgs& a, hipStream_t st) {
+  if (RunTable::many_rows(geo.ppx)) launch_apply_rows<WMAX, SECOND, true>(geo, recs, counts, cs, a, st);
+  else launch_apply_rows<WMAX, SECOND, false>(geo, recs, counts, cs, a, st);
 }
 
 template <int WMAX>

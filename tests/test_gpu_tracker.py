@@ -446,3 +446,29 @@ def test_step_skewed_batch_overflows_reserved_regions(hot_frac):
     want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
                      "bad_group", "after_stepdown"), stats.tolist()))
     assert {k: got[k] for k in want} == want
+
+
+@pytest.mark.timeout(300)
+def test_step_dense_batch_many_parts_per_region():
+    """Eight records per group in one call (every follower acks twice): a
+    region's share is ~32K records, so the regions hold up to 17 parts each
+    and a chunk's run table has more than 64 rows (RunTable::finish loads
+    them in passes, locate falls back to its loop) — equal to the sequential
+    oracle, stats included."""
+    n, G, M = 5, 1 << 18, 1 << 21
+    rng = np.random.default_rng(91)
+    st = _random_state(rng, n, G)
+    tr = _tracker_from(n, st, track_next=False)
+    st.pop("next")
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, st, higher=0.0002,
+                                                         nonmember=0.001)
+    stats = oc.appresp_sequential(n, G, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    assert np.array_equal(batch.as_u64(tr.match), st["match"])
+    assert np.array_equal(batch.as_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+    got = tr.stats_dict()
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert {k: got[k] for k in want} == want

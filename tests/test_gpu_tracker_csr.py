@@ -440,3 +440,21 @@ def test_csr_step_skewed_batch_overflows_reserved_regions():
     want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
                      "bad_group", "after_stepdown"), stats.tolist()))
     assert tr.stats_dict() == want
+
+
+@pytest.mark.timeout(300)
+def test_csr_step_dense_batch_many_parts_per_region():
+    """The CSR step with eight records per group in one call: run tables of
+    more than 64 rows (see the FIXED test of the same name)."""
+    G, M = 1 << 18, 1 << 21
+    rng = np.random.default_rng(92)
+    off, cfg, sizes, st = _state(rng, "ragged", G)
+    st.pop("next")
+    tr = _tracker(off, cfg, st, track_next=False)
+    group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, higher=0.0002)
+    stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    _compare(tr, st, G)
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert tr.stats_dict() == want
