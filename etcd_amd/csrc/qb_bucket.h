@@ -115,6 +115,15 @@ constexpr u32 kRegionShards = kXcds;
 // (batches of up to ~8 records per group per call before the reserved
 // regions overflow; round 4 started with 64 rows, i.e. ~2 per group).
 constexpr u32 kMaxRows = 256;
+// Parts of a region (K4): kTile records each, the last one up to kTile +
+// slack so a region just past a multiple of kTile does not leave a part of a
+// few records (each such part adds a run of ~1 record to every chunk's table:
+// a line fetched per column for one record).  The wide form (the leader's
+// K4, a 1024 x 5-record tile) takes kWideSlack; the compact form none.
+constexpr u32 kWideSlack = 1024;
+__host__ __device__ __forceinline__ u32 region_parts(u32 fill, u32 slack) {
+  return fill <= u32(kTile) + slack ? (fill ? 1u : 0u) : (fill - slack + u32(kTile) - 1u) / u32(kTile);
+}
 // interleaved super-buckets (Geometry::il) for the tracker steps
 constexpr bool kSbIl = true;
 // K5 write-back (k_bk_apply, k_csr_apply): a wave whose 64-element segment
@@ -281,7 +290,7 @@ inline Cols compact_at(char* base, char* cl) {
 // flattened record f maps to a buffer index by binary search.
 // Lane r's row of a run table (RunTableT::issue_regions).
 struct RunRegs {
-  u32 l, len, n;
+  u32 l, len, n, slack;
 };
 // R rows of LDS (kMaxRows for the MANY instantiations, 64 otherwise: the
 // common kernels keep their LDS and so their occupancy).
@@ -303,7 +312,7 @@ struct RunTableT {
   __device__ __forceinline__ static void row_run(const u32* __restrict__ cs,
                                                  const u32* __restrict__ counts, u32 sb, u32 ppx,
                                                  u32 cap, u32 cl, u32 n, u32 rr_in, u32& l,
-                                                 u32& len) {
+                                                 u32& len, u32 slack) {
     const bool in = rr_in < n;
     const u32 rr = in ? rr_in : 0u;
     const u32 x = rr / ppx, j = rr - x * ppx;
@@ -312,16 +321,18 @@ struct RunTableT {
     const u32 h = cs[row + cl + 1];
     u32 fill = counts[sb * kRegionShards + x];
     fill = fill < cap ? fill : cap;
-    len = in && j * u32(kTile) < fill ? h - l : 0u;
+    len = in && j < region_parts(fill, slack) ? h - l : 0u;
   }
-  // Lane r loads row r and its region's count in one round trip.
+  // Lane r loads row r and its region's count in one round trip (slack: the
+  // form's last-part slack, region_parts).
   __device__ __forceinline__ static Regs issue_regions(const u32* __restrict__ cs,
                                                        const u32* __restrict__ counts, u32 sb,
-                                                       u32 ppx, u32 cap, u32 cl) {
+                                                       u32 ppx, u32 cap, u32 cl, u32 slack = 0) {
     const u32 n = kRegionShards * ppx;
     Regs q;
     q.n = n;
-    row_run(cs, counts, sb, ppx, cap, cl, n, threadIdx.x & 63u, q.l, q.len);
+    q.slack = slack;
+    row_run(cs, counts, sb, ppx, cap, cl, n, threadIdx.x & 63u, q.l, q.len, slack);
     return q;
   }
   // Only the non-empty runs enter the table (a region's part past its fill
@@ -341,7 +352,7 @@ struct RunTableT {
     u32 carry = 0, kb = 0;
     for (u32 p0 = 0; p0 < (MANY ? q.n : 1u); p0 += 64) {
       u32 l = q.l, len = q.len;
-      if (MANY && p0) row_run(cs, counts, sb, ppx, cap, cl, q.n, p0 + r, l, len);
+      if (MANY && p0) row_run(cs, counts, sb, ppx, cap, cl, q.n, p0 + r, l, len, q.slack);
       u32 x = len;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {

@@ -85,6 +85,10 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
   Carve c{};
   size_t o = 0;
   c.geo = bk::geometry(16, G, M);
+  // the wide form's last part takes kWideSlack more records (bk::region_parts),
+  // so a region has fewer parts: fewer run-table rows for every chunk
+  const u32 wp = bk::region_parts(c.geo.cap, bk::kWideSlack);
+  c.geo.ppx = wp ? wp : 1u;
   c.bucketed = c.geo.NSB <= 4096;
   if (c.bucketed) {
     c.bcv = bk::carve(c.geo, 3);
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_gather(u64 G, qb_leader_inbox in,
 
 // --------------------------------------------------------- L2 / L3 (bk) ----
 // Records of chunk c: the sum of its runs over the parts of its super-bucket's
-// regions (a part exists iff j * kTile < its region's fill), plus the chunk's
+// regions (bk::region_parts with the wide form's slack), plus the chunk's
 // records in the overflow area.
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
                                                            const u32* __restrict__ counts,
@@ -290,7 +294,8 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
   for (u32 x = 0; x < bk::kRegionShards; ++x) {
     u32 fill = counts[sb * bk::kRegionShards + x];
     fill = fill < geo.cap ? fill : geo.cap;
-    for (u32 j = 0; j < geo.ppx && j * u32(bk::kTile) < fill; ++j) {
+    const u32 np = bk::region_parts(fill, bk::kWideSlack);
+    for (u32 j = 0; j < geo.ppx && j < np; ++j) {
       const u64 row = (u64(sb) * nrow + x * geo.ppx + j) * (bk::kChunksPerSb + 1) + cl;
       s += cs[row + 1] - cs[row];
     }
@@ -334,8 +339,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   cur[t] = 0;
   if (t < 64)  // wave 0
-    rt.template finish<MANY>(bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl), cs,
-                             counts, sb, geo.ppx, geo.cap, cl);
+    rt.template finish<MANY>(
+        bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack), cs, counts,
+        sb, geo.ppx, geo.cap, cl);
   // overflow records of this chunk (K3 flagged it): the area is scanned
   const u32 novf = chunk_flags[c] ? *ovf.total : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published

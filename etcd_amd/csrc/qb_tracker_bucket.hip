@@ -87,7 +87,8 @@ __device__ __forceinline__ u32 tile_scan_bins(u32* cnt, u32 nb, u32* wsum) {
   return total;
 }
 
-__device__ __forceinline__ void tile_perm(TileLds& L, const u32* start, u32 nrec) {
+template <class Lds>
+__device__ __forceinline__ void tile_perm(Lds& L, const u32* start, u32 nrec) {
   for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
     const u16 b = L.bin[k];
     if (b != kNoBin) L.perm[start[b] + L.rank[k]] = u16(k);
@@ -314,28 +315,46 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
 }
 
 // ---------------------------------------------------------------- K4 ----
-// Level 2 over the region grid: part p = region r's j-th kTile records
-// (p = r * ppx + j; a part past its region's fill exits after one load); a
-// counting sort of the part by chunk-low, written to the SAME range of buf2;
-// cs[p][c] = first record of chunk-low c in part p (cs[p][128] = part end).
-// The wide columns (the leader step) move through the permutation walk.
+// Level 2 over the region grid: part p = region r's j-th part (p = r * ppx
+// + j; kTile records, the last one up to kTile + kWideSlack: region_parts;
+// a part past its region's fill exits after one load); a counting sort of
+// the part by chunk-low, written to the SAME range of buf2; cs[p][c] = first
+// record of chunk-low c in part p (cs[p][128] = part end).  The wide columns
+// (the leader step) move through the permutation walk.
+constexpr u32 kWideTile = kTile + kWideSlack;
+constexpr int kPerW = int(kWideTile / kPartThreads);  // records per thread
+static_assert(kWideTile % kPartThreads == 0, "whole records per thread");
+struct alignas(16) TileLdsW {
+  u16 bin[kWideTile];
+  u16 rank[kWideTile];
+  u16 perm[kWideTile];
+  u64 stage[kWideTile];
+  u32 wsum[kPartThreads / 64];
+};
 __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
                                                                 const u32* __restrict__ counts,
                                                                 Cols in, Cols out,
                                                                 u32* __restrict__ cs) {
-  const u32 p = blockIdx.x;
-  const u32 r = p / geo.ppx, j0 = p - r * geo.ppx;
+  // part-major order: workgroup b takes part j0 = b / R of region r = b % R
+  // (R = NSB x 8), so the first parts of neighbouring regions go to
+  // different XCDs whatever ppx is (region-major order put every first part
+  // on the XCDs b % 8 = (r * ppx) % 8: two of eight for an even ppx), and
+  // region (sb, x)'s first part runs on the XCD slot x that wrote it in K3
+  const u32 R = geo.NSB * kRegionShards;
+  const u32 j0 = blockIdx.x / R, r = blockIdx.x - j0 * R;
+  const u32 p = r * geo.ppx + j0;  // the part's run-table row
   u32 fill = counts[r];
   fill = fill < geo.cap ? fill : geo.cap;
-  if (j0 * u32(kTile) >= fill) return;  // no such part this call
-  __shared__ TileLds L;
+  const u32 np = region_parts(fill, kWideSlack);
+  if (j0 >= np) return;  // no such part this call
+  __shared__ TileLdsW L;
   __shared__ u32 start[kChunksPerSb];
   const u32 lo = r * geo.cap + j0 * u32(kTile);
-  const u32 nrec = fill - j0 * u32(kTile) < u32(kTile) ? fill - j0 * u32(kTile) : u32(kTile);
+  const u32 nrec = j0 + 1 == np ? fill - j0 * u32(kTile) : u32(kTile);
   // The payload columns are loaded now, with mr, and held in registers.
-  u64 vi[kPer], vt[kPer], vm[kPer];  // loaded together: one round trip
+  u64 vi[kPerW], vt[kPerW], vm[kPerW];  // loaded together: one round trip
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
+  for (int j = 0; j < kPerW; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
     vi[j] = k < nrec ? in.index[lo + k] : 0ull;
     vt[j] = k < nrec ? u64(in.term32[lo + k]) : 0ull;
@@ -344,7 +363,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
+  for (int j = 0; j < kPerW; ++j) {
     const u32 k = threadIdx.x + j * kPartThreads;
     if (k >= nrec) continue;
     const u16 b = u16((u32(vm[j]) >> 10) & 127u);
@@ -362,7 +381,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
   __syncthreads();
   for (int col = 0; col < 2; ++col) {
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
+    for (int j = 0; j < kPerW; ++j) {
       const u32 k = threadIdx.x + j * kPartThreads;
       if (k < nrec) L.stage[k] = col == 0 ? vi[j] : vt[j];
     }
@@ -386,6 +405,10 @@ constexpr int kSplitPer = kTile / kSplitThreads;
 __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
     Geometry geo, const u32* __restrict__ counts, Cols in, Cols out, u32* __restrict__ cs) {
   // part p = region r's j-th kTile records (the region grid, qb_bucket.h)
+  // region-major order (the parts of a region on neighbouring workgroups):
+  // with the tracker's ppx (5 at the bench) the first parts still spread over
+  // the XCDs, and the part-major order of k_bk_split_wide measured +1 % here
+  // (profiles/r04/leader/resv/)
   const u32 p = blockIdx.x;
   const u32 r = p / geo.ppx, j = p - r * geo.ppx;
   u32 fill = counts[r];
