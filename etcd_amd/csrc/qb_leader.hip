@@ -337,13 +337,15 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   __shared__ u32 wsum[kBlock / 64];
   const u32 c = blockIdx.x, t = threadIdx.x;
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
+  // overflow records of this chunk (K3 flagged it): the area is scanned
+  // (both words loaded up front, unconditionally)
+  const u32 cflag = chunk_flags[c], otot = *ovf.total;
   cur[t] = 0;
   if (t < 64)  // wave 0
     rt.template finish<MANY>(
         bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack), cs, counts,
         sb, geo.ppx, geo.cap, cl);
-  // overflow records of this chunk (K3 flagged it): the area is scanned
-  const u32 novf = chunk_flags[c] ? *ovf.total : 0u;  // workgroup-uniform
+  const u32 novf = cflag ? otot : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published
   const u32 total1 = rt.pre[rt.nr];  // the region records (workgroup-uniform)
   // Common case (round 3, one pass): no overflow and at most kStageRecs
