@@ -71,7 +71,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   __shared__ u64 acc[CAP];
   __shared__ u64 accn[NEXT ? CAP : 1];
   __shared__ u32 offs[CH + 1];
-  __shared__ u64 gterm[CH];
+  // group terms saturated to u32 (2 KB less LDS: four 512-thread workgroups
+  // per CU fit in 40 KB); a term >= 2^32 - 1 is read again from group_term
+  __shared__ u32 gterm[CH];
   __shared__ u32 act[CH];
   __shared__ u32 slow;
   __shared__ u32 tl[4];
@@ -149,7 +151,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
 #pragma unroll
   for (u32 q = 0; q < GPT; ++q) {
-    gterm[threadIdx.x + q * B] = gtr[q];
+    gterm[threadIdx.x + q * B] = gtr[q] < 0xFFFFFFFFull ? u32(gtr[q]) : 0xFFFFFFFFu;
   }
   for (u32 k = threadIdx.x; k < CH; k += B) act[k] = 0;
   __syncthreads();
@@ -197,7 +199,8 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
             idx = rec_index[ridx];
             t = rec_term[ridx];
           }
-          const u64 gt = gterm[lg];
+          u64 gt = gterm[lg];
+          if (gt == 0xFFFFFFFFull) gt = group_term[g0 + lg];  // (terms past 32 bits)
           if (t > gt) {
             slow = 1;  // higher term: step-down order (raft.go:875-879)
           } else if (t < gt) {
@@ -293,7 +296,8 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 }
 
 template <int WMAX, int CAPW, bool NEXT, bool MANY>
-__global__ __launch_bounds__(csr_block()) void k_csr_apply(QB_CSR_APPLY_PARAMS) {
+__global__ __launch_bounds__(csr_block()) __attribute__((amdgpu_num_sgpr(80))) void k_csr_apply(
+    QB_CSR_APPLY_PARAMS) {
   csr_apply_chunk<WMAX, CAPW, NEXT, false, MANY>(blockIdx.x, QB_CSR_APPLY_ARGS);
 }
 
