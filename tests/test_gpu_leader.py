@@ -274,6 +274,43 @@ def test_skewed_batch_overflows_reserved_regions(outbox):
     torch.cuda.synchronize()
 
 
+def test_dense_batch_many_run_table_rows_vs_c_oracle():
+    """Eight streaming batches concatenated into one call (8 records per
+    group over 1M groups): the regions hold ~32K records, so a chunk's run
+    table has more than 64 rows (k_ld_chunk_runs<true>) — every state array
+    and message against the C oracle on the same batch."""
+    import torch
+    from etcd_amd.quorum.leader import LeaderInbox, streaming_inbox, synth_streaming
+    from tests import oracle_c as oc
+    G = 1 << 20
+    lg, base = synth_streaming(G, device="cuda")
+    host = {k: v.copy() for k, v in lg.numpy().items()}
+    parts = [streaming_inbox(G, base, k, device="cuda") for k in range(8)]
+    col = {n: torch.cat([getattr(p_, n) for p_ in parts]).cpu().numpy()
+           for n in ("group", "flags", "index", "term", "hint", "log_term")}
+    flags = col["flags"]
+    ib = LeaderInbox.from_numpy(col["group"].view(np.uint32), flags & 0x0F, (flags >> 4) & 3,
+                                col["index"].view(np.uint64), col["term"].view(np.uint64),
+                                reject=(flags & 0x80) != 0, hint=col["hint"].view(np.uint64),
+                                log_term=col["log_term"].view(np.uint64))
+    M = 8 * G
+    res = lg.step(ib, msg_cap=6 * M)
+    rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
+           "index": ib.index.cpu().numpy().view(np.uint64),
+           "term": ib.term.cpu().numpy().view(np.uint64),
+           "hint": ib.hint.cpu().numpy().view(np.uint64),
+           "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
+    msgs, total, sd, gf, stats = oc.leader_step(host, 32, 0, 0, rec, threads=16, msg_cap=6 * M)
+    dev = lg.numpy()
+    for name in host:
+        assert np.array_equal(dev[name], host[name]), name
+    assert res.msg_total == total
+    assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))
+    assert np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)
+    assert res.stats["applied"] == int(stats[0]) == M
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("outbox", [False, True])
 def test_readindex_workload_vs_c_oracle(outbox):
     """The ReadIndex bench workload (§8f row 2) at 256K groups: queues,
