@@ -226,15 +226,16 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
 // Workspace carve (all offsets 256-byte aligned).  [shards, zero_end) is
 // zeroed by one memset per call (bucket_records).
 struct Carve {
-  size_t shards, flags, counts, chunk_flags, ovf_cnt, zero_end, chunk_start, buf1, buf2, cl, ovf,
-      total;
+  size_t shards, flags, counts, chunk_flags, ovf_cnt, user, zero_end, chunk_start, buf1, buf2, cl,
+      ovf, total;
   u64 nrec;  // records per column of buf1 / buf2 (the region grid)
 };
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 // ncols = 3: the wide form (index, term32, mr; the leader step) with its
 // overflow area; ncols = 1: the compact form, whose u8 chunk-low column rides
-// in the carve's cl area (the tracker steps).
-inline Carve carve(const Geometry& g, int ncols = 3) {
+// in the carve's cl area (the tracker steps).  user: bytes of the caller's
+// own (at `user`) zeroed with the rest by bucket_records' memset.
+inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   Carve c{};
   size_t o = 0;
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
@@ -242,6 +243,7 @@ inline Carve carve(const Geometry& g, int ncols = 3) {
   c.counts = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards);  // region fills
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
   c.ovf_cnt = o;  o += ncols == 3 ? up256(sizeof(u32) * (u64(g.NC) + 1)) : 0;
+  c.user = o;  o += up256(user);
   c.zero_end = o;
   // one row per part of the region grid (NSB x 8 x ppx)
   const u64 nrows = u64(g.NSB) * kRegionShards * g.ppx;

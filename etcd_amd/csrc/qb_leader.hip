@@ -90,9 +90,14 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
   const u32 wp = bk::region_parts(c.geo.cap, bk::kWideSlack);
   c.geo.ppx = wp ? wp : 1u;
   c.bucketed = c.geo.NSB <= 4096;
+  const size_t pool_b = up256(sizeof(u32) * 2), shard_b = up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
   if (c.bucketed) {
-    c.bcv = bk::carve(c.geo, 3);
+    // the message-chunk pool and the stat shards ride in the bucket carve's
+    // user area: bucket_records' memset zeroes them (no memset of their own)
+    c.bcv = bk::carve(c.geo, 3, pool_b + shard_b);
     c.bkt = o;   o += up256(c.bcv.total);
+    c.pool = c.bkt + c.bcv.user;
+    c.shards = c.pool + pool_b;
     c.ctot = o;  o += up256(sizeof(u32) * (u64(c.geo.NC) + 1));
     c.cbsum = o; o += up256(sizeof(u32) * (scan::blocks(c.geo.NC) + 1));
   }
@@ -114,8 +119,10 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
     c.cnext = o;  o += up256(sizeof(u32) * c.nchunks);
     c.chunks = o; o += up256(sizeof(Msg) * kChunk * c.nchunks);
   }
-  c.pool = o;   o += up256(sizeof(u32) * 2);
-  c.shards = o; o += up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
+  if (!c.bucketed) {
+    c.pool = o;   o += pool_b;
+    c.shards = o; o += shard_b;
+  }
   c.total = o;
   return c;
 }
@@ -1282,13 +1289,16 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
                        reinterpret_cast<u64*>(ws + c.rlt)};
   u32* pool = reinterpret_cast<u32*>(ws + c.pool);
   u64* shards = reinterpret_cast<u64*>(ws + c.shards);
-  // pool and stat shards are adjacent in the carve: one memset zeroes both
-  hipError_t e = hipMemsetAsync(pool, 0, c.shards - c.pool + sizeof(u64) * QB_LSTAT_COUNT * 64, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
   u64* bshards = nullptr;
   // QB_LEADER_OPT_ATOMIC_GROUPING selects the per-record-atomic grouping
   // even when the bucket geometry fits (both paths are tested).
   const bool force_atomic = (lg->options & QB_LEADER_OPT_ATOMIC_GROUPING) != 0;
+  hipError_t e = hipSuccess;
+  if (!c.bucketed || force_atomic) {  // (else bucket_records' memset zeroes them)
+    // pool and stat shards are adjacent in the carve: one memset zeroes both
+    e = hipMemsetAsync(pool, 0, c.shards - c.pool + sizeof(u64) * QB_LSTAT_COUNT * 64, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(leader workspace)");
+  }
   if (c.bucketed && !force_atomic) {
     char* bws = ws + c.bkt;
     bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);
