@@ -20,7 +20,10 @@
 //                    (wide columns) into chunks of 256 groups through LDS
 //                    counting sorts into reserved regions (bad groups
 //                    counted; a skewed batch's excess to the overflow area)
-//   L2 k_ld_chunk_total + scan  records per chunk -> each chunk's base
+//   L2 k_ld_chunk_total  records per chunk, scanned within each block of
+//                    256 chunks (+ the block's total); a chunk's base is that
+//                    prefix plus the totals of the blocks before it (L3 adds
+//                    them: no scan kernels)
 //   L3 k_ld_chunk_runs  per chunk: LDS count per group, block scan (writes
 //                    the per-group run starts), LDS-atomic scatter of the
 //                    batch indexes into the groups' runs
@@ -99,7 +102,7 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
     c.pool = c.bkt + c.bcv.user;
     c.shards = c.pool + pool_b;
     c.ctot = o;  o += up256(sizeof(u32) * (u64(c.geo.NC) + 1));
-    c.cbsum = o; o += up256(sizeof(u32) * (scan::blocks(c.geo.NC) + 1));
+    c.cbsum = o; o += up256(sizeof(u32) * ((u64(c.geo.NC) + kBlock - 1) / kBlock + 1));
   }
   c.cnt = o;    o += up256(sizeof(u32) * (G + 1));
   c.bsum = o;   o += up256(sizeof(u32) * (scan::blocks(G) + 1));
@@ -292,22 +295,43 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
                                                            const u32* __restrict__ counts,
                                                            const u32* __restrict__ cs,
                                                            const u32* __restrict__ ovf_cnt,
-                                                           u32* __restrict__ ctot) {
+                                                           u32* __restrict__ cloc,
+                                                           u32* __restrict__ bsum) {
+  __shared__ u32 wsum[kBlock / 64];
   const u32 c = blockIdx.x * kBlock + threadIdx.x;
-  if (c >= geo.NC) return;
-  const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
-  const u32 nrow = bk::kRegionShards * geo.ppx;
-  u32 s = ovf_cnt[c];
-  for (u32 x = 0; x < bk::kRegionShards; ++x) {
-    u32 fill = counts[sb * bk::kRegionShards + x];
-    fill = fill < geo.cap ? fill : geo.cap;
-    const u32 np = bk::region_parts(fill, bk::kWideSlack);
-    for (u32 j = 0; j < geo.ppx && j < np; ++j) {
-      const u64 row = (u64(sb) * nrow + x * geo.ppx + j) * (bk::kChunksPerSb + 1) + cl;
-      s += cs[row + 1] - cs[row];
+  u32 s = 0;
+  if (c < geo.NC) {
+    const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
+    const u32 nrow = bk::kRegionShards * geo.ppx;
+    s = ovf_cnt[c];
+    for (u32 x = 0; x < bk::kRegionShards; ++x) {
+      u32 fill = counts[sb * bk::kRegionShards + x];
+      fill = fill < geo.cap ? fill : geo.cap;
+      const u32 np = bk::region_parts(fill, bk::kWideSlack);
+      for (u32 j = 0; j < geo.ppx && j < np; ++j) {
+        const u64 row = (u64(sb) * nrow + x * geo.ppx + j) * (bk::kChunksPerSb + 1) + cl;
+        s += cs[row + 1] - cs[row];
+      }
     }
   }
-  ctot[c] = s;
+  // exclusive prefix within the block, and the block's total
+  const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  u32 inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = u32(__shfl_up(int(inc), o, 64));
+    if (lane >= u32(o)) inc += y;
+  }
+  if (lane == 63u) wsum[w] = inc;
+  __syncthreads();
+  u32 before = 0, total = 0;
+#pragma unroll
+  for (u32 q = 0; q < kBlock / 64; ++q) {
+    total += wsum[q];
+    if (q < w) before += wsum[q];
+  }
+  if (c < geo.NC) cloc[c] = before + inc - s;
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
 constexpr u32 kStageRecs = 1024;  // chunk records placed through LDS
@@ -335,7 +359,8 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
                                                           const u32* __restrict__ cs,
                                                           const u8* __restrict__ chunk_flags,
                                                           bk::Ovf ovf,
-                                                          const u32* __restrict__ cbase,
+                                                          const u32* __restrict__ cloc,
+                                                          const u32* __restrict__ bsum,
                                                           u32* __restrict__ cnt,
                                                           u32* __restrict__ perm,
                                                           qb_leader_inbox in, RecCols rc) {
@@ -346,12 +371,20 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
   // overflow records of this chunk (K3 flagged it): the area is scanned
   // (both words loaded up front, unconditionally)
-  const u32 cflag = chunk_flags[c], otot = *ovf.total;
+  const u32 cflag = chunk_flags[c], otot = *ovf.total, ocnt = ovf.cnt[c];
+  const u32 clo = cloc[c];  // the chunk's prefix within its block of kBlock chunks
+  __shared__ u32 s_bpre;
   cur[t] = 0;
-  if (t < 64)  // wave 0
-    rt.template finish<MANY>(
-        bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack), cs, counts,
-        sb, geo.ppx, geo.cap, cl);
+  if (t < 64) {  // wave 0: the run table, and the totals of the blocks before this chunk's
+    const bk::RunRegs rq = bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack);
+    const u32 nb = c / kBlock;
+    u32 bp = 0;
+    for (u32 i = t; i < nb; i += 64) bp += bsum[i];
+    rt.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bp += u32(__shfl_xor(int(bp), o, 64));
+    if (t == 0) s_bpre = bp;
+  }
   const u32 novf = cflag ? otot : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published
   const u32 total1 = rt.pre[rt.nr];  // the region records (workgroup-uniform)
@@ -397,12 +430,13 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   if ((t & 63u) == 63u) wsum[t >> 6] = inc;
   __syncthreads();
   for (u32 w = 0; w < (t >> 6); ++w) inc += wsum[w];
-  const u32 base = cbase[c], start = inc - x;
+  const u32 base = s_bpre + clo, start = inc - x;
+  // the chunk's records: its region runs plus its overflow records
+  const u32 ntot = total1 + (cflag ? ocnt : 0u);  // workgroup-uniform
   const u64 g = u64(c) * kCh + t;
   if (g < geo.G) cnt[g] = base + start;
-  if (c + 1 == geo.NC && t == 0) cnt[geo.G] = cbase[geo.NC];
+  if (c + 1 == geo.NC && t == 0) cnt[geo.G] = base + ntot;
   cur[t] = start;
-  const u32 ntot = cbase[c + 1] - base;  // workgroup-uniform
   __syncthreads();  // every group's cur[] start is written
   // the chunk's records one at a time (region runs, then overflow): the full
   // term (a kTermEscape term32 is read from the batch by ridx)
@@ -1302,7 +1336,8 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
   if (c.bucketed && !force_atomic) {
     char* bws = ws + c.bkt;
     bshards = reinterpret_cast<u64*>(bws + c.bcv.shards);
-    u32* ctot = reinterpret_cast<u32*>(ws + c.ctot);
+    u32* cloc = reinterpret_cast<u32*>(ws + c.ctot);
+    u32* cbs = reinterpret_cast<u32*>(ws + c.cbsum);
     const u32* counts = reinterpret_cast<const u32*>(bws + c.bcv.counts);
     const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
     const bk::Ovf ovf = bk::ovf_at(bws, c.bcv, c.geo);
@@ -1312,19 +1347,17 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
                                       /*compact=*/false);
     if (rc != QB_OK) return rc;
     hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, st, c.geo, counts, cs, ovf.cnt, ctot);
+                       dim3(kBlock), 0, st, c.geo, counts, cs, ovf.cnt, cloc, cbs);
     QB_CHECK_LAUNCH("k_ld_chunk_total");
-    scan::launch(ctot, c.geo.NC, reinterpret_cast<u32*>(ws + c.cbsum), st);
-    QB_CHECK_LAUNCH("scan(chunks)");
     bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, c.bcv.nrec, 3);
     b2.term32 = reinterpret_cast<u32*>(b2.term);
     const u8* cfl = reinterpret_cast<const u8*>(bws + c.bcv.chunk_flags);
     if (bk::RunTable::many_rows(c.geo.ppx))
       hipLaunchKernelGGL(ld::k_ld_chunk_runs<true>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
-                         counts, cs, cfl, ovf, ctot, cnt, perm, *in, rcols);
+                         counts, cs, cfl, ovf, cloc, cbs, cnt, perm, *in, rcols);
     else
       hipLaunchKernelGGL(ld::k_ld_chunk_runs<false>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
-                         counts, cs, cfl, ovf, ctot, cnt, perm, *in, rcols);
+                         counts, cs, cfl, ovf, cloc, cbs, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");
   } else {
     u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);
