@@ -74,7 +74,7 @@ constexpr u32 kCh = bk::chunk_groups(16);  // groups per bucket chunk (256)
 static_assert(kCh == kBlock, "one thread per group of a chunk");
 
 struct Carve {
-  size_t cnt, bsum, cursor, perm, rflags, rterm, rindex, rhint, rlt, mcnt, mbsum, fix, chead,
+  size_t cnt, bsum, cursor, perm, rflags, rterm, rindex, rhint, rlt, mcnt, mbs, mbsum, fix, chead,
       cnext, chunks, pool, shards;
   size_t bkt, ctot, cbsum, total;
   u64 nchunks;
@@ -115,7 +115,10 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
   c.rlt = o;    o += up256(sizeof(u64) * (M + 1));
   if (!outbox) {
     c.mcnt = o;   o += up256(sizeof(u32) * (G + 1));
-    c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks(G) + 1));
+    // per-workgroup message totals of k_ld_step (scanned), and their scan's
+    // block sums
+    c.mbs = o;    o += up256(sizeof(u32) * ((G + kBlock - 1) / kBlock + 1));
+    c.mbsum = o;  o += up256(sizeof(u32) * (scan::blocks((G + kBlock - 1) / kBlock) + 1));
     c.fix = o;    o += up256(sizeof(Msg) * kFix * G);
     c.chead = o;  o += up256(sizeof(u32) * (G + 1));
     c.nchunks = M / 8 + 1024;  // 4 spilled messages per record on average
@@ -146,7 +149,8 @@ struct Args {
   const u32* cnt;     // exclusive scan of per-group record counts, [G+1]
   u32* perm;          // batch indexes grouped by group (each run ascending)
   RecCols rec;        // the records in perm order
-  u32* mcnt;          // messages per group
+  u32* mcnt;          // messages per group (outbox); in-workgroup prefix (ordered)
+  u32* mbs;           // ordered form: each workgroup's message total (else null)
   Msg* fix;           // [kFix][G]: message k of every group contiguous
   u32* chead;         // first overflow chunk per group
   u32* cnext;         // chunk links
@@ -1118,6 +1122,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
       if (A.stepdown_at) A.stepdown_at[g] = kNone;
       if (A.gflags) A.gflags[g] = 0;
     }
+    if (A.mbs && threadIdx.x == 0) A.mbs[blockIdx.x] = 0;
     return;
   }
   // issued before the slot stage's loads so both round trips overlap
@@ -1149,7 +1154,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
       if (staged) step_group<true>(A, g, r0, r1, s0, s1, sb, pre, stepdown, gfl, n);
       else step_group<false>(A, g, r0, r1, s0, s1, sb, pre, stepdown, gfl, n);
     }
-    A.mcnt[g] = n.stored;
+    if (!A.mbs) A.mcnt[g] = n.stored;  // (ordered: the prefix below)
     if (A.stepdown_at) A.stepdown_at[g] = stepdown;
     if (A.gflags) A.gflags[g] = gfl;
   }
@@ -1167,8 +1172,31 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
   tally.t[4] += wsum(n.after);
   tally.t[5] += wsum(n.msgs);
   tally.t[6] += wsum(n.msgs - n.stored);
+  // ordered form: the messages' place within the workgroup (a scan of the
+  // stored counts over its 256 groups) and the workgroup's total, so no scan
+  // kernel runs over the G counts (k_ld_emit adds the workgroups' prefix)
+  __shared__ u32 mwave[kBlock / 64];
+  u32 minc = n.stored;
+  if (A.mbs) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = u32(__shfl_up(int(minc), o, 64));
+      if ((threadIdx.x & 63u) >= u32(o)) minc += y;
+    }
+    if ((threadIdx.x & 63u) == 63u) mwave[threadIdx.x >> 6] = minc;
+  }
   tally.stage(lds);
   __syncthreads();
+  if (A.mbs) {
+    u32 before = 0, total = 0;
+#pragma unroll
+    for (u32 q = 0; q < kBlock / 64; ++q) {
+      total += mwave[q];
+      if (q < (threadIdx.x >> 6)) before += mwave[q];
+    }
+    if (live) A.mcnt[g] = before + minc - n.stored;
+    if (threadIdx.x == 0) A.mbs[blockIdx.x] = total;
+  }
   {
     const int slot[7] = {QB_LSTAT_APPLIED, QB_LSTAT_STALE_TERM, QB_LSTAT_HIGHER_TERM,
                          QB_LSTAT_NON_MEMBER, QB_LSTAT_AFTER_STEPDOWN, QB_LSTAT_MSGS,
@@ -1192,6 +1220,8 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
 // the counts), the workgroup's output range written with coalesced word
 // stores.  Messages past msg_cap are counted as dropped.
 __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict__ moff,
+                                                    const u32* __restrict__ mbs,
+                                                    const u32* __restrict__ mbsum, u32 nblk,
                                                     const Msg* __restrict__ fix,
                                                     const u32* __restrict__ chead,
                                                     const u32* __restrict__ cnext,
@@ -1203,7 +1233,13 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
   __shared__ u32 lo[kBlock + 1];
   const u64 g0 = u64(blockIdx.x) * kBlock;
   const u32 ng = u32(G - g0 < kBlock ? G - g0 : kBlock);
-  for (u32 t = threadIdx.x; t <= ng; t += kBlock) lo[t] = moff[g0 + t];
+  // group g's first message: its prefix within the step's workgroup (moff)
+  // plus the workgroup's place (mbs scanned; two levels, off_at style)
+  auto boff = [&](u32 i) -> u32 {
+    return i < nblk ? mbs[i] + mbsum[i / scan::kScanPer] : mbs[nblk];
+  };
+  const u32 base = boff(blockIdx.x), next = boff(blockIdx.x + 1);
+  for (u32 t = threadIdx.x; t <= ng; t += kBlock) lo[t] = t < ng ? moff[g0 + t] + base : next;
   __syncthreads();
   if (threadIdx.x < ng && msg_off) msg_off[g0 + threadIdx.x] = lo[threadIdx.x];
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
@@ -1389,6 +1425,7 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
   A.perm = perm;
   A.rec = rcols;
   A.mcnt = sink->count;
+  A.mbs = msg_total ? reinterpret_cast<u32*>(ws + c.mbs) : nullptr;
   A.fix = sink->fix;
   A.chead = sink->chead;
   A.cnext = sink->cnext;
@@ -1400,13 +1437,18 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
   A.gflags = gflags;
   hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
   QB_CHECK_LAUNCH("k_ld_step");
-  if (msg_total) {  // the group-ordered array: scan of the counts, then the copy
+  if (msg_total) {  // the group-ordered array: the workgroups' totals scanned, then the copy
+    const u32 nblk = u32((G + kBlock - 1) / kBlock);
     u32* mbsum = reinterpret_cast<u32*>(ws + c.mbsum);
-    scan::launch(sink->count, G, mbsum, st);
-    QB_CHECK_LAUNCH("scan(messages)");
-    hipLaunchKernelGGL(ld::k_ld_emit, dim3(grid_for(G)), dim3(kBlock), 0, st, G, sink->count, A.fix,
-                       A.chead, A.cnext, A.chunks, reinterpret_cast<ld::Msg*>(msgs),
-                       msg_cap, msg_off, ld::U(msg_total), shards);
+    // a local scan of the totals + the block sums' scan (the add-back is in
+    // k_ld_emit); mbs[nblk] = all messages
+    const u32 nsb = scan::blocks(nblk);
+    hipLaunchKernelGGL(scan::k_scan_local, dim3(nsb), dim3(1024), 0, st, A.mbs, u64(nblk), mbsum);
+    hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, mbsum, nsb, A.mbs + nblk);
+    QB_CHECK_LAUNCH("scan(message totals)");
+    hipLaunchKernelGGL(ld::k_ld_emit, dim3(grid_for(G)), dim3(kBlock), 0, st, G, sink->count, A.mbs,
+                       mbsum, nblk, A.fix, A.chead, A.cnext, A.chunks,
+                       reinterpret_cast<ld::Msg*>(msgs), msg_cap, msg_off, ld::U(msg_total), shards);
     QB_CHECK_LAUNCH("k_ld_emit");
   }
   hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64 * QB_LSTAT_COUNT), 0, st, shards, bshards,
