@@ -70,7 +70,8 @@ struct Args {
   const u64* infl_buf;
   u32 K;
   // new
-  u32* new_cnt;  // [G+1] counts, then (after the scan) offsets
+  u32* new_cnt;  // [G+1] counts, then 4096-block local prefixes; the write pass stores the offsets
+  const u32* nbsum;  // the local scan's block sums, scanned (add-back folded into the write pass)
   u64 S_cap;
   u64* n_ids;
   u32* n_cfg;
@@ -323,7 +324,13 @@ __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
   int n_old;
   int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
   const u32 s0 = A.off[g];
-  const u64 d0 = A.new_cnt[g], d1 = A.new_cnt[g + 1];
+  // the group's offset: its local prefix plus its scan block's sum (round 4:
+  // the scan's add-back pass folded here, which also stores the offset);
+  // its end from its own count (the next group's entry may already hold its
+  // final offset)
+  const u64 d0 = u64(A.new_cnt[g]) + A.nbsum[g / scan::kScanPer];
+  const u64 d1 = d0 + (rc ? u32(n_old) : u32(__popc(r.prs)));
+  A.new_cnt[g] = u32(d0);
   if (d1 > A.S_cap) return;  // the caller's capacity is exceeded (reported by new_off[G])
   if (rc) {  // the old config is kept
     r = Roles{};
@@ -534,7 +541,13 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
   hipLaunchKernelGGL((cc::k_cc_count<cc::kSmall, false>), dim3(grid), dim3(cc::kBlk), 0, st, A);
   hipLaunchKernelGGL((cc::k_cc_count<cc::kTab, true>), dim3(big_grid), dim3(cc::kBlk), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_count");
-  scan::launch(out->new_off, G, static_cast<u32*>(workspace), st);
+  {  // local scan + block sums (the add-back is in k_cc_write); new_off[G] = total
+    u32* bsum = static_cast<u32*>(workspace);
+    const u32 nb = scan::blocks(G);
+    hipLaunchKernelGGL(scan::k_scan_local, dim3(nb), dim3(1024), 0, st, out->new_off, G, bsum);
+    hipLaunchKernelGGL(scan::k_scan_sums, dim3(1), dim3(1024), 0, st, bsum, nb, out->new_off + G);
+    A.nbsum = bsum;
+  }
   QB_CHECK_LAUNCH("scan(conf change)");
   hipLaunchKernelGGL((cc::k_cc_write<cc::kSmall, false>), dim3(grid), dim3(cc::kBlk), 0, st, A);
   hipLaunchKernelGGL((cc::k_cc_write<cc::kTab, true>), dim3(big_grid), dim3(cc::kBlk), 0, st, A);
