@@ -92,14 +92,37 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+def _stage_report(stage_dir: str, n: int) -> str:
+    """Each rank's last stage (tools/rankguard.py writes rank<r>.stage)."""
+    rows = []
+    for r in range(n):
+        try:
+            with open(os.path.join(stage_dir, f"rank{r}.stage")) as f:
+                rows.append(f"  rank {r}: " + f.read().strip().replace("\n", " | "))
+        except OSError:
+            rows.append(f"  rank {r}: (no stage recorded)")
+    return "\n".join(rows)
+
+
+def spawn_ranks(n: int, argv, deadline_s: float = 0.0, grace_s: float = 30.0) -> int:
     """Start n child ranks of this same command (before any GPU call in this
-    process: no exec, children are separate processes) and wait; returns the
-    first non-zero exit code (the others are then terminated) or 0."""
+    process: no exec, children are separate processes) and wait.  Returns 0,
+    or the first non-zero exit code: the other ranks then get ``grace_s`` to
+    finish on their own (every rank decides a workload's failure together
+    and exits after rank 0 has printed its line) before they are terminated.
+    With ``deadline_s`` > 0 every child still running at deadline_s + 60 s
+    is terminated and 124 returned (each rank's own watchdog exits at
+    deadline_s; this is the backstop).  On any failure each rank's last
+    stage is printed to stderr."""
+    import tempfile
     port = _free_port()
+    stage_dir = tempfile.mkdtemp(prefix="bench_stages_")
+    base = dict(os.environ, BENCH_STAGE_DIR=stage_dir)
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e)
-             for e in launch_envs(n, os.environ, port)]
+             for e in launch_envs(n, base, port)]
     rc = 0
+    t_end = time.monotonic() + deadline_s + 60.0 if deadline_s > 0 else None
+    t_grace = None
     try:
         pending = list(procs)
         while pending:
@@ -110,13 +133,30 @@ def spawn_ranks(n: int, argv) -> int:
                 pending.remove(p)
                 if r != 0 and rc == 0:
                     rc = r
-                    for q in pending:
-                        q.terminate()
+                    t_grace = time.monotonic() + grace_s
+            now = time.monotonic()
+            if pending and ((t_grace is not None and now > t_grace)
+                            or (t_end is not None and now > t_end)):
+                if rc == 0:
+                    rc = 124
+                    print(f"bench.py: deadline ({deadline_s:.0f} s) passed; terminating "
+                          f"{len(pending)} rank(s)", file=sys.stderr, flush=True)
+                for q in pending:
+                    q.terminate()
+                for q in pending:
+                    try:
+                        q.wait(10)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                pending = []
             time.sleep(0.05)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        if rc != 0:
+            print("bench.py: ranks' last stages:\n" + _stage_report(stage_dir, n),
+                  file=sys.stderr, flush=True)
     return rc
 
 
@@ -167,7 +207,7 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
-def timed_region(run, streams, K, barrier):
+def timed_region(run, streams, K, barrier, name="region"):
     """K steps between barrier + synchronize.  Device time = from the earliest
     start event to the latest end event, one event pair per launch stream
     (no cross-stream hop inside the region: a fork + join around a 20-step
@@ -176,9 +216,12 @@ def timed_region(run, streams, K, barrier):
     clock stops when the host sees every stream's end event complete, then
     the device-wide synchronize runs (a torch.cuda.synchronize() costs ~20 us
     more than the event waits, 10 % of a 20-step region).
-    Returns (wall seconds, device seconds per step)."""
+    A generator (``yield from``): agreement points (tools/rankguard.py)
+    before each barrier, so a rank whose steps fail leaves together with the
+    others.  Returns (wall seconds, device seconds per step)."""
     TS = len(streams)
     ev = HipEvents(2 * TS)
+    yield name
     barrier()
     for s_, st in enumerate(streams):
         ev.record(ev.ev[s_], st.cuda_stream)
@@ -190,6 +233,7 @@ def timed_region(run, streams, K, barrier):
         ev.synchronize(TS + s_)
     t1 = time.perf_counter()
     torch.cuda.synchronize()
+    yield name + ":end"
     barrier()
     starts = [0.0] + [ev.elapsed_ms(0, s_) for s_ in range(1, TS)]
     ends = [ev.elapsed_ms(0, TS + s_) for s_ in range(TS)]
@@ -347,11 +391,68 @@ TRACKER_BYTES = 101
 TRACKER_STATE = ("match", "committed", "active", "stepdown_at")
 
 
-def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7):
+# Skewed streams (--skew; VERDICT r4 "Next" 2): a massive multi-raft host's
+# ticks have hot groups.  The same stream (one record per group per tick on
+# average, E new entries per tick) with the records' groups drawn as
+#   zipf         exact discrete Zipf(s = 1.1) over group ranks 1..G, ranks
+#                mapped to groups by a fixed random permutation (the hottest
+#                group gets ~11 % of the batch: ~1.9M records per 16M-record
+#                tick, far above what raft lets one group receive);
+#   zipf-capped  the same, with at most ZIPF_CAP records per group per tick:
+#                a follower acks at most the MsgApps its leader has in flight,
+#                MaxInflightMsgs = 4096 / 8 = 512 per follower in etcd
+#                (server/etcdserver/raft.go:39, raft/raft.go:162), so 4 x 512
+#                for a 5-voter group; the excess records are redrawn uniformly;
+#   sb10 / sb30  10 % / 30 % of the records on the groups of ONE super-bucket
+#                (chunks 0, 8, ..., 1016 of CH = 512 groups: the interleaved
+#                super-bucket 0 of qb_bucket.h, 64K groups), the rest uniform.
+SKEWS = ("none", "zipf", "zipf-capped", "sb10", "sb30")
+ZIPF_S = 1.1
+ZIPF_CAP = 4 * 512
+
+
+def skewed_groups(G: int, M: int, skew: str, gen, dev, zipf=None) -> torch.Tensor:
+    """M record groups (int32) of the given skew (SKEWS); ``zipf`` = the
+    (cdf, permutation) pair shared by every batch of a stream."""
+    if skew == "none":
+        return torch.randint(0, G, (M,), generator=gen, device=dev, dtype=torch.int32)
+    if skew.startswith("zipf"):
+        cdf, perm = zipf
+        u = torch.rand(M, generator=gen, device=dev, dtype=torch.float64)
+        g = perm[torch.searchsorted(cdf, u).clamp_(max=G - 1)]
+        if skew == "zipf-capped":
+            # records past their group's ZIPF_CAP-th (in batch order) are redrawn
+            order = torch.sort(g, stable=True).indices
+            gs = g[order]
+            first = torch.searchsorted(gs, gs, side="left")
+            pos = torch.arange(M, device=dev) - first
+            over = order[pos >= ZIPF_CAP]
+            g[over] = torch.randint(0, G, (over.numel(),), generator=gen, device=dev)
+        return g.to(torch.int32)
+    frac = {"sb10": 0.1, "sb30": 0.3}[skew]
+    g = torch.randint(0, G, (M,), generator=gen, device=dev, dtype=torch.int64)
+    hot = torch.rand(M, generator=gen, device=dev) < frac
+    nh = int(hot.sum().item())
+    nchunks = min(128, ((G + 511) // 512 + 7) // 8)  # chunks 8j < NC of the first window
+    c = 8 * torch.randint(0, nchunks, (nh,), generator=gen, device=dev)
+    gg = c * 512 + torch.randint(0, 512, (nh,), generator=gen, device=dev)
+    g[hot] = torch.minimum(gg, torch.tensor(G - 1, device=dev))
+    return g.to(torch.int32)
+
+
+def zipf_table(G: int, gen, dev):
+    w = torch.arange(1, G + 1, dtype=torch.float64, device=dev).pow_(-ZIPF_S)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    return cdf, torch.randperm(G, generator=gen, device=dev)
+
+
+def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7, skew="none"):
     """nb distinct streaming batches (device tensors)."""
     out = []
+    zipf = zipf_table(G, gen, dev) if skew.startswith("zipf") else None
     for k in range(nb):
-        group = torch.randint(0, G, (G,), generator=gen, device=dev, dtype=torch.int32)
+        group = skewed_groups(G, G, skew, gen, dev, zipf)
         slot = n_slots_fn(group, gen)
         lag = torch.randint(0, 96, (G,), generator=gen, device=dev, dtype=torch.int64)
         index = last[group.long()] + (k + 1) * TRACKER_E - lag
@@ -361,12 +462,12 @@ def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7):
     return out
 
 
-def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool):
+def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool, skew: str = "none"):
     """The configs[4] stream as the bench runs it: the leader state (after
     the initial maybeCommit, the leader's own match raised to the last of the
-    nb * E entries it appended) and the nb device batches.  Returns
-    (tracker, batches, info).  tests/ replays exactly this stream on the
-    oracle."""
+    nb * E entries it appended) and the nb device batches (``skew``: the
+    records' group distribution, SKEWS).  Returns (tracker, batches, info).
+    tests/ replays exactly this stream on the oracle."""
     n = 5
     gen = torch.Generator(device=dev)
     gen.manual_seed(TRACKER_SEED + 7919 * rank)
@@ -401,7 +502,7 @@ def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool):
         slots_mean = voters_mean = float(n)
     tr.term.fill_(7)
     tr.commit_advance()
-    batches = tracker_batches(G, nb, last, slots, gen, dev)
+    batches = tracker_batches(G, nb, last, slots, gen, dev, skew=skew)
     if csr:
         tr.match[first] = last + nb * TRACKER_E   # the leader appended nb*E entries
     else:
@@ -410,40 +511,54 @@ def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool):
     return tr, batches, {"slots_mean": slots_mean, "voters_mean": voters_mean, "gen": gen}
 
 
-def tracker_host_state(tr, csr: bool, Gs: int):
-    """The first Gs groups of a tracker's state as the oracle's numpy dict
-    (off and cfg as well for the CSR layout)."""
-    Gs = min(Gs, tr.G)
+def tracker_host_state(tr, csr: bool, Gs: int, g0: int = 0):
+    """Groups [g0, g0 + Gs) of a tracker's state as the oracle's numpy dict,
+    rebased to local group 0 (off and cfg as well for the CSR layout)."""
+    g0 = min(g0, tr.G)
+    Gs = min(Gs, tr.G - g0)
+    sl = slice(g0, g0 + Gs)
     if csr:
-        off = tr.off[: Gs + 1].cpu().numpy().view(np.uint32).copy()
-        S = int(off[-1])
-        match = batch.as_u64(tr.match[:S]).copy() if S else np.zeros(0, np.uint64)
-        cfg = tr.cfg[:Gs].cpu().numpy().view(np.uint32).copy()
+        off = tr.off[g0: g0 + Gs + 1].cpu().numpy().view(np.uint32).copy()
+        a, e = int(off[0]), int(off[-1])
+        off -= np.uint32(a)
+        match = batch.as_u64(tr.match[a:e]).copy() if e > a else np.zeros(0, np.uint64)
+        cfg = tr.cfg[sl].cpu().numpy().view(np.uint32).copy()
     else:
         off = cfg = None
-        match = batch.as_u64(tr.match[:, :Gs]).copy()
-    st = {"match": match, "committed": batch.as_u64(tr.committed[:Gs]).copy(),
-          "active": tr.active[:Gs].cpu().numpy().view(np.uint16).copy(),
-          "term": batch.as_u64(tr.term[:Gs]).copy(),
-          "term_start": batch.as_u64(tr.term_start[:Gs]).copy(),
-          "stepped_down": (tr.stepdown_at[:Gs] != -1).cpu().numpy().astype(np.uint8)}
+        match = batch.as_u64(tr.match[:, sl]).copy()
+    st = {"match": match, "committed": batch.as_u64(tr.committed[sl]).copy(),
+          "active": tr.active[sl].cpu().numpy().view(np.uint16).copy(),
+          "term": batch.as_u64(tr.term[sl]).copy(),
+          "term_start": batch.as_u64(tr.term_start[sl]).copy(),
+          "stepped_down": (tr.stepdown_at[sl] != -1).cpu().numpy().astype(np.uint8)}
     return off, cfg, st
 
 
-def host_records(b, Gs: int):
-    """The batch's records for groups < Gs, in batch order, as numpy."""
-    keep = (b.group.long() & 0xFFFFFFFF) < Gs
-    return (b.group[keep].cpu().numpy().view(np.uint32).copy(),
+def host_records(b, Gs: int, g0: int = 0):
+    """The batch's records for groups [g0, g0 + Gs), in batch order, groups
+    rebased to g0, as numpy."""
+    g = b.group.long() & 0xFFFFFFFF
+    keep = (g >= g0) & (g < g0 + Gs)
+    return ((g[keep] - g0).to(torch.int32).cpu().numpy().view(np.uint32).copy(),
             b.flags[keep].cpu().numpy().copy(),
             batch.as_u64(b.index[keep]).copy(), batch.as_u64(b.term[keep]).copy())
 
 
-def tracker_state_mismatches(tr, csr, st, Gs):
-    """Fields where the device state of the first Gs groups differs from the
+def tracker_state_mismatches(tr, csr, st, Gs, g0: int = 0):
+    """Fields where the device state of groups [g0, g0 + Gs) differs from the
     oracle's ``st``."""
-    _, _, dev_st = tracker_host_state(tr, csr, Gs)
+    _, _, dev_st = tracker_host_state(tr, csr, Gs, g0)
     return [k for k in ("match", "committed", "active", "stepped_down")
             if not np.array_equal(dev_st[k], st[k])]
+
+
+def parity_windows(G: int, Gs: int):
+    """The tracker's parity windows: the whole shard when Gs >= G, else three
+    windows of Gs / 3 groups (start, middle, end of the shard)."""
+    if Gs >= G:
+        return [(0, G)]
+    w = max(1, Gs // 3)
+    return [(0, w), ((G - w) // 2, w), (G - w, w)]
 
 
 def tracker_cpu_baseline(seconds: float, csr: bool):
@@ -522,19 +637,22 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
             "value_1thread": r1}
 
 
-def tracker_parity(tr, csr, snap_host, batches, Gs, threads):
-    """The final device state of the first Gs groups against the oracle's
+def tracker_parity(tr, csr, snaps, batches, threads):
+    """The final device state of every parity window against the oracle's
     sequential replay of every batch the bench applied since the last
-    restore (the nb batches in order), restricted to those groups."""
+    restore (the nb batches in order), restricted to the window's groups.
+    ``snaps``: [(g0, Gs, host state)] taken before the first batch."""
     from tests import oracle_c as oc
-    off, cfg, st = snap_host
-    for b in batches:
-        rec = host_records(b, Gs)
-        if csr:
-            oc.csr_appresp_sequential(off, cfg, rec, st, threads=threads)
-        else:
-            oc.appresp_sequential(5, len(st["committed"]), rec, st, threads=threads)
-    return tracker_state_mismatches(tr, csr, st, Gs)
+    bad = []
+    for g0, Gs, (off, cfg, st) in snaps:
+        for b in batches:
+            rec = host_records(b, Gs, g0)
+            if csr:
+                oc.csr_appresp_sequential(off, cfg, rec, st, threads=threads)
+            else:
+                oc.appresp_sequential(5, len(st["committed"]), rec, st, threads=threads)
+        bad += [f"{k} in [{g0}, {g0 + Gs})" for k in tracker_state_mismatches(tr, csr, st, Gs, g0)]
+    return bad
 
 
 def _timed(fn, barrier, warm=2, reps=5):
@@ -558,40 +676,49 @@ def _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen, restore
     all-gather (qb_dev_allgather_results).  Node-wide checks: every record
     arrives at its owner (count, ownership and a checksum of the global group
     numbers over all ranks), and the delta-maintained vector equals a fresh
-    full gather of every shard's committed vector after a real tick."""
+    full gather of every shard's committed vector after a real tick.
+    A generator: an agreement point before every group of collectives."""
     total = world * G
-    ranks = _rccl_ranks(args, world)
-    coll = {}
     # routing: one batch of G records per rank with global group numbers
     b = batches[0]
     gl = torch.randint(0, total, (G,), generator=gen, device=dev, dtype=torch.int64)
     cols = {"group": gl.to(torch.int32), "flags": b.flags, "index": b.index, "term": b.term}
+    yield "comm"
     route, route_impl = _router(args, dev)
+    gather, gather_impl = _gather(args, dev)
+    delta, delta_impl = _delta(args, dev)
+    ranks = _rccl_ranks(args, world)
+    yield "route_records"
     route_ms, got = _timed(lambda: route(cols, total), barrier)
-    coll["route_records"] = {"ms": route_ms, "impl": route_impl, "ranks": world,
-                             "rccl_ranks": ranks, "records_per_rank": G}
+    coll = {"route_records": {"ms": route_ms, "impl": route_impl, "ranks": world,
+                              "rccl_ranks": ranks, "records_per_rank": G}}
     lg = got["group"].long() & 0xFFFFFFFF
     sums = torch.tensor([got["group"].numel(), int((lg + rank * G).sum().item()),
                          int(gl.sum().item()), G], dtype=torch.int64, device=dev)
-    dist.all_reduce(sums)
     owned = bool((lg < G).all().item())
+    yield "route_check"
+    dist.all_reduce(sums)
     route_ok = _all_ok(owned, world, dev) and int(sums[0].item()) == int(sums[3].item()) \
         and int(sums[1].item()) == int(sums[2].item())
     # the changed-commit delta after a real tick, against a full gather
-    gather, gather_impl = _gather(args, dev)
     vote0 = torch.zeros(G, dtype=torch.uint8, device=dev)
     adv = torch.zeros(G, dtype=torch.uint8, device=dev)
     restore()
     for k in range(W):
         tr.step(batches[k], reset_stats=False, rearm=False)
+    torch.cuda.synchronize(dev)
+    yield "allgather_results"
     commit_all, _ = gather(tr.committed, vote0, total)      # the vector before the tick
     commit_all = commit_all.to(dev).clone()
     tr.step(batches[W], advanced_out=adv, reset_stats=False, rearm=False)
-    delta, delta_impl = _delta(args, dev)
+    torch.cuda.synchronize(dev)
+    yield "allgather_changed"
     delta_changed = delta(adv, tr.committed, total, commit_all)   # applied once: checked below
     full_ms, (full_c, _) = _timed(lambda: gather(tr.committed, vote0, total), barrier)
-    delta_ok = _all_ok(torch.equal(commit_all, full_c.to(dev)), world, dev)
+    same = torch.equal(commit_all, full_c.to(dev))
     scratch = commit_all.clone()
+    yield "delta_check"
+    delta_ok = _all_ok(same, world, dev)
     delta_ms, _ = _timed(lambda: delta(adv, tr.committed, total, scratch), barrier)
     coll["allgather_changed"] = {"ms": delta_ms, "impl": delta_impl, "ranks": world,
                                  "rccl_ranks": ranks, "changed_groups": delta_changed}
@@ -605,24 +732,29 @@ def _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen, restore
 
 
 def tracker_main(args, world, rank, dev, barrier):
+    """configs[4] (a generator run by RankGuard.run: agreement points before
+    every collective)."""
     csr = args.workload == "tracker-csr"
     G = args.groups if args.groups != 1 << 20 else 1 << 24
     K = args.steps if args.steps != 1000 else 20
     W = args.warmup if args.warmup is not None else 4
     nb = W + K
+    skew = getattr(args, "skew", "none") or "none"
     if nb > TRACKER_MAX_BATCHES:
         raise SystemExit(f"--workload {args.workload} keeps one distinct batch per step resident: "
                          f"--steps + --warmup must be <= {TRACKER_MAX_BATCHES}")
-    tr, batches, info = tracker_setup(G, nb, rank, dev, csr)
+    tr, batches, info = tracker_setup(G, nb, rank, dev, csr, skew)
     gen = info["gen"]
     snap = {k: getattr(tr, k).clone() for k in TRACKER_STATE}
     # the whole shard at N = 1; with N ranks sharing the node's CPUs, each
-    # rank checks the first 2M groups of its shard (the GPU suite checks the
-    # full 16M-group stream tick by tick)
+    # rank checks three windows (start, middle, end of its shard) of 2M
+    # groups in all (the GPU suite checks the full 16M-group stream tick by
+    # tick)
     tpg = args.tracker_parity_groups if args.tracker_parity_groups > 0 else (
         G if world == 1 else 1 << 21)
-    Gs = min(G, tpg)
-    snap_host = tracker_host_state(tr, csr, Gs) if not args.no_parity else None
+    windows = parity_windows(G, min(G, tpg))
+    snaps = ([(g0, n_, tracker_host_state(tr, csr, n_, g0)) for g0, n_ in windows]
+             if not args.no_parity else None)
 
     def restore():
         for k in TRACKER_STATE:
@@ -680,24 +812,31 @@ def tracker_main(args, world, rank, dev, barrier):
                 e.record(main)
         for k in range(W, nb):
             step(batches[k])
-    elapsed, step_s = timed_region(region, [st], K, barrier)
+    elapsed, step_s = yield from timed_region(region, [st], K, barrier)
     stats = tr.stats_dict()
     parity = None
-    if snap_host is not None:
-        bad = tracker_parity(tr, csr, snap_host, batches, Gs, oracle_threads(world))
-        parity = (f"bit-exact {Gs}/{Gs} groups (first {Gs} of the shard: match, committed, active, "
-                  f"stepdown after all {nb} ticks vs the sequential C oracle)" if not bad
-                  else f"MISMATCH in {bad} (first {Gs} groups after {nb} ticks)")
+    if snaps is not None:
+        bad = tracker_parity(tr, csr, snaps, batches, oracle_threads(world))
+        ng = sum(n_ for _, n_ in windows)
+        where = ("the whole shard" if len(windows) == 1 else
+                 "three windows of the shard: " + ", ".join(f"[{a}, {a + n_})" for a, n_ in windows))
+        parity = (f"bit-exact {ng}/{ng} groups ({where}: match, committed, active, stepdown after "
+                  f"all {nb} ticks vs the sequential C oracle)" if not bad
+                  else f"MISMATCH in {bad} (after {nb} ticks)")
     route_ms = route_impl = delta_ms = delta_impl = delta_changed = None
     collectives = {}
-    per_rank = _per_rank_values(G * K / elapsed, world)
+    rate_local = G * K / elapsed
+    yield "times"
+    per_rank = _per_rank_values(rate_local, world)
     if world > 1:
         t = torch.tensor([elapsed, step_s], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_s = (float(x) for x in t.tolist())
         route_ms, route_impl, delta_ms, delta_impl, delta_changed, collectives, note = \
-            _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen, restore, barrier)
+            yield from _tracker_collectives(args, world, rank, dev, G, W, tr, batches, gen,
+                                            restore, barrier)
         parity = (parity or "") + "; " + note
+    yield "parity_agree"
     parity = _agree(parity, world, dev)
     if rank != 0:
         return parity, None
@@ -728,10 +867,12 @@ def tracker_main(args, world, rank, dev, barrier):
                    "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
                    "stale_term_fraction": 0.01, "mean_slots": info["slots_mean"],
                    "mean_voters": info["voters_mean"],
+                   "skew": skew,
                    "pipelined_ticks": bool(pipe),
                    "parallelism": f"groups sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic(key) if skew == "none" else None,
                      "kernel": f"{'qb_dev_csr_tracker_step' if csr else 'qb_dev_fixed_tracker_step'}"
                                f" (one step = {kern})",
                      "bytes_per_group": bpg, "avg_kernel_us": step_s * 1e6,
@@ -833,7 +974,8 @@ def _nodewide_eval_parity(args, world, rank, dev, G, B, n, gc, gv, c, v, threads
     slice equals its own outputs (which it checked bit-exact against the
     oracle over the whole shard); on rank 0, every rank's slice against the
     oracle over the first --parity-groups groups of that rank's batch 0 (the
-    counter-based inputs regenerate any sub-range)."""
+    counter-based inputs regenerate any sub-range).  A generator: rank 0's
+    oracle work is followed by an agreement point before the collective."""
     b0 = rank * G
     own = (torch.equal(gc[b0:b0 + G].to(dev), c) and torch.equal(gv[b0:b0 + G].to(dev), v))
     ok0 = True
@@ -845,6 +987,7 @@ def _nodewide_eval_parity(args, world, rank, dev, G, B, n, gc, gv, c, v, threads
             ec, ev_ = eval_oracle(eval_inputs_host(args.workload, n, Gs, (r * B) * G), threads)
             ok0 &= np.array_equal(hc[r * G:r * G + Gs], ec)
             ok0 &= np.array_equal(hv[r * G:r * G + Gs], ev_)
+    yield "nodewide_parity"
     ok = _all_ok(own and ok0, world, dev)
     return (f"node-wide all-gather ({world} ranks) bit-exact: each rank's slice = its own checked "
             f"output, and rank 0 checked the first {Gs} groups of every rank's slice vs the oracle"
@@ -1019,16 +1162,16 @@ def eval_main(args, world, rank, dev, barrier):
                 break
     # (graph replays run on the main stream, forked inside the graph)
     tstreams = [main_stream] if graph is not None else streams
-    elapsed, avg_kernel_s = timed_region(lambda: run_steps(K, fork=graph is not None), tstreams, K,
-                                         barrier)
+    elapsed, avg_kernel_s = yield from timed_region(lambda: run_steps(K, fork=graph is not None),
+                                                    tstreams, K, barrier)
 
     # MALL-warm single-batch rate (informational): one batch (51 MB at
     # configs[1], inside the 256 MB MALL) re-read K times, timed exactly as
     # the region above (events on the launch streams, no fork/join)
     run_steps(W, fixed_batch=0)
     torch.cuda.synchronize()
-    warm_elapsed, warm_kernel_s = timed_region(lambda: run_steps(K, fixed_batch=0, fork=False),
-                                               streams, K, barrier)
+    warm_elapsed, warm_kernel_s = yield from timed_region(
+        lambda: run_steps(K, fixed_batch=0, fork=False), streams, K, barrier, "mall_warm")
 
     # parity: every resident batch's outputs (the last values written by the
     # timed steps; the MALL-warm pass rewrote batch 0 with the same result)
@@ -1049,7 +1192,9 @@ def eval_main(args, world, rank, dev, barrier):
 
     allgather_ms = gather_impl = None
     collectives = {}
-    per_rank = _per_rank_values(G * K / elapsed, world)
+    rate_local = G * K / elapsed
+    yield "times"
+    per_rank = _per_rank_values(rate_local, world)
     if world > 1:
         t = torch.tensor([elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s], dtype=torch.float64,
                          device=dev)
@@ -1057,8 +1202,10 @@ def eval_main(args, world, rank, dev, barrier):
         elapsed, warm_elapsed, avg_kernel_s, warm_kernel_s = (float(x) for x in t.tolist())
         # node-wide result: all-gather one batch's commit (u64) and vote (u8)
         # vectors, timed after the region
+        yield "comm"
         gather, gather_impl = _gather(args, dev)
         c, v = outs[0]
+        yield "allgather_results"
         for _ in range(3):
             gc, gv = gather(c, v, world * G)
         barrier()
@@ -1073,8 +1220,9 @@ def eval_main(args, world, rank, dev, barrier):
             "rccl_ranks": _rccl_ranks(args, world),
             "bytes_received_per_rank": 9 * G * (world - 1)}
         if not args.no_parity:
-            parity = (parity or "") + "; " + _nodewide_eval_parity(
-                args, world, rank, dev, G, B, n, gc, gv, c, v, threads)
+            parity = (parity or "") + "; " + (yield from _nodewide_eval_parity(
+                args, world, rank, dev, G, B, n, gc, gv, c, v, threads))
+    yield "parity_agree"
     parity = _agree(parity, world, dev)
 
     if rank == 0:
@@ -1189,8 +1337,8 @@ def other_summary(o2, p2):
     d = {"workload": o2["config"]["workload"], "value": o2["value"], "unit": o2["unit"],
          "n_gpus": o2["n_gpus"], "steps": o2["steps"], "warmup": o2["warmup"],
          "ms_per_step": o2["ms_per_step"], "value_per_rank": o2.get("value_per_rank"),
-         "roofline": {k: r[k] for k in ("achieved", "frac", "traffic", "bytes_per_group",
-                                        "avg_kernel_us", "kernel")},
+         "roofline": {k: r.get(k) for k in ("achieved", "frac", "traffic", "bytes_per_group",
+                                            "avg_kernel_us", "kernel")},
          "parity": p2}
     if o2.get("collectives"):
         d["collectives"] = o2["collectives"]
@@ -1253,9 +1401,58 @@ def line_shape_errors(line: dict) -> list:
 
 
 def run_other(args, world, rank, dev, barrier):
-    """One secondary workload of the default run (its parity, its JSON dict)."""
+    """One secondary workload of the default run: the generator RankGuard.run
+    drives (its parity, its JSON dict)."""
+    if getattr(args, "fake_workloads", False):
+        return fake_main(args, world, rank, dev, barrier)
     run = tracker_main if args.workload.startswith("tracker") else eval_main
     return run(args, world, rank, dev, barrier)
+
+
+def fake_main(args, world, rank, dev, barrier):
+    """CPU rehearsal of one workload (``--fake-workloads``; tests/
+    test_bench_launcher.py): the stages and collectives of eval_main /
+    tracker_main — region barriers, the per-rank values, a node-wide gather,
+    the parity agreement — over tiny host tensors, so the failure agreement
+    and the deadlines run without a GPU."""
+    x = torch.arange(1 << 12, dtype=torch.int64)
+    yield "region"
+    barrier()
+    t0 = time.perf_counter()
+    y = int((x * 3).sum())
+    elapsed = time.perf_counter() - t0 + 1e-6
+    yield "region:end"
+    barrier()
+    parity = ("bit-exact (cpu rehearsal)" if y == 3 * ((1 << 12) - 1) * (1 << 11)
+              else "MISMATCH (cpu rehearsal)")
+    yield "times"
+    per_rank = _per_rank_values(x.numel() / elapsed, world)
+    coll = {}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        yield "allgather_results"
+        out = [torch.zeros(4, dtype=torch.int64) for _ in range(world)]
+        t0 = time.perf_counter()
+        dist.all_gather(out, torch.full((4,), rank, dtype=torch.int64))
+        ok = all(int(o[0]) == r for r, o in enumerate(out))
+        for c in COLLECTIVES.get(args.workload, ("allgather_results",)):
+            coll[c] = {"ms": (time.perf_counter() - t0) * 1e3 + 1e-3, "impl": "torch gloo (cpu)",
+                       "ranks": world, "rccl_ranks": 0}
+        parity += "; node-wide: all-gather of rank ids" + ("" if ok else " MISMATCH")
+    yield "parity_agree"
+    parity = _agree(parity, world, dev)
+    if rank != 0:
+        return parity, None
+    return parity, {
+        "metric": METRIC, "value": world * x.numel() / elapsed, "unit": "groups/s",
+        "n_gpus": world, "rccl_ranks": 0, "steps": 1, "warmup": 0, "ms_per_step": elapsed * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "cpu rehearsal (--fake-workloads)",
+        "config": {"workload": f"cpu rehearsal of {args.workload}"},
+        "roofline": {k: None for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")},
+        "parity": parity, "collectives": coll, "value_per_rank": per_rank}
 
 
 def parse_args(argv=None):
@@ -1309,37 +1506,91 @@ def parse_args(argv=None):
     ap.add_argument("--lab-lib", default=None,
                     help="A/B lab runs: bind this build of libquorumbatch.so instead of the "
                          "in-tree one (etcd_amd._lib.use_lab_library)")
+    ap.add_argument("--skew", default="none", choices=list(SKEWS),
+                    help="tracker workloads: the records' group distribution (SKEWS: zipf = "
+                         "Zipf(1.1) over groups, zipf-capped = at most 4 x 512 records per group, "
+                         "sb10 / sb30 = 10 %% / 30 %% of the records on one super-bucket)")
+    ap.add_argument("--deadline-s", type=float, default=1500.0,
+                    help="job deadline: a rank still running after this long exits 124 naming "
+                         "its stage (spawned ranks: the parent terminates them 60 s later); "
+                         "0 = none")
+    ap.add_argument("--stage-timeout-s", type=float, default=600.0,
+                    help="one stage's limit (rank watchdog, and torch.distributed's collective "
+                         "timeout); 0 = none")
+    ap.add_argument("--inject-fail", default=None, help=argparse.SUPPRESS)   # R:WORKLOAD:STAGE
+    ap.add_argument("--inject-hang", default=None, help=argparse.SUPPRESS)   # R:WORKLOAD:STAGE
+    ap.add_argument("--fake-workloads", action="store_true", help=argparse.SUPPRESS)  # CPU tests
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def error_line(world: int, workload: str, err: str) -> dict:
+    """The line rank 0 prints when the headline workload failed on some rank."""
+    return {"metric": METRIC, "value": None, "unit": "groups/s", "n_gpus": world,
+            "steps": None, "warmup": None, "ms_per_step": None, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": workload}, "roofline": None, "parity": None,
+            "error": err}
 
 
 def main():
     args = parse_args()
     world, rank, local, spawn = resolve_world(args.gpus, os.environ)
     if spawn:  # no GPU call has happened in this process
-        sys.exit(spawn_ranks(world, sys.argv[1:]))
+        sys.exit(spawn_ranks(world, sys.argv[1:], deadline_s=args.deadline_s))
     if args.launch_check:  # launcher wiring self-test (tests/test_bench_launcher.py)
         print(json.dumps({"rank": rank, "local_rank": local, "world": world,
                           "master": f"{os.environ.get('MASTER_ADDR')}:"
                                     f"{os.environ.get('MASTER_PORT')}"}), flush=True)
         return
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from rankguard import RankGuard, WorkloadAborted, parse_inject
     if args.lab_lib:
         _lib.use_lab_library(args.lab_lib)
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
+    fake = args.fake_workloads
+    if fake:
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:  # rehearsal of the N > 1 path on fewer GPUs
-            dist.init_process_group(args.backend)
+        import datetime
+        kw = ({"timeout": datetime.timedelta(seconds=args.stage_timeout_s)}
+              if args.stage_timeout_s > 0 else {})
+        if args.backend == "nccl" and not fake:
+            dist.init_process_group("nccl", device_id=dev, **kw)
+        else:  # rehearsal of the N > 1 path on fewer GPUs (or none: --fake-workloads)
+            dist.init_process_group(args.backend if not fake else "gloo", **kw)
+    flag_dev = dev if (args.backend == "nccl" and not fake) else torch.device("cpu")
+
+    def agree_fn(flag: int) -> int:
+        t = torch.tensor([flag], dtype=torch.int32, device=flag_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
+    def gather_fn(obj):
+        box = [None] * world
+        dist.all_gather_object(box, obj)
+        return box
+
+    guard = RankGuard(world, rank, agree_fn if world > 1 else None, gather_fn=gather_fn,
+                      stage_timeout_s=args.stage_timeout_s, job_deadline_s=args.deadline_s,
+                      stage_dir=os.environ.get("BENCH_STAGE_DIR"),
+                      inject_fail=parse_inject(args.inject_fail),
+                      inject_hang=parse_inject(args.inject_hang))
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if not fake:
+            torch.cuda.synchronize()
 
-    run = tracker_main if args.workload.startswith("tracker") else eval_main
-    parity, out = run(args, world, rank, dev, barrier)
+    failed = []
+    try:
+        parity, out = guard.run(args.workload, lambda: run_other(args, world, rank, dev, barrier))
+    except WorkloadAborted as ex:
+        parity, out = None, (error_line(world, args.workload, str(ex)) if rank == 0 else None)
+        failed.append(args.workload)
     bad = parity is not None and "MISMATCH" in parity
     if args.workload == "fixed" and not args.no_others:
         # the other BASELINE configs, measured by the same command (so the
@@ -1347,35 +1598,60 @@ def main():
         # configs[3] joint, configs[4] streaming tracker (fixed and ragged CSR
         # groups) — each at its full per-GPU size with its own warm-up, K = 20,
         # parity check and (N > 1) its node-wide collectives and checks.  Every
-        # rank runs them (the collectives need all ranks); rank 0 reports.
+        # rank runs them (the collectives need all ranks); rank 0 reports.  A
+        # failure on any rank is decided by every rank together at the next
+        # agreement point (tools/rankguard.py): all ranks leave that workload,
+        # the line names the error, the others still run.
         others = {}
         for wl in OTHER_WORKLOADS:
             sub = argparse.Namespace(**vars(args))
             sub.workload, sub.steps, sub.warmup, sub.no_cpu_baseline = wl, 20, None, True
             sub.preroll_ms, sub.settle_ms = min(args.preroll_ms, 200.0), min(args.settle_ms, 1000.0)
+            sub.skew = "none"
             try:
-                p2, o2 = run_other(sub, world, rank, dev, barrier)
-            except Exception as ex:  # reported in the line; the headline stands
-                others[wl] = {"error": f"{type(ex).__name__}: {ex}"}
-                torch.cuda.empty_cache()
+                p2, o2 = guard.run(wl, lambda: run_other(sub, world, rank, dev, barrier))
+            except WorkloadAborted as ex:  # every rank: reported in the line
+                others[wl] = {"error": str(ex)}
+                failed.append(wl)
+                if not fake:
+                    torch.cuda.empty_cache()
                 continue
             bad |= p2 is not None and "MISMATCH" in p2
             if o2 is not None:
                 others[wl] = other_summary(o2, p2)
-            torch.cuda.empty_cache()
+            if not fake:
+                torch.cuda.empty_cache()
         if out is not None:
             out["other_configs"] = others
-            if world == 1:
+            if world == 1 and not fake:
+                guard.stage("next_rows")
                 out["next_rows"] = next_rows()
     if out is not None:
+        if failed:
+            out["failed_workloads"] = failed
         print(json.dumps(out), flush=True)
+    guard.stage("exit")
     for c in _COMM:
         c.close()
     if world > 1:
+        guard.agree(False)  # no rank exits before rank 0 has printed the line
         dist.destroy_process_group()
+    guard.close()
     if bad:
         sys.exit(3)
+    if failed:
+        sys.exit(4)
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as ex:  # noqa: BLE001 — e.g. a collective timed out: no agreement left
+        import traceback
+        traceback.print_exc()
+        print(f"bench.py: rank {os.environ.get('RANK', '0')}: {type(ex).__name__}: {ex}; "
+              "exiting 5 (the process group cannot be trusted after this)", file=sys.stderr,
+              flush=True)
+        os._exit(5)

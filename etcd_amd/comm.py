@@ -63,18 +63,54 @@ class RcclComm:
         b, e = shard_range(total, self.world, self.rank)
         return e - b
 
+    @staticmethod
+    def _check_device(name: str, t: torch.Tensor) -> None:
+        if t.device.type != "cuda":
+            raise ValueError(f"{name}: a device tensor is required (got {t.device})")
+
     def _check(self, name: str, t: torch.Tensor, numel: int, sizes) -> None:
         """The C side reads ``numel`` elements from the raw device pointer: a
         wrong length, a host tensor or another element size would be an
         out-of-bounds device read (or a fault inside RCCL), so refuse it."""
-        if t.device.type != "cuda":
-            raise ValueError(f"{name}: a device tensor is required (got {t.device})")
+        self._check_device(name, t)
         if t.element_size() not in sizes:
             raise ValueError(f"{name}: element size {t.element_size()}, expected {sizes}")
         if t.numel() != numel:
             raise ValueError(f"{name}: {t.numel()} elements, expected {numel}")
         if not t.is_contiguous():
             raise ValueError(f"{name}: must be contiguous")
+
+    def _pg_ok(self) -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() == self.world
+
+    def _agree(self, err: Optional[str], extra=None):
+        """Decide the callers' argument checks on every rank together (ADVICE
+        r4): a refusal on one rank alone would leave the others waiting in the
+        RCCL exchange.  When torch.distributed spans the same ranks, one
+        all-reduce (SUM) carries [failed, *extra]; every rank raises if any
+        rank refused.  Returns the summed ``extra`` (or None).  Without a
+        process group the embedder's own channel must agree (the C ABI's
+        route exchange decides its own failures collectively)."""
+        if not self._pg_ok():
+            if err:
+                raise ValueError(err)
+            return None
+        vals = [1 if err else 0] + list(extra or [])
+        dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor(vals, dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        if int(t[0].item()):
+            raise ValueError(err or f"{int(t[0].item())} other rank(s) refused their arguments")
+        return [int(x) for x in t[1:].tolist()]
+
+    def _checked(self, checks) -> Optional[str]:
+        """Run the argument checks locally; the first refusal's text."""
+        try:
+            for c in checks:
+                c()
+        except ValueError as ex:
+            return str(ex)
+        return None
 
     def _workspace(self, nbytes: int) -> torch.Tensor:
         if self._ws is None or self._ws.numel() < nbytes:
@@ -86,16 +122,18 @@ class RcclComm:
                           vote_all: Optional[torch.Tensor] = None):
         """Node-wide commit (u64) / vote (u8) vectors from this rank's shard
         (qb_dev_allgather_results; shard_range order).  ``commit`` / ``vote``
-        hold exactly this rank's shard_range (device, 8-byte / 1-byte)."""
+        hold exactly this rank's shard_range (device, 8-byte / 1-byte).
+        Every rank passes the same ``total``; a refused argument on any rank
+        raises ValueError on every rank (``_agree``)."""
         n = self._shard_len(total)
-        self._check("commit", commit, n, (8,))
-        self._check("vote", vote, n, (1,))
         if commit_all is None:
             commit_all = torch.empty(total, dtype=torch.int64, device=self.device)
         if vote_all is None:
             vote_all = torch.empty(total, dtype=torch.uint8, device=self.device)
-        self._check("commit_all", commit_all, total, (8,))
-        self._check("vote_all", vote_all, total, (1,))
+        self._agree(self._checked([lambda: self._check("commit", commit, n, (8,)),
+                                   lambda: self._check("vote", vote, n, (1,)),
+                                   lambda: self._check("commit_all", commit_all, total, (8,)),
+                                   lambda: self._check("vote_all", vote_all, total, (1,))]))
         need = _lib.fn("qb_allgather_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         _lib.call("qb_dev_allgather_results", self._h, total, commit.data_ptr(), vote.data_ptr(),
@@ -108,15 +146,19 @@ class RcclComm:
         """Apply every rank's changed-commit delta (qb_dev_allgather_changed)
         to ``commit_all`` (device, total u64 kept across ticks, updated in
         place).  ``changed`` (u8) / ``commit``: this rank's shard.  Returns the
-        number of changed groups node-wide."""
-        if changed.dtype not in (torch.uint8, torch.bool):
-            raise ValueError("allgather_changed: changed must be uint8 / bool")
+        number of changed groups node-wide.  Every rank passes the same
+        ``total``; a refused argument on any rank raises on every rank."""
         n = self._shard_len(total)
-        changed = changed.contiguous().view(torch.uint8)
-        commit = commit.contiguous()
-        self._check("changed", changed, n, (1,))
-        self._check("commit", commit, n, (8,))
-        self._check("commit_all", commit_all, total, (8,))
+        err = None
+        if changed.dtype not in (torch.uint8, torch.bool):
+            err = "allgather_changed: changed must be uint8 / bool"
+        else:
+            changed = changed.contiguous().view(torch.uint8)
+            commit = commit.contiguous()
+            err = self._checked([lambda: self._check("changed", changed, n, (1,)),
+                                 lambda: self._check("commit", commit, n, (8,)),
+                                 lambda: self._check("commit_all", commit_all, total, (8,))])
+        self._agree(err)
         need = _lib.fn("qb_allgather_changed_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         n = C.c_uint64(0)
@@ -133,21 +175,23 @@ class RcclComm:
         bound the records this rank receives; by default it is the sum of
         every rank's batch size (all-reduced over torch.distributed when it is
         initialised — ranks may hold batches of different sizes — else world x
-        this rank's M)."""
+        this rank's M).  Ranks may pass different ``out_cap`` values, or some
+        none: the all-reduce runs on every rank either way, and it also
+        carries the column checks, so a rank whose columns are refused raises
+        together with every other rank (the C ABI then decides capacity
+        overflows collectively itself)."""
         from etcd_amd.shard import _device_columns
-        cols = _device_columns(cols)
-        for name, col in cols.items():
-            if col.device.type != "cuda":
-                raise ValueError(f"route_records: column {name!r} must be a device tensor")
-        M = cols["group"].numel()
+        err, M = None, 0
+        try:
+            cols = _device_columns(cols)
+            for name, col in cols.items():
+                self._check_device(f"route_records: column {name!r}", col)
+            M = cols["group"].numel()
+        except ValueError as ex:
+            err = str(ex)
+        summed = self._agree(err, [M])
         if out_cap is None:
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() == self.world:
-                t = torch.tensor([M], dtype=torch.int64,
-                                 device=self.device if dist.get_backend() == "nccl" else "cpu")
-                dist.all_reduce(t)
-                out_cap = int(t.item())
-            else:
-                out_cap = self.world * M
+            out_cap = summed[0] if summed is not None else self.world * M
         out = {}
         for name, col in cols.items():
             out[name] = torch.empty(max(out_cap, 1), dtype=col.dtype, device=self.device)

@@ -92,7 +92,9 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
   // so a region has fewer parts: fewer run-table rows for every chunk
   const u32 wp = bk::region_parts(c.geo.cap, bk::kWideSlack);
   c.geo.ppx = wp ? wp : 1u;
-  c.bucketed = c.geo.NSB <= 4096;
+  // the bucket pass addresses its region grid (NSB x 8 x cap records, about
+  // 2x M) with u32 offsets: a geometry past that takes the atomic grouping
+  c.bucketed = c.geo.NSB <= 4096 && bk::carve(c.geo, 3).nrec <= 0xFFFFFFFFull;
   const size_t pool_b = up256(sizeof(u32) * 2), shard_b = up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
   if (c.bucketed) {
     // the message-chunk pool and the stat shards ride in the bucket carve's
@@ -1302,11 +1304,14 @@ __global__ __launch_bounds__(kBlock) void k_ld_emit(u64 G, const u32* __restrict
 
 // bshards: the bucket pass's shards (bad groups), or null.
 // One wave per counter: lanes sum strided shards, then a shuffle reduction.
+// chunks_used = the chunks actually drawn: the pool counter also counts
+// failed draws (a group finding the pool exhausted), so it is clamped to
+// nchunks.
 __global__ void k_ld_fold(const u64* __restrict__ shards, const u64* __restrict__ bshards,
                           u64* __restrict__ stats, const u32* __restrict__ pool,
-                          u32* __restrict__ chunks_used) {
+                          u32* __restrict__ chunks_used, u64 nchunks) {
   const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (chunks_used && threadIdx.x == 0) *chunks_used = *pool;
+  if (chunks_used && threadIdx.x == 0) *chunks_used = u32(u64(*pool) < nchunks ? u64(*pool) : nchunks);
   if (k >= QB_LSTAT_COUNT) return;
   u64 s = shards[lane * QB_LSTAT_COUNT + k];
   if (bshards && k == QB_LSTAT_BAD_GROUP)
@@ -1452,7 +1457,7 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
     QB_CHECK_LAUNCH("k_ld_emit");
   }
   hipLaunchKernelGGL(ld::k_ld_fold, dim3(1), dim3(64 * QB_LSTAT_COUNT), 0, st, shards, bshards,
-                     ld::U(stats), pool, sink->chunks_used);
+                     ld::U(stats), pool, sink->chunks_used, sink->nchunks);
   QB_CHECK_LAUNCH("k_ld_fold");
   return QB_OK;
 }

@@ -769,7 +769,8 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
 
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
-  return bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 1).total;
+  const bk::Carve cv = bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 1);
+  return cv.nrec <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 region grid)
 }
 
 namespace {
@@ -783,6 +784,11 @@ int fixed_tracker_check(uint32_t n, uint64_t G, uint64_t M, const void* workspac
   QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
   *geo = bk::geometry(n, G, M, 0, bk::kSbIl);
   *cv = bk::carve(*geo, 1);
+  // the reserved regions (NSB x 8 x cap records, about 2x M) are addressed
+  // with u32 offsets by K3-K5
+  QB_REQUIRE(cv->nrec <= 0xFFFFFFFFull,
+             "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
+             (unsigned long long)M, (unsigned long long)cv->nrec);
   QB_REQUIRE(workspace && workspace_bytes >= cv->total,
              "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv->total);
   QB_REQUIRE(geo->NSB <= 4096, "shard too large for the bucket pass (G=%llu)",

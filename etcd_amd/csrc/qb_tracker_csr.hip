@@ -385,7 +385,8 @@ u32 csr_wmax(uint32_t max_slots) {
 extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
   if (max_slots > QB_MAX_SLOTS) return 0;
   const u32 w = csr_wmax(max_slots);
-  return bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 1).total;
+  const bk::Carve cv = bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 1);
+  return cv.nrec <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 region grid)
 }
 
 extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
@@ -412,6 +413,9 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax), bk::kSbIl);
   geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
   const bk::Carve cv = bk::carve(geo, 1);
+  QB_REQUIRE(cv.nrec <= 0xFFFFFFFFull,
+             "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
+             (unsigned long long)M, (unsigned long long)cv.nrec);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
              "workspace too small: need %zu bytes (qb_csr_tracker_workspace_bytes)", cv.total);
   QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",

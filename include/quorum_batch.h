@@ -302,7 +302,9 @@ int qb_dev_fixed_commit_advance(uint32_t n, uint64_t G, const uint64_t* match,
  *   - workspace: device scratch of qb_fixed_tracker_workspace_bytes(n, G, M)
  *     bytes (caller-owned, reusable across calls of the same or smaller
  *     size; no allocation inside, so the call can be graph-captured).
- * Requires G, M < 2^32.
+ * Requires G, M < 2^32, and a batch whose reserved regions (about 2 x M
+ * records) stay below 2^32 records: qb_fixed_tracker_workspace_bytes
+ * returns 0 for a larger one and the step QB_EINVAL.
  * qb_dev_stepdown_check_armed is the opt-in check of that entry rule (for a
  * caller's debug builds): it counts the entries != UINT32_MAX on the device,
  * synchronises the stream and returns QB_EINVAL naming the count if any
@@ -585,7 +587,8 @@ int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
  * g's first chunk, chunk_next[c] the next), in the order the reference
  * emits them.  count[g] = messages stored for g (a group whose chunk could
  * not be drawn — all nchunks used — stops there; the rest is counted in
- * QB_LSTAT_MSGS_DROPPED); *chunks_used (device u32) = chunks drawn.
+ * QB_LSTAT_MSGS_DROPPED); *chunks_used (device u32) = chunks drawn, at most
+ * nchunks (chunks[0 .. chunks_used) hold messages).
  * stepdown_at / gflags / stats as qb_dev_leader_step. */
 #define QB_LEADER_OUTBOX_SLOTS 8
 #define QB_LEADER_OUTBOX_CHUNK 32

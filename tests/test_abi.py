@@ -178,3 +178,26 @@ def test_fake_rccl_library_covers_every_rccl_import():
     assert {s for s in syms(prod, "T") if s.startswith("qb_")} <= have
     ldd = subprocess.run(["ldd", fake], capture_output=True, text=True).stdout
     assert "rccl" not in ldd
+
+
+def test_tracker_region_grid_u32_guard():
+    """The bucketed tracker steps address their reserved regions (about 2 x M
+    records) with u32 offsets: a batch past that has no workspace size (0)
+    and the step refuses it with QB_EINVAL before touching the device
+    (G = 2^30 with M = 2^31 would wrap the region offsets)."""
+    lib = _lib.load()
+    assert lib.qb_fixed_tracker_workspace_bytes(5, 1 << 24, 1 << 24) > 0
+    assert lib.qb_fixed_tracker_workspace_bytes(5, 1 << 30, 1 << 31) == 0
+    assert lib.qb_csr_tracker_workspace_bytes(1 << 24, 8, 1 << 24) > 0
+    assert lib.qb_csr_tracker_workspace_bytes(1 << 30, 8, 1 << 31) == 0
+    dummy = C.c_void_p(0x1000)  # never dereferenced: the check fails first
+    rc = lib.qb_dev_fixed_tracker_step(5, 1 << 30, 1 << 31, dummy, dummy, dummy, dummy, dummy,
+                                       dummy, dummy, None, dummy, dummy, dummy, None, dummy,
+                                       dummy, C.c_size_t(1 << 62), None)
+    assert rc == _lib.QB_EINVAL
+    assert b"region records" in lib.qb_last_error()
+    rc = lib.qb_dev_csr_tracker_step(1 << 30, 8, dummy, dummy, 1 << 31, dummy, dummy, dummy, dummy,
+                                     dummy, dummy, dummy, None, dummy, dummy, dummy, None, dummy,
+                                     dummy, C.c_size_t(1 << 62), None)
+    assert rc == _lib.QB_EINVAL
+    assert b"region records" in lib.qb_last_error()

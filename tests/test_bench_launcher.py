@@ -171,3 +171,100 @@ def test_committed_rehearsal_line_shape(path):
         line = json.loads([x for x in f.read().splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2
     assert bench.line_shape_errors(line) == []
+
+
+# ------------------------------------------------------- failure agreement ---
+# bench.py's workloads run under tools/rankguard.py: a rank-local failure is
+# decided by every rank together at the next agreement point, and a hang is
+# bounded by each rank's watchdog and the launcher's deadline.  These run the
+# real launcher and main loop over --fake-workloads (the workloads' stages and
+# collectives on host tensors, gloo) at world 2.
+
+def _fake_run(*extra, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    t0 = __import__("time").monotonic()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--fake-workloads", *extra], env=env, capture_output=True, text=True,
+                         timeout=timeout)
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    return out, lines, __import__("time").monotonic() - t0
+
+
+def test_fake_world2_run_reports_every_workload():
+    out, lines, _ = _fake_run()
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert len(lines) == 1
+    line = lines[0]
+    assert set(line["other_configs"]) == set(bench.OTHER_WORKLOADS)
+    for wl, o in line["other_configs"].items():
+        assert "error" not in o and "node-wide" in o["parity"], (wl, o)
+        assert set(o["collectives"]) == set(bench.COLLECTIVES[wl])
+    assert "failed_workloads" not in line
+
+
+@pytest.mark.parametrize("inject", ["1:joint:setup", "1:joint:region", "0:tracker:region:end",
+                                    "1:tracker-csr:allgather_results", "0:ragged:parity_agree"])
+def test_injected_failure_every_rank_leaves_the_workload_together(inject):
+    """An exception on one rank of a world-2 run: both ranks leave that
+    workload at the same agreement point (nobody waits in a collective), the
+    line names the failing rank and stage, every other workload still runs,
+    and both ranks exit non-zero (4)."""
+    out, lines, wall = _fake_run("--inject-fail", inject, "--stage-timeout-s", "60")
+    assert out.returncode == 4, out.stderr[-2000:]
+    r, wl, stage = inject.split(":", 2)
+    line = lines[0]
+    assert line["failed_workloads"] == [wl]
+    err = line["other_configs"][wl]["error"]
+    assert f"rank {r} failed at stage {stage!r}" in err and "injected failure" in err
+    for other in bench.OTHER_WORKLOADS:
+        if other != wl:
+            assert "node-wide" in line["other_configs"][other]["parity"]
+    assert wall < 120
+
+
+def test_injected_headline_failure_prints_an_error_line():
+    out, lines, _ = _fake_run("--inject-fail", "1:fixed:times", "--stage-timeout-s", "60")
+    assert out.returncode == 4, out.stderr[-2000:]
+    assert lines[0]["value"] is None and "rank 1 failed at stage 'times'" in lines[0]["error"]
+    assert all("error" not in o for o in lines[0]["other_configs"].values())
+
+
+def test_injected_hang_ends_within_the_stage_limit_and_names_the_stage():
+    """A rank that stops making progress: the other rank's collective times
+    out, the hung rank's watchdog exits 124, the launcher reports each
+    rank's last stage — all within the stage limit plus the grace period."""
+    out, _, wall = _fake_run("--inject-hang", "1:ragged:region", "--stage-timeout-s", "8",
+                             "--deadline-s", "120")
+    assert out.returncode != 0
+    assert wall < 60, wall
+    assert "ranks' last stages" in out.stderr
+    assert "rank 1: ragged:" in out.stderr and "watchdog" in out.stderr
+
+
+def test_job_deadline_terminates_the_ranks():
+    """--deadline-s bounds the whole job whatever the stage limit."""
+    out, _, wall = _fake_run("--inject-hang", "0:joint:setup", "--stage-timeout-s", "0",
+                             "--deadline-s", "6")
+    assert out.returncode != 0 and wall < 60, (out.returncode, wall)
+    assert "job deadline passed" in out.stderr
+
+
+def test_rankguard_world1_raises_local_failures_as_aborted():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from rankguard import RankGuard, WorkloadAborted
+
+    def ok():
+        yield "a"
+        yield "b"
+        return 7
+
+    def boom():
+        yield "a"
+        raise ValueError("x")
+
+    g = RankGuard(1, 0, stage_timeout_s=0)
+    assert g.run("w", ok) == 7
+    with pytest.raises(WorkloadAborted, match="rank 0 failed at stage 'after a' of w: ValueError"):
+        g.run("w", boom)
+    g.close()

@@ -194,3 +194,59 @@ def test_compact_changed_host():
     idx = np.nonzero(changed)[0]
     assert np.array_equal(gid.numpy().astype(np.int64), idx + 40)
     assert np.array_equal(val.numpy().view(np.uint64), commit[idx])
+
+
+def _comm_agree_worker(rank, world, port, q):
+    """RcclComm's argument checks decided on every rank together:
+    the object is built without qb_comm_init (no RCCL here); the checks run
+    before any C call, so a refusal on one rank must raise on all ranks
+    instead of leaving the others in the exchange."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etcd_amd.comm import RcclComm
+        c = RcclComm.__new__(RcclComm)
+        c.world, c.rank, c.device = world, rank, torch.device("cpu")
+        c._check_device = lambda name, t: None   # host tensors stand in for device ones here
+        res = []
+        # only rank 1's column is refused (a host tensor, and an int32 term)
+        M = 8 + rank
+        cols = {"group": torch.zeros(M, dtype=torch.int32), "flags": torch.zeros(M, dtype=torch.uint8),
+                "index": torch.zeros(M, dtype=torch.int64),
+                "term": torch.zeros(M, dtype=torch.int32 if rank == 1 else torch.int64)}
+        try:
+            c.route_records(cols, 100)
+            res.append("no error")
+        except ValueError as ex:
+            res.append(str(ex))
+        except Exception as ex:  # e.g. the C call: must not be reached
+            res.append(f"other {type(ex).__name__}")
+        # agreement with extras: every rank's M summed, no refusal
+        res.append(c._agree(None, [M]))
+        # a refusal on rank 0 only, through allgather_results' checks
+        try:
+            c.allgather_results(torch.zeros(3 if rank == 0 else 50, dtype=torch.int64),
+                                torch.zeros(50, dtype=torch.uint8), 100)
+            res.append("no error")
+        except ValueError as ex:
+            res.append(str(ex))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_argument_refusals_raise_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_comm_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    r0, r1 = got[0], got[1]
+    assert "term" in r1[0] and "refused" in r0[0]      # rank 1's refusal raised on rank 0 too
+    assert r0[1] == r1[1] == [8 + 9]
+    assert "commit" in r0[2] and "refused" in r1[2]
