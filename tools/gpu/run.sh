@@ -6,6 +6,7 @@
 #   tests:FILE[::K]  one GPU test file / test
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     bench.py with ARGS (commas for spaces), JSON to OUTDIR/bench_<n>.json
+#                    (limit $BENCH_TIMEOUT seconds, default 400)
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pmc:CTR[:ARGS]   one rocprofv3 --pmc pass (one counter group) of bench.py ARGS
 #   info             host / GPU description
@@ -27,7 +28,7 @@ for s in "$@"; do
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
         || { echo "smoke failed"; cat "$O/smoke.log"; exit 1; } ;;
     bench)
-      timeout -k 10 400 python -u bench.py $args > "$O/bench_$n.json" 2> "$O/bench_$n.err" \
+      timeout -k 10 ${BENCH_TIMEOUT:-400} python -u bench.py $args > "$O/bench_$n.json" 2> "$O/bench_$n.err" \
         || { echo "bench $args failed"; tail -20 "$O/bench_$n.err"; exit 1; } ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run \
