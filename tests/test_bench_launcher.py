@@ -159,17 +159,19 @@ def test_line_shape_check(n):
 
 COMMITTED_LINES = [
     "profiles/r04/multi/bench_n2_gloo_spawned.json",
+    "profiles/r05/multi/bench_n8_gloo_spawned.json",
 ]
 
 
 @pytest.mark.parametrize("path", COMMITTED_LINES)
 def test_committed_rehearsal_line_shape(path):
-    """The committed `bench.py --gpus 2 --backend gloo` line (two ranks
-    spawned by bench.py on the one-GPU box, torch gloo collectives standing
-    in for RCCL) has every key the N > 1 contract asks for."""
+    """The committed `bench.py --gpus N --backend gloo` lines (N = 2, and the
+    driver's N = 8 in round 5: N ranks spawned by bench.py on the one-GPU
+    box, torch gloo collectives standing in for RCCL) have every key the
+    N > 1 contract asks for."""
     with open(os.path.join(ROOT, path)) as f:
         line = json.loads([x for x in f.read().splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2
+    assert line["n_gpus"] in (2, 8)
     assert bench.line_shape_errors(line) == []
 
 
