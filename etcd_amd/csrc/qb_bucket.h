@@ -50,23 +50,11 @@ struct Cols {
 };
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
 // chunk_slow values: 1 = slow (k_bk_slow applies the chunk from the batch),
-// 2 = deferred to the CSR step's second launch, 3 = a record of the chunk did
-// not fit its reserved region (K3; K5 then sends the chunk to the slow path).
-// Wide records (the leader step) that do not fit go to the overflow area
-// (Ovf) instead, and K3 sets the chunk's flag to 1.
+// 2 = deferred to the CSR step's second launch, 3 = a record of the chunk
+// found no place (K3: the overflow pool was exhausted — never with the
+// sizing below, kept as the exact fallback; K5 sends the chunk to the slow
+// path).
 constexpr u8 kChunkOverflow = 3;
-// Wide records that did not fit their reserved region (a batch concentrated
-// on a few super-buckets), appended in any order with their chunk; the
-// leader's chunk placement (k_ld_chunk_runs) adds a flagged chunk's records
-// from here.  Exact always, slower only for such batches.
-struct Ovf {
-  u32* total;    // records appended (the carve's flag word 1)
-  u32* cnt;      // [NC] records per chunk
-  u64* mr;       // [M] the three wide columns and the chunk
-  u64* index;
-  u32* term32;
-  u32* chunk;
-};
 __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
   return t < u64(kTermEscape) ? u32(t) : kTermEscape;
 }
@@ -102,6 +90,63 @@ struct RecFmt {
 // us; the 4M-group leader step (NSB = 64, 64-record runs) measured its K3
 // 41 -> 55 us with it, so it keeps the linear order.
 constexpr u32 kXcds = 8;
+// Overflow pool (round 5).  A region's records past its `cap` continue in
+// kTile-record pool parts: part k of region r's overflow is pool part
+// ptab[r * kmax + k] - 2 (0 = not drawn yet, 1 = being drawn), drawn from a
+// pool counter by the first K3 workgroup that writes into it.  K4 sorts a
+// pool part by chunk-low like a region part (its chunk-start row is
+// region_rows() + the part's id), and the chunk's run table reads its pool
+// rows after its region rows, in windows of 64 rows (RunTableT::pool_window).
+// So a batch concentrated on a few super-buckets (10 % / 30 % of
+// a 16M-record tick on one super-bucket took 2.6-2.9x a uniform tick through
+// the slow path) is still sorted and applied through LDS; the round-4 slow
+// path for capacity overflow and the leader's scanned overflow area (ADVICE
+// r4: O(flagged chunks x overflow records)) are gone.
+constexpr u32 kPartEmpty = 0, kPartBusy = 1, kPartBase = 2;
+constexpr u32 kNoPart = 0xFFFFFFFFu;
+struct Pool {
+  u32* ptab;      // [NSB * 8 * kmax] (zeroed per call)
+  u32* ctr;       // parts drawn (zeroed per call)
+  u32* owner_r;   // [npool] region of each drawn part
+  u32* owner_k;   // [npool] its index in the region's overflow
+  u32 kmax, npool;
+  u64 base;       // record index of pool part 0 (after the region grid)
+};
+__host__ __device__ __forceinline__ u32 pool_parts_of(u32 fill, u32 cap) {
+  return fill > cap ? (fill - cap + u32(kTile) - 1u) / u32(kTile) : 0u;
+}
+// Part k of region r's overflow (K3; every thread writing into it calls
+// this): the part's id, or kNoPart when the pool or the region's table is
+// exhausted (never with Geometry's sizing; the caller's records then take
+// the exact slow path).  The first caller draws the id (CAS 0 -> 1, pool
+// counter, publish id + 2); the others wait for the published id.  The
+// wait always ends: the draw sits before the wait loop in straight-line
+// code, so every wave publishes each part any of its lanes drew before any
+// of its lanes starts waiting — a lane waits only on a part whose drawing
+// lane has just its counter atomic and one store left, and is not itself
+// waiting (two lanes of one wave never share a region: K3 gives each lane
+// its own super-bucket).
+__device__ __forceinline__ u32 pool_acquire(const Pool& p, u32 r, u32 k) {
+  const bool in = k < p.kmax;
+  u32* e = p.ptab + u64(r) * p.kmax + (in ? k : 0u);
+  u32 v = in ? __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kNoPart;
+  const bool won = v == kPartEmpty && atomicCAS(e, kPartEmpty, kPartBusy) == kPartEmpty;
+  if (won) {
+    const u32 id = atomicAdd(p.ctr, 1u);
+    if (id < p.npool) {
+      p.owner_r[id] = r;
+      p.owner_k[id] = k;
+    }
+    v = id < p.npool ? id + kPartBase : kNoPart;
+    __hip_atomic_store(e, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  while (v < kPartBase) {  // (a winner's v is already >= kPartBase)
+    __builtin_amdgcn_s_sleep(2);
+    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return v == kNoPart ? kNoPart : v - kPartBase;
+}
+
 // Reserved regions per super-bucket (K3, both record forms): the workgroup
 // on XCD x (blockIdx % 8) draws its runs from region x of each super-bucket,
 // so a region is written by one XCD only and the partial lines at its runs'
@@ -163,6 +208,11 @@ struct Geometry {
   // (blockIdx % kRegionShards) go to region sb * kRegionShards + x of cap
   // records, cut into ppx parts of kTile.
   u32 cap, ppx;
+  // Overflow pool: kmax parts per region at most (a region receives at most
+  // its XCD slot's tiles' records), npool parts in all (enough for any
+  // distribution of the batch: see geometry()).
+  u32 kmax, npool;
+  __host__ __device__ u64 region_rows() const { return u64(NSB) * kRegionShards * ppx; }
   __host__ __device__ u32 chunk_of(u32 g) const { return g >> ch_shift; }
   __host__ __device__ u32 sb_of_chunk(u32 c) const {
     return il ? (c & (kXcds - 1u)) | ((c >> 10) << 3) : c >> 7;
@@ -220,58 +270,67 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
   cap = cap < 256 ? 256 : cap > capmax ? capmax : cap;
   g.cap = u32(cap);
   g.ppx = u32((cap + kTile - 1) / kTile);
+  // pool: a region's overflow needs at most ceil((tps * kTile - cap) / kTile)
+  // parts; all regions together at most sum(ceil(ovf_r / kTile)) <=
+  // M / kTile + (overflowing regions), and a region overflows only past cap
+  // records, so there are at most min(regions, M / cap) of them
+  g.kmax = u32(tps + 1);
+  const u64 regions = u64(g.NSB) * S;
+  const u64 novf = (M + cap - 1) / cap;
+  g.npool = M ? u32((M + kTile - 1) / kTile + (novf < regions ? novf : regions) + 1) : 0u;
   return g;
 }
 
 // Workspace carve (all offsets 256-byte aligned).  [shards, zero_end) is
 // zeroed by one memset per call (bucket_records).
 struct Carve {
-  size_t shards, flags, counts, chunk_flags, ovf_cnt, user, zero_end, chunk_start, buf1, buf2, cl,
-      ovf, total;
-  u64 nrec;  // records per column of buf1 / buf2 (the region grid)
+  size_t shards, flags, counts, chunk_flags, ptab, user, zero_end, owner, chunk_start, buf1, buf2,
+      cl, total;
+  u64 nrec;    // records of the region grid (pool part 0 starts here)
+  u64 nrec_all;  // records per column of buf1 / buf2: the region grid + the pool
 };
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
-// ncols = 3: the wide form (index, term32, mr; the leader step) with its
-// overflow area; ncols = 1: the compact form, whose u8 chunk-low column rides
-// in the carve's cl area (the tracker steps).  user: bytes of the caller's
-// own (at `user`) zeroed with the rest by bucket_records' memset.
+// ncols = 3: the wide form (index, term32, mr; the leader step); ncols = 1:
+// the compact form, whose u8 chunk-low column rides in the carve's cl area
+// (the tracker steps).  user: bytes of the caller's own (at `user`) zeroed
+// with the rest by bucket_records' memset.  Both forms' columns hold the
+// region grid followed by the overflow pool (Pool).
+constexpr u32 kFlagPoolCtr = 2;  // flag word: pool parts drawn
 inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   Carve c{};
   size_t o = 0;
   c.shards = o;  o += up256(sizeof(u64) * QB_STAT_COUNT * kShards);
-  c.flags = o;  o += 256;  // u32 words: any_slow (0), Ovf::total (1), slow-path barrier (16..)
+  c.flags = o;  o += 256;  // u32 words: any_slow (0), pool counter (2), slow-path barrier (16..)
   c.counts = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards);  // region fills
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
-  c.ovf_cnt = o;  o += ncols == 3 ? up256(sizeof(u32) * (u64(g.NC) + 1)) : 0;
+  c.ptab = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards * g.kmax);  // pool part table
   c.user = o;  o += up256(user);
   c.zero_end = o;
-  // one row per part of the region grid (NSB x 8 x ppx)
-  const u64 nrows = u64(g.NSB) * kRegionShards * g.ppx;
+  c.owner = o;  o += 2 * up256(sizeof(u32) * (u64(g.npool) + 1));
+  // one row per part of the region grid (NSB x 8 x ppx), then one per pool part
+  const u64 nrows = g.region_rows() + g.npool;
   c.chunk_start = o;  o += up256(sizeof(u32) * nrows * (kChunksPerSb + 1));
   // (columns of at least one record: K5's branch-free loads read record 0 of
   // an empty chunk)
   c.nrec = u64(g.NSB) * kRegionShards * g.cap;
-  const u64 nrec = c.nrec ? c.nrec : 1;
+  c.nrec_all = c.nrec + u64(g.npool) * kTile;
+  const u64 nrec = c.nrec_all ? c.nrec_all : 1;
   c.buf1 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.buf2 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.cl = o;  o += ncols == 1 ? up256(nrec) : 0;
-  // wide: the overflow area, M records (mr, index, term32, chunk)
-  const u64 M1 = g.M ? g.M : 1;
-  c.ovf = o;  o += ncols == 3 ? 2 * up256(sizeof(u64) * M1) + 2 * up256(sizeof(u32) * M1) : 0;
   c.total = o;
   return c;
 }
-inline Ovf ovf_at(char* ws, const Carve& c, const Geometry& g) {
-  const u64 M1 = g.M ? g.M : 1;
-  char* b = ws + c.ovf;
-  Ovf v{};
-  v.total = reinterpret_cast<u32*>(ws + c.flags) + 1;
-  v.cnt = reinterpret_cast<u32*>(ws + c.ovf_cnt);
-  v.mr = reinterpret_cast<u64*>(b);
-  v.index = reinterpret_cast<u64*>(b + up256(sizeof(u64) * M1));
-  v.term32 = reinterpret_cast<u32*>(b + 2 * up256(sizeof(u64) * M1));
-  v.chunk = reinterpret_cast<u32*>(b + 2 * up256(sizeof(u64) * M1) + up256(sizeof(u32) * M1));
-  return v;
+inline Pool pool_at(char* ws, const Carve& c, const Geometry& g) {
+  Pool p{};
+  p.ptab = reinterpret_cast<u32*>(ws + c.ptab);
+  p.ctr = reinterpret_cast<u32*>(ws + c.flags) + kFlagPoolCtr;
+  p.owner_r = reinterpret_cast<u32*>(ws + c.owner);
+  p.owner_k = reinterpret_cast<u32*>(ws + c.owner + up256(sizeof(u32) * (u64(g.npool) + 1)));
+  p.kmax = g.kmax;
+  p.npool = g.npool;
+  p.base = c.nrec;
+  return p;
 }
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
@@ -293,6 +352,7 @@ inline Cols compact_at(char* base, char* cl) {
 // Lane r's row of a run table (RunTableT::issue_regions).
 struct RunRegs {
   u32 l, len, n, slack;
+  u32 fill8;  // lanes 0..7: region x = lane's fill (the pool rows' count)
 };
 // R rows of LDS (kMaxRows for the MANY instantiations, 64 otherwise: the
 // common kernels keep their LDS and so their occupancy).
@@ -302,6 +362,8 @@ struct RunTableT {
   u32 lo[kRuns];
   u32 pre[kRuns + 1];
   u32 nr;
+  u32 npool;     // the chunk's pool rows (finish); windows of 64 (pool_window)
+  u32 ppre[kRegionShards + 1];  // pool rows of regions 0..x-1
   // issue_regions() loads lane r's run (every wave, branch-free: a row past
   // the table reads row 0 and counts nothing); finish() scans the lengths and
   // wave 0 publishes the table.  The caller synchronises before locate().
@@ -335,6 +397,7 @@ struct RunTableT {
     q.n = n;
     q.slack = slack;
     row_run(cs, counts, sb, ppx, cap, cl, n, threadIdx.x & 63u, q.l, q.len, slack);
+    q.fill8 = counts[sb * kRegionShards + (threadIdx.x & (kRegionShards - 1u))];
     return q;
   }
   // Only the non-empty runs enter the table (a region's part past its fill
@@ -370,11 +433,65 @@ struct RunTableT {
       carry += u32(__shfl(int(x), 63, 64));
       kb += u32(__popcll(ne));
     }
+    // the pool rows (round 5): region x's overflow parts, prefix over x
+    {
+      const u32 pp = r < kRegionShards ? pool_parts_of(q.fill8, cap) : 0u;
+      u32 x = pp;
+#pragma unroll
+      for (int o = 1; o < int(kRegionShards); o <<= 1) {
+        const u32 y = u32(__shfl_up(int(x), o, 64));
+        if (r >= u32(o)) x += y;
+      }
+      if (threadIdx.x < kRegionShards) ppre[r + 1] = x;
+      if (threadIdx.x == 0) ppre[0] = 0;
+      const u32 tp = u32(__shfl(int(x), int(kRegionShards) - 1, 64));
+      if (threadIdx.x == 0) npool = tp;
+    }
     if (threadIdx.x == 0) {
       pre[0] = 0;
       nr = kb;
     }
     return carry;
+  }
+  // Window w of the chunk's pool rows (rows [64 w, 64 w + 64) of npool,
+  // region-major): the table is rebuilt from them; returns their records
+  // (wave 0's lanes; the others read pre[nr] after the caller's barrier).
+  // Called by wave 0 after a barrier that published finish()'s npool /
+  // ppre and retired every reader of the previous table.
+  __device__ __forceinline__ u32 pool_window(u32 w, const u32* __restrict__ cs,
+                                             const u32* __restrict__ ptab, u32 kmax,
+                                             u64 region_rows, u32 sb, u32 cl) {
+    const u32 r = threadIdx.x & 63u;
+    const u32 rho = w * 64u + r;
+    u32 l = 0, len = 0;
+    if (rho < npool) {
+      u32 x = 0;
+#pragma unroll
+      for (u32 i = 1; i < kRegionShards; ++i) x = ppre[i] <= rho ? i : x;
+      const u32 e = ptab[u64(sb * kRegionShards + x) * kmax + (rho - ppre[x])];
+      if (e != kNoPart && e >= kPartBase) {
+        const u64 row = (region_rows + (e - kPartBase)) * (kChunksPerSb + 1) + cl;
+        l = cs[row];
+        len = cs[row + 1] - l;
+      }
+    }
+    u32 x = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = u32(__shfl_up(int(x), o, 64));
+      if (r >= u32(o)) x += y;
+    }
+    const u64 ne = __ballot(len != 0);
+    const u32 k = u32(__popcll(ne & ((1ull << r) - 1ull)));
+    if (threadIdx.x < 64 && ((ne >> r) & 1ull)) {
+      lo[k] = l;
+      pre[k + 1] = x;
+    }
+    if (threadIdx.x == 0) {
+      pre[0] = 0;
+      nr = u32(__popcll(ne));
+    }
+    return u32(__shfl(int(x), 63, 64));
   }
   __device__ __forceinline__ u32 locate(u32 f) const {
     u32 a = 0, b = nr;  // pre[a] <= f < pre[b]
@@ -409,15 +526,14 @@ using RunTableOf = RunTableT<MANY ? kMaxRows : 64u>;
 // chunk's records as one run per part of its super-bucket's reserved regions;
 // counts (region fills) and cs (chunk run starts per part) describe them
 // (RunTable::issue_regions reads them).  One memset zeroes [cv.shards,
-// cv.zero_end) first: stat shards, flag words, region fills, chunk flags
-// (and the wide form's per-chunk overflow counts).  Records with group >= G
-// are dropped and counted into shards[QB_STAT_BAD_GROUP], and with n < 16
-// those with slot >= n into shards[QB_STAT_NON_MEMBER].  compact (carve with
-// ncols = 1): the 8-byte compact record (RecFmt) through both levels,
-// chunk-low in the carve's cl bytes between them; a record past its region
-// marks its chunk kChunkOverflow.  Otherwise (carve with ncols = 3) the wide
-// columns (index, term32, mr); a record past its region goes to the overflow
-// area (ovf_at) and its chunk is flagged 1.
+// cv.zero_end) first: stat shards, flag words, region fills, chunk flags and
+// the pool part table.  Records with group >= G are dropped and counted into
+// shards[QB_STAT_BAD_GROUP], and with n < 16 those with slot >= n into
+// shards[QB_STAT_NON_MEMBER].  compact (carve with ncols = 1): the 8-byte
+// compact record (RecFmt) through both levels, chunk-low in the carve's cl
+// bytes between them.  Otherwise (carve with ncols = 3) the wide columns
+// (index, term32, mr).  Records past a region's cap continue in its pool
+// parts (Pool), sorted by K4 like region parts: cs row region_rows() + id.
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
                    hipStream_t st, bool compact);

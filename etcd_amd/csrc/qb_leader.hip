@@ -94,7 +94,7 @@ inline Carve carve(u64 G, u64 M, bool outbox = false) {
   c.geo.ppx = wp ? wp : 1u;
   // the bucket pass addresses its region grid (NSB x 8 x cap records, about
   // 2x M) with u32 offsets: a geometry past that takes the atomic grouping
-  c.bucketed = c.geo.NSB <= 4096 && bk::carve(c.geo, 3).nrec <= 0xFFFFFFFFull;
+  c.bucketed = c.geo.NSB <= 4096 && bk::carve(c.geo, 3).nrec_all <= 0xFFFFFFFFull;
   const size_t pool_b = up256(sizeof(u32) * 2), shard_b = up256(sizeof(u64) * QB_LSTAT_COUNT * 64);
   if (c.bucketed) {
     // the message-chunk pool and the stat shards ride in the bucket carve's
@@ -295,12 +295,12 @@ __global__ __launch_bounds__(kBlock) void k_ld_gather(u64 G, qb_leader_inbox in,
 
 // --------------------------------------------------------- L2 / L3 (bk) ----
 // Records of chunk c: the sum of its runs over the parts of its super-bucket's
-// regions (bk::region_parts with the wide form's slack), plus the chunk's
-// records in the overflow area.
+// regions (bk::region_parts with the wide form's slack) and over their
+// overflow pool parts (a skewed batch).
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
                                                            const u32* __restrict__ counts,
                                                            const u32* __restrict__ cs,
-                                                           const u32* __restrict__ ovf_cnt,
+                                                           const u32* __restrict__ ptab,
                                                            u32* __restrict__ cloc,
                                                            u32* __restrict__ bsum) {
   __shared__ u32 wsum[kBlock / 64];
@@ -309,13 +309,19 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_total(bk::Geometry geo,
   if (c < geo.NC) {
     const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
     const u32 nrow = bk::kRegionShards * geo.ppx;
-    s = ovf_cnt[c];
     for (u32 x = 0; x < bk::kRegionShards; ++x) {
-      u32 fill = counts[sb * bk::kRegionShards + x];
-      fill = fill < geo.cap ? fill : geo.cap;
+      const u32 fill_all = counts[sb * bk::kRegionShards + x];
+      const u32 fill = fill_all < geo.cap ? fill_all : geo.cap;
       const u32 np = bk::region_parts(fill, bk::kWideSlack);
       for (u32 j = 0; j < geo.ppx && j < np; ++j) {
         const u64 row = (u64(sb) * nrow + x * geo.ppx + j) * (bk::kChunksPerSb + 1) + cl;
+        s += cs[row + 1] - cs[row];
+      }
+      const u32 npp = bk::pool_parts_of(fill_all, geo.cap);
+      for (u32 k = 0; k < npp; ++k) {
+        const u32 e = ptab[u64(sb * bk::kRegionShards + x) * geo.kmax + k];
+        if (e == bk::kNoPart || e < bk::kPartBase) continue;
+        const u64 row = (geo.region_rows() + (e - bk::kPartBase)) * (bk::kChunksPerSb + 1) + cl;
         s += cs[row + 1] - cs[row];
       }
     }
@@ -357,14 +363,14 @@ __device__ __forceinline__ ChunkStage& chunk_stage() {
 // run start, cnt[G] = all valid records), then place every record's batch
 // index in its group's run with an LDS cursor.  Order inside a run is
 // arbitrary; the step sorts each run.  The chunk's records are its runs in
-// the parts of its super-bucket's regions (one run table) and, for a chunk
-// flagged by K3 (a skewed batch), its records in the overflow area.
+// the parts of its super-bucket's regions (one run table) and, after a
+// skewed batch, in their overflow pool parts (windows of 64 pool rows
+// through the same table: bk::RunTableT::pool_window).
 template <bool MANY>
 __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::Cols recs,
                                                           const u32* __restrict__ counts,
                                                           const u32* __restrict__ cs,
-                                                          const u8* __restrict__ chunk_flags,
-                                                          bk::Ovf ovf,
+                                                          const u32* __restrict__ ptab,
                                                           const u32* __restrict__ cloc,
                                                           const u32* __restrict__ bsum,
                                                           u32* __restrict__ cnt,
@@ -375,14 +381,12 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   __shared__ u32 wsum[kBlock / 64];
   const u32 c = blockIdx.x, t = threadIdx.x;
   const u32 sb = geo.sb_of_chunk(c), cl = geo.cl_of_chunk(c);
-  // overflow records of this chunk (K3 flagged it): the area is scanned
-  // (both words loaded up front, unconditionally)
-  const u32 cflag = chunk_flags[c], otot = *ovf.total, ocnt = ovf.cnt[c];
   const u32 clo = cloc[c];  // the chunk's prefix within its block of kBlock chunks
   __shared__ u32 s_bpre;
   cur[t] = 0;
+  bk::RunRegs rq{};
   if (t < 64) {  // wave 0: the run table, and the totals of the blocks before this chunk's
-    const bk::RunRegs rq = bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack);
+    rq = bk::RunTable::issue_regions(cs, counts, sb, geo.ppx, geo.cap, cl, bk::kWideSlack);
     const u32 nb = c / kBlock;
     u32 bp = 0;
     for (u32 i = t; i < nb; i += 64) bp += bsum[i];
@@ -391,17 +395,40 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     for (int o = 32; o > 0; o >>= 1) bp += u32(__shfl_xor(int(bp), o, 64));
     if (t == 0) s_bpre = bp;
   }
-  const u32 novf = cflag ? otot : 0u;  // workgroup-uniform
   __syncthreads();  // the run table is published
   const u32 total1 = rt.pre[rt.nr];  // the region records (workgroup-uniform)
-  // Common case (round 3, one pass): no overflow and at most kStageRecs
+  const u32 npool = rt.npool;        // the chunk's pool rows (workgroup-uniform)
+  // Common case (round 3, one pass): no pool rows and at most kStageRecs
   // records — each record is loaded once, into registers (kRegRecs per
   // thread), counted from there and placed from there; otherwise the
   // records are read twice (count, then place) by the loops below.
   constexpr u32 kRegRecs = kStageRecs / kBlock;
   u64 rv[kRegRecs], ri[kRegRecs];
   u32 rt32[kRegRecs];
-  const bool onepass = novf == 0 && total1 <= kStageRecs;  // block-uniform
+  const bool onepass = npool == 0 && total1 <= kStageRecs;  // block-uniform
+  // the chunk's records one at a time (region runs, then the pool rows'
+  // windows, after which the region table is rebuilt for the next pass);
+  // every thread calls it (barriers inside when there are pool rows)
+  auto each = [&](auto&& fn) {
+    for (u32 f = t; f < total1; f += kBlock) {
+      const u32 b = rt.locate(f);
+      fn(recs.mr[b], recs.term32[b], recs.index[b]);
+    }
+    if (npool == 0) return;
+    for (u32 w = 0; w * 64u < npool; ++w) {
+      __syncthreads();
+      if (t < 64) rt.pool_window(w, cs, ptab, geo.kmax, geo.region_rows(), sb, cl);
+      __syncthreads();
+      const u32 tot = rt.pre[rt.nr];
+      for (u32 f = t; f < tot; f += kBlock) {
+        const u32 b = rt.locate(f);
+        fn(recs.mr[b], recs.term32[b], recs.index[b]);
+      }
+    }
+    __syncthreads();
+    if (t < 64) rt.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
+    __syncthreads();
+  };
   if (onepass) {
     u32 b[kRegRecs];
 #pragma unroll
@@ -421,9 +448,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     for (u32 r = 0; r < kRegRecs; ++r)
       if (t + r * kBlock < total1) atomicAdd(&cur[u32(rv[r]) & 1023u], 1u);
   } else {
-    for (u32 f = t; f < total1; f += kBlock) atomicAdd(&cur[u32(recs.mr[rt.locate(f)]) & 1023u], 1u);
-    for (u32 o = t; o < novf; o += kBlock)
-      if (ovf.chunk[o] == c) atomicAdd(&cur[u32(ovf.mr[o]) & 1023u], 1u);
+    each([&](u64 v, u32, u64) { atomicAdd(&cur[u32(v) & 1023u], 1u); });
   }
   __syncthreads();
   const u32 x = cur[t];
@@ -435,25 +460,19 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
   }
   if ((t & 63u) == 63u) wsum[t >> 6] = inc;
   __syncthreads();
-  for (u32 w = 0; w < (t >> 6); ++w) inc += wsum[w];
+  u32 ntot = 0;  // the chunk's records: its region runs plus its pool runs (workgroup-uniform)
+#pragma unroll
+  for (u32 w = 0; w < kBlock / 64; ++w) {
+    if (w < (t >> 6)) inc += wsum[w];
+    ntot += wsum[w];
+  }
   const u32 base = s_bpre + clo, start = inc - x;
-  // the chunk's records: its region runs plus its overflow records
-  const u32 ntot = total1 + (cflag ? ocnt : 0u);  // workgroup-uniform
   const u64 g = u64(c) * kCh + t;
   if (g < geo.G) cnt[g] = base + start;
   if (c + 1 == geo.NC && t == 0) cnt[geo.G] = base + ntot;
   cur[t] = start;
   __syncthreads();  // every group's cur[] start is written
-  // the chunk's records one at a time (region runs, then overflow): the full
-  // term (a kTermEscape term32 is read from the batch by ridx)
-  auto each = [&](auto&& fn) {
-    for (u32 f = t; f < total1; f += kBlock) {
-      const u32 b = rt.locate(f);
-      fn(recs.mr[b], recs.term32[b], recs.index[b]);
-    }
-    for (u32 o = t; o < novf; o += kBlock)
-      if (ovf.chunk[o] == c) fn(ovf.mr[o], ovf.term32[o], ovf.index[o]);
-  };
+  // the full term (a kTermEscape term32 is read from the batch by ridx)
   auto full_term = [&](u64 v, u32 t32) -> u64 {
     return t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
   };
@@ -1381,24 +1400,23 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
     u32* cbs = reinterpret_cast<u32*>(ws + c.cbsum);
     const u32* counts = reinterpret_cast<const u32*>(bws + c.bcv.counts);
     const u32* cs = reinterpret_cast<const u32*>(bws + c.bcv.chunk_start);
-    const bk::Ovf ovf = bk::ovf_at(bws, c.bcv, c.geo);
+    const u32* ptab = reinterpret_cast<const u32*>(bws + c.bcv.ptab);
     // bucket_records zeroes bshards itself (before its first count)
     const int rc = bk::bucket_records(c.geo, c.bcv, bws, in->group, in->flags,
                                       ld::U(in->index), ld::U(in->term), bshards, st,
                                       /*compact=*/false);
     if (rc != QB_OK) return rc;
     hipLaunchKernelGGL(ld::k_ld_chunk_total, dim3((c.geo.NC + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, st, c.geo, counts, cs, ovf.cnt, cloc, cbs);
+                       dim3(kBlock), 0, st, c.geo, counts, cs, ptab, cloc, cbs);
     QB_CHECK_LAUNCH("k_ld_chunk_total");
-    bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, c.bcv.nrec, 3);
+    bk::Cols b2 = bk::cols_at(bws + c.bcv.buf2, c.bcv.nrec_all, 3);
     b2.term32 = reinterpret_cast<u32*>(b2.term);
-    const u8* cfl = reinterpret_cast<const u8*>(bws + c.bcv.chunk_flags);
     if (bk::RunTable::many_rows(c.geo.ppx))
       hipLaunchKernelGGL(ld::k_ld_chunk_runs<true>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
-                         counts, cs, cfl, ovf, cloc, cbs, cnt, perm, *in, rcols);
+                         counts, cs, ptab, cloc, cbs, cnt, perm, *in, rcols);
     else
       hipLaunchKernelGGL(ld::k_ld_chunk_runs<false>, dim3(c.geo.NC), dim3(kBlock), 0, st, c.geo, b2,
-                         counts, cs, cfl, ovf, cloc, cbs, cnt, perm, *in, rcols);
+                         counts, cs, ptab, cloc, cbs, cnt, perm, *in, rcols);
     QB_CHECK_LAUNCH("k_ld_chunk_runs");
   } else {
     u32* cursor = reinterpret_cast<u32*>(ws + c.cursor);

@@ -102,27 +102,41 @@ __device__ __forceinline__ void tile_perm(Lds& L, const u32* start, u32 nrec) {
 // issued before the first LDS step, so the loads overlap each other and the
 // ranking.  Each super-bucket's run of the tile reserves its place in region
 // b * 8 + x (x = the XCD slot, blockIdx % 8) with one returning atomic on the
-// region's fill counter; what does not fit (a skewed batch) is marked (the
-// compact form: the chunk goes to the slow path) or appended to the overflow
-// area (the wide form).  Invalid records go to the stat shards.
+// region's fill counter; what lies past the region's cap (a skewed batch)
+// continues in the region's overflow pool parts (Pool, qb_bucket.h: at most
+// two per run, drawn here).  Invalid records go to the stat shards.
 constexpr int kPer = kTile / kPartThreads;  // records per thread
+static_assert((kTile & (kTile - 1)) == 0, "pool offsets by shift and mask");
+constexpr u32 kTileShift = 12;
+static_assert((1u << kTileShift) == u32(kTile), "kTile = 2^kTileShift");
+// Record index of region-relative position rel of super-bucket b's region x
+// (the region grid, then the pool parts p0 / p1 drawn for the run that
+// starts at gs), or ~0 when the run's pool part could not be drawn.
+__device__ __forceinline__ u64 region_dst(const Geometry& geo, const Pool& pool, u32 b, u32 x,
+                                          u32 rel, u32 gs, u32 p0, u32 p1) {
+  if (rel < geo.cap) return u64(b * kRegionShards + x) * geo.cap + rel;
+  const u32 q = rel - geo.cap, k = q >> kTileShift;
+  const u32 k0 = ((gs > geo.cap ? gs : geo.cap) - geo.cap) >> kTileShift;
+  const u32 pid = k == k0 ? p0 : p1;
+  if (pid == kNoPart) return ~0ull;
+  return pool.base + u64(pid) * kTile + (q & (u32(kTile) - 1u));
+}
 // (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs)
 // COMPACT: the 8-byte records (the tracker steps) go from registers straight
 // to their sorted LDS slot (round 3: K3 115 -> 112 us against the
 // permutation walk); else the wide columns (the leader step) move through
 // the permutation walk, one column at a time.
-struct NoOvf {};
 template <bool COMPACT>
 __global__ __launch_bounds__(kPartThreads)
 __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatter(
     Geometry geo, const u32* __restrict__ rg, const u8* __restrict__ rf,
     const u64* __restrict__ ri, const u64* __restrict__ rt, Cols out, u32* __restrict__ counts,
-    u64* __restrict__ shards, u8* __restrict__ chunk_slow,
-    std::conditional_t<COMPACT, NoOvf, Ovf> ovf) {
+    u64* __restrict__ shards, u8* __restrict__ chunk_slow, Pool pool) {
   extern __shared__ __attribute__((aligned(16))) u32 dyn[];
   u32* start = dyn;               // NSB: count, then local exclusive start
   u32* gstart = dyn + geo.NSB;    // NSB: the run's offset in its region
-  u32* obase = dyn + 2 * geo.NSB; // NSB (wide): overflow slot of region offset 0
+  u32* pid0 = dyn + 2 * geo.NSB;  // NSB: pool parts of the run past the cap
+  u32* pid1 = dyn + 3 * geo.NSB;
   __shared__ TileLds L;
   const u32 tile = geo.tile();
   if (tile >= geo.NT) return;
@@ -216,13 +230,15 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     const u32 nbin = start[b];
     if (!nbin) continue;
-    const u32 gs = atomicAdd(&counts[b * kRegionShards + blockIdx.x % kRegionShards], nbin);
+    const u32 r = b * kRegionShards + blockIdx.x % kRegionShards;
+    const u32 gs = atomicAdd(&counts[r], nbin);
     gstart[b] = gs;  // region-relative
-    if constexpr (!COMPACT) {
-      if (gs + nbin > geo.cap) {  // the run's tail goes to the overflow area
-        const u32 lo = gs > geo.cap ? gs : geo.cap;
-        obase[b] = atomicAdd(ovf.total, gs + nbin - lo) - lo;
-      }
+    if (gs + nbin > geo.cap) {  // the run's tail continues in pool parts (<= 2)
+      const u32 lo = gs > geo.cap ? gs : geo.cap;
+      const u32 k0 = (lo - geo.cap) >> kTileShift, k1 = (gs + nbin - 1u - geo.cap) >> kTileShift;
+      const u32 a = pool_acquire(pool, r, k0);
+      pid0[b] = a;
+      pid1[b] = k1 != k0 ? pool_acquire(pool, r, k1) : a;
     }
   }
   if ((threadIdx.x & 63) == 0 && (nbad | nnon)) {
@@ -247,12 +263,14 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     const u32 x = blockIdx.x % kRegionShards;
     for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
       const u32 b = L.bin[e];
-      const u32 rel = gstart[b] + (e - start[b]);
-      if (rel < geo.cap) {
-        const u32 d = (b * kRegionShards + x) * geo.cap + rel;
+      const u32 gs = gstart[b];
+      const u32 rel = gs + (e - start[b]);
+      const u64 d = rel < geo.cap ? u64(b * kRegionShards + x) * geo.cap + rel
+                                  : region_dst(geo, pool, b, x, rel, gs, pid0[b], pid1[b]);
+      if (d != ~0ull) {
         out.mr[d] = L.stage[e];
         out.cl[d] = L.cl[e];
-      } else {  // past the region (a skewed batch): the chunk takes the slow path
+      } else {  // no pool part (never with the carve's sizing): the exact slow path
         chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
       }
     }
@@ -287,27 +305,18 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
       for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
         const u32 k = L.perm[e];
         const u32 b = L.bin[k];
-        const u32 rel = gstart[b] + (e - start[b]);
+        const u32 gs = gstart[b];
+        const u32 rel = gs + (e - start[b]);
         const u64 val = L.stage[k];
-        if (rel < geo.cap) {
-          const u32 d = (b * kRegionShards + x) * geo.cap + rel;
-          if (col == 0) out.index[d] = val;
-          else if (col == 1) out.term32[d] = term_to32(val);
-          else out.mr[d] = val;
-        } else {  // past the region: the overflow area, the chunk flagged
-          const u32 o = obase[b] + rel;
-          if (col == 0) {
-            ovf.index[o] = val;
-          } else if (col == 1) {
-            ovf.term32[o] = term_to32(val);
-          } else {
-            const u32 c = geo.chunk_of_sb_cl(b, (u32(val) >> 10) & 127u);
-            ovf.mr[o] = val;
-            ovf.chunk[o] = c;
-            chunk_slow[c] = 1;
-            atomicAdd(&ovf.cnt[c], 1u);
-          }
-        }
+        const u64 d = rel < geo.cap ? u64(b * kRegionShards + x) * geo.cap + rel
+                                    : region_dst(geo, pool, b, x, rel, gs, pid0[b], pid1[b]);
+        // (no part: impossible with geometry()'s pool sizing — every region
+        // has kmax > its most parts, the pool >= M / kTile + the overflowing
+        // regions — and the wide form has no slow path to send it to)
+        if (d == ~0ull) continue;
+        if (col == 0) out.index[d] = val;
+        else if (col == 1) out.term32[d] = term_to32(val);
+        else out.mr[d] = val;
       }
       __syncthreads();
     }
@@ -331,26 +340,12 @@ struct alignas(16) TileLdsW {
   u64 stage[kWideTile];
   u32 wsum[kPartThreads / 64];
 };
-__global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
-                                                                const u32* __restrict__ counts,
-                                                                Cols in, Cols out,
-                                                                u32* __restrict__ cs) {
-  // part-major order: workgroup b takes part j0 = b / R of region r = b % R
-  // (R = NSB x 8), so the first parts of neighbouring regions go to
-  // different XCDs whatever ppx is (region-major order put every first part
-  // on the XCDs b % 8 = (r * ppx) % 8: two of eight for an even ppx), and
-  // region (sb, x)'s first part runs on the XCD slot x that wrote it in K3
-  const u32 R = geo.NSB * kRegionShards;
-  const u32 j0 = blockIdx.x / R, r = blockIdx.x - j0 * R;
-  const u32 p = r * geo.ppx + j0;  // the part's run-table row
-  u32 fill = counts[r];
-  fill = fill < geo.cap ? fill : geo.cap;
-  const u32 np = region_parts(fill, kWideSlack);
-  if (j0 >= np) return;  // no such part this call
+// One part (nrec records at lo of `in`) sorted by chunk-low into the same
+// range of `out`; cs row `row` gets the chunk starts.
+__device__ __forceinline__ void split_wide_part(Cols in, Cols out, u32* __restrict__ cs, u32 lo,
+                                                u32 nrec, u64 row) {
   __shared__ TileLdsW L;
   __shared__ u32 start[kChunksPerSb];
-  const u32 lo = r * geo.cap + j0 * u32(kTile);
-  const u32 nrec = j0 + 1 == np ? fill - j0 * u32(kTile) : u32(kTile);
   // The payload columns are loaded now, with mr, and held in registers.
   u64 vi[kPerW], vt[kPerW], vm[kPerW];  // loaded together: one round trip
 #pragma unroll
@@ -374,7 +369,7 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
   __syncthreads();
   tile_scan_bins(start, kChunksPerSb, L.wsum);
   if (threadIdx.x <= kChunksPerSb)
-    cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
+    cs[row * (kChunksPerSb + 1) + threadIdx.x] =
         lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
   tile_perm(L, start, nrec);
   for (u32 e = threadIdx.x; e < nrec; e += blockDim.x) out.mr[lo + e] = L.stage[L.perm[e]];
@@ -396,29 +391,93 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
   }
 }
 
+// Records of pool part pid: the rest of its region's fill past the part's
+// start (a drawn part's positions below the fill are all written by K3).
+__device__ __forceinline__ u32 pool_part_records(const Geometry& geo, const Pool& pool,
+                                                 const u32* __restrict__ counts, u32 pid) {
+  const u32 r = pool.owner_r[pid], k = pool.owner_k[pid];
+  const u32 first = geo.cap + k * u32(kTile), fill = counts[r];
+  const u32 n = fill > first ? fill - first : 0u;
+  return n < u32(kTile) ? n : u32(kTile);
+}
+
+// K4's part for this workgroup: the region grid's part blockIdx.x, or —
+// for the workgroups past `kparts`, one per part the pool can hold — the
+// overflow pool's part blockIdx.x - kparts if it was drawn.  Returns false
+// when there is none (a pool workgroup of a balanced batch returns after one
+// load).  One call site of the part sort per kernel, and no loop: either a
+// second call site or a loop over pool parts measured +21-27 VGPRs and +31
+// SGPRs on the compact K4 (occupancy 8 -> 5).
+template <bool WIDE>
+__device__ __forceinline__ bool k4_item(const Geometry& geo, const Pool& pool,
+                                        const u32* __restrict__ counts, u32 kparts, u32& lo,
+                                        u32& nrec, u64& row) {
+  if (blockIdx.x < kparts) {
+    u32 r, j;
+    if constexpr (WIDE) {
+      // part-major order: workgroup b takes part j = b / R of region r = b % R
+      // (R = NSB x 8), so the first parts of neighbouring regions go to
+      // different XCDs whatever ppx is (region-major order put every first
+      // part on the XCDs b % 8 = (r * ppx) % 8: two of eight for an even
+      // ppx), and region (sb, x)'s first part runs on the XCD slot x that
+      // wrote it in K3
+      const u32 R = geo.NSB * kRegionShards;
+      j = blockIdx.x / R;
+      r = blockIdx.x - j * R;
+    } else {
+      // region-major order (the parts of a region on neighbouring
+      // workgroups): with the tracker's ppx (5 at the bench) the first parts
+      // still spread over the XCDs, and the part-major order measured +1 %
+      // here (profiles/r04/leader/resv/)
+      r = blockIdx.x / geo.ppx;
+      j = blockIdx.x - r * geo.ppx;
+    }
+    u32 fill = counts[r];
+    fill = fill < geo.cap ? fill : geo.cap;
+    if constexpr (WIDE) {
+      const u32 np = region_parts(fill, kWideSlack);
+      if (j >= np) return false;  // no such part this call
+      nrec = j + 1 == np ? fill - j * u32(kTile) : u32(kTile);
+    } else {
+      if (j * u32(kTile) >= fill) return false;  // no such part this tick
+      nrec = fill - j * u32(kTile) < u32(kTile) ? fill - j * u32(kTile) : u32(kTile);
+    }
+    lo = r * geo.cap + j * u32(kTile);
+    row = u64(r) * geo.ppx + j;
+    return true;
+  }
+  const u32 drawn = *pool.ctr;
+  const u32 np = drawn < pool.npool ? drawn : pool.npool;
+  const u32 pid = blockIdx.x - kparts;
+  if (pid >= np) return false;
+  lo = u32(pool.base + u64(pid) * kTile);
+  nrec = pool_part_records(geo, pool, counts, pid);
+  row = geo.region_rows() + pid;
+  return true;
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
+                                                                const u32* __restrict__ counts,
+                                                                Cols in, Cols out,
+                                                                u32* __restrict__ cs, Pool pool,
+                                                                u32 kparts) {
+  u32 lo, nrec;
+  u64 row;
+  if (k4_item<true>(geo, pool, counts, kparts, lo, nrec, row))
+    split_wide_part(in, out, cs, lo, nrec, row);
+}
+
 // K4 for compact records (the tracker steps) in its own kernel: only the
 // staged records and the chunk counters in LDS (33 KB instead of the shared
 // tile's 61 KB) and 512 threads of 8 records, so four parts run per CU
 // instead of two (round 3: fixed tick 583.5 -> 572.2 us).
 constexpr int kSplitThreads = 512;
 constexpr int kSplitPer = kTile / kSplitThreads;
-__global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
-    Geometry geo, const u32* __restrict__ counts, Cols in, Cols out, u32* __restrict__ cs) {
-  // part p = region r's j-th kTile records (the region grid, qb_bucket.h)
-  // region-major order (the parts of a region on neighbouring workgroups):
-  // with the tracker's ppx (5 at the bench) the first parts still spread over
-  // the XCDs, and the part-major order of k_bk_split_wide measured +1 % here
-  // (profiles/r04/leader/resv/)
-  const u32 p = blockIdx.x;
-  const u32 r = p / geo.ppx, j = p - r * geo.ppx;
-  u32 fill = counts[r];
-  fill = fill < geo.cap ? fill : geo.cap;
-  if (j * u32(kTile) >= fill) return;  // no such part this tick
+__device__ __forceinline__ void split_compact_part(Cols in, Cols out, u32* __restrict__ cs, u32 lo,
+                                                   u32 nrec, u64 row) {
   __shared__ u64 stage[kTile];
   __shared__ u32 start[kChunksPerSb];
   __shared__ u32 wsum[kSplitThreads / 64];
-  const u32 lo = r * geo.cap + j * u32(kTile);
-  const u32 nrec = fill - j * u32(kTile) < u32(kTile) ? fill - j * u32(kTile) : u32(kTile);
   u64 vm[kSplitPer];  // loaded together: one round trip
   u32 vc[kSplitPer];
 #pragma unroll
@@ -438,7 +497,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
   __syncthreads();
   tile_scan_bins(start, kChunksPerSb, wsum);
   if (threadIdx.x <= kChunksPerSb)
-    cs[u64(p) * (kChunksPerSb + 1) + threadIdx.x] =
+    cs[row * (kChunksPerSb + 1) + threadIdx.x] =
         lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
 #pragma unroll
   for (int j = 0; j < kSplitPer; ++j) {
@@ -447,6 +506,17 @@ __global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
   }
   __syncthreads();
   for (u32 e = threadIdx.x; e < nrec; e += kSplitThreads) out.mr[lo + e] = stage[e];
+}
+
+__global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
+    Geometry geo, const u32* __restrict__ counts, Cols in, Cols out, u32* __restrict__ cs,
+    Pool pool, u32 kparts) {
+  // part p = region r's j-th kTile records (the region grid, qb_bucket.h),
+  // then the overflow pool's parts
+  u32 lo, nrec;
+  u64 row;
+  if (k4_item<false>(geo, pool, counts, kparts, lo, nrec, row))
+    split_compact_part(in, out, cs, lo, nrec, row);
 }
 
 // ---------------------------------------------------------------- K5 ----
@@ -477,7 +547,8 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
-    u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards) {
+    u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards,
+    const u32* __restrict__ ptab) {
   constexpr u32 CH = chunk_groups(N);
   constexpr u32 B = k5_block(N);
   constexpr u32 GPT = CH / B;  // groups per thread in the commit phase
@@ -599,11 +670,30 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
 #pragma unroll
   for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
   apply(0, total);
-  for (u32 f0 = B * kRecPer; f0 < total; f0 += B * kRecPer) {  // (all rows in one table)
-    fetch(f0, total);
+  // The rest of the region table, then the chunk's records in the overflow
+  // pool (a skewed batch; none otherwise) in windows of 64 pool rows
+  // through the same table — one loop, so the record pass is inlined twice
+  // only (a loop per source cost 13 VGPRs).  Block-uniform control flow.
+  {
+    const u32 npool = rt.npool;
+    u32 tot = total, w = 0;
+    for (u32 f0 = B * kRecPer;;) {
+      if (f0 >= tot) {
+        if (w * 64u >= npool) break;
+        __syncthreads();  // every reader of the previous table is done
+        if (threadIdx.x < 64) rt.pool_window(w, cs, ptab, geo.kmax, geo.region_rows(), sb, cl);
+        __syncthreads();
+        ++w;
+        tot = rt.pre[rt.nr];
+        f0 = 0;
+        continue;
+      }
+      fetch(f0, tot);
 #pragma unroll
-    for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
-    apply(f0, total);
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+      apply(f0, tot);
+      f0 += B * kRecPer;
+    }
   }
   // the counts are final: staged before the barrier the block takes anyway,
   // published after it (a flush with barriers of its own at the end cost
@@ -668,6 +758,7 @@ struct ApplyArgs {
   u8* chunk_slow;
   u32* any_slow;
   u64* stats;
+  const u32* ptab;  // the overflow pool's part table
 };
 
 template <int N, bool MANY>
@@ -676,11 +767,11 @@ void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const 
   if (a.next)
     hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
                        counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats);
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab);
   else
     hipLaunchKernelGGL((k_bk_apply<N, false, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
                        counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats);
+                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab);
 }
 template <int N>
 void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
@@ -739,27 +830,31 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
   if (geo.M == 0) return QB_OK;
   const unsigned kparts = geo.NSB * kRegionShards * geo.ppx;
+  // K4's grid: the region grid's parts, then one workgroup per part the
+  // overflow pool can hold (they return at once when none was drawn)
+  const unsigned pblocks = geo.npool;
+  const Pool pool = pool_at(ws, cv, geo);
   if (compact) {
     const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl), buf2 = compact_at(ws + cv.buf2, nullptr);
     hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads),
-                       2 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
-                       buf1, counts, shards, chunk_flags, NoOvf{});
+                       4 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
+                       buf1, counts, shards, chunk_flags, pool);
     QB_CHECK_LAUNCH("k_bk_scatter");
-    hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts), dim3(kSplitThreads), 0, st, geo, counts, buf1,
-                       buf2, cs);
+    hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts + pblocks), dim3(kSplitThreads), 0, st, geo,
+                       counts, buf1, buf2, cs, pool, kparts);
     QB_CHECK_LAUNCH("k_bk_split_compact");
     return QB_OK;
   }
   // wide: index, term32 (in a u64 column's space) and mr
-  Cols buf1 = cols_at(ws + cv.buf1, cv.nrec, 3), buf2 = cols_at(ws + cv.buf2, cv.nrec, 3);
+  Cols buf1 = cols_at(ws + cv.buf1, cv.nrec_all, 3), buf2 = cols_at(ws + cv.buf2, cv.nrec_all, 3);
   buf1.term32 = reinterpret_cast<u32*>(buf1.term);
   buf2.term32 = reinterpret_cast<u32*>(buf2.term);
   hipLaunchKernelGGL(k_bk_scatter<false>, dim3(geo.tile_grid()), dim3(kPartThreads),
-                     3 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term, buf1,
-                     counts, shards, chunk_flags, ovf_at(ws, cv, geo));
+                     4 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term, buf1,
+                     counts, shards, chunk_flags, pool);
   QB_CHECK_LAUNCH("k_bk_scatter");
-  hipLaunchKernelGGL(k_bk_split_wide, dim3(kparts), dim3(kPartThreads), 0, st, geo, counts, buf1, buf2,
-                     cs);
+  hipLaunchKernelGGL(k_bk_split_wide, dim3(kparts + pblocks), dim3(kPartThreads), 0, st, geo, counts,
+                     buf1, buf2, cs, pool, kparts);
   QB_CHECK_LAUNCH("k_bk_split_wide");
   return QB_OK;
 }
@@ -770,7 +865,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
 extern "C" size_t qb_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
   if (n < 1 || n > QB_MAX_SLOTS) return 0;
   const bk::Carve cv = bk::carve(bk::geometry(n, G, M, 0, bk::kSbIl), 1);
-  return cv.nrec <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 region grid)
+  return cv.nrec_all <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 record index)
 }
 
 namespace {
@@ -786,9 +881,9 @@ int fixed_tracker_check(uint32_t n, uint64_t G, uint64_t M, const void* workspac
   *cv = bk::carve(*geo, 1);
   // the reserved regions (NSB x 8 x cap records, about 2x M) are addressed
   // with u32 offsets by K3-K5
-  QB_REQUIRE(cv->nrec <= 0xFFFFFFFFull,
+  QB_REQUIRE(cv->nrec_all <= 0xFFFFFFFFull,
              "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
-             (unsigned long long)M, (unsigned long long)cv->nrec);
+             (unsigned long long)M, (unsigned long long)cv->nrec_all);
   QB_REQUIRE(workspace && workspace_bytes >= cv->total,
              "workspace too small: need %zu bytes (qb_fixed_tracker_workspace_bytes)", cv->total);
   QB_REQUIRE(geo->NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
@@ -856,7 +951,8 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
                         advanced_out,
                         reinterpret_cast<u8*>(ws + cv.chunk_flags),
                         reinterpret_cast<u32*>(ws + cv.flags),
-                        shards};
+                        shards,
+                        reinterpret_cast<const u32*>(ws + cv.ptab)};
   bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, counts, cs, a,
                      st);
   QB_CHECK_LAUNCH("k_bk_apply");

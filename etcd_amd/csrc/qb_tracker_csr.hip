@@ -55,10 +55,11 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
       const u64 *__restrict__ group_term, const u64 *__restrict__ term_start,                     \
       u64 *__restrict__ match, u64 *__restrict__ next, u16 *__restrict__ active,                  \
       u64 *__restrict__ committed, u32 *__restrict__ stepdown_at, u8 *__restrict__ advanced,      \
-      u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards
+      u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards,          \
+      const u32 *__restrict__ ptab
 #define QB_CSR_APPLY_ARGS                                                                      \
   geo, recs, counts, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
-      stepdown_at, advanced, chunk_slow, any_slow, shards
+      stepdown_at, advanced, chunk_slow, any_slow, shards, ptab
 
 // One chunk c (the whole workgroup).
 template <int WMAX, int CAPW, bool NEXT, bool SECOND, bool MANY>
@@ -168,6 +169,16 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
   u32 total = rtab.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
   __syncthreads();
+  // records in the overflow pool: applied by the launch that carries the
+  // pool loop (below); the first launch defers the chunk to it, before
+  // anything is written (block-uniform: rtab.npool is published)
+  constexpr bool kPoolHere = SECOND || CAPW >= WMAX;
+  if constexpr (!kPoolHere) {
+    if (rtab.npool && !overflow) {
+      if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
+      return;
+    }
+  }
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
@@ -232,6 +243,25 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
     apply(f0, total);
+  }
+  // The chunk's records in the overflow pool (a skewed batch; none
+  // otherwise): windows of 64 pool rows through the same table.  Only the
+  // instantiation that applies deferred chunks (or has no second launch)
+  // carries this loop: it cost the first launch 14 VGPRs (occupancy 8 -> 7),
+  // so that launch defers a chunk with pool rows (above).
+  if constexpr (kPoolHere) {
+    for (u32 w = 0; w * 64u < rtab.npool; ++w) {  // block-uniform (LDS, published before)
+      __syncthreads();  // every reader of the previous table is done
+      if (threadIdx.x < 64) rtab.pool_window(w, cs, ptab, geo.kmax, geo.region_rows(), sb, cl);
+      __syncthreads();
+      const u32 tot = rtab.pre[rtab.nr];
+      for (u32 f0 = 0; f0 < tot; f0 += B * kRecPer) {
+        load(f0, tot);
+#pragma unroll
+        for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+        apply(f0, tot);
+      }
+    }
   }
   if (!fits && threadIdx.x == 0) slow = 1;
   tally.stage(tl);  // the counts are final; published after the barrier
@@ -334,6 +364,7 @@ struct CsrStepArgs {
   u8* chunk_slow;
   u32* any_slow;
   u64* shards;
+  const u32* ptab;  // the overflow pool's part table
 };
 
 template <int WMAX, bool SECOND, bool MANY>
@@ -347,7 +378,7 @@ void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const 
                      grid, dim3(csr_block()), 0, st, geo, recs, counts, cs, a.ri, a.rt, a.off, a.cfg, \
                      a.gt, a.ts,                                                                   \
                      a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
-                     a.any_slow, a.shards)
+                     a.any_slow, a.shards, a.ptab)
   if (a.next) QB_CSR_LAUNCH(true);
   else QB_CSR_LAUNCH(false);
 #undef QB_CSR_LAUNCH
@@ -386,7 +417,7 @@ extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots,
   if (max_slots > QB_MAX_SLOTS) return 0;
   const u32 w = csr_wmax(max_slots);
   const bk::Carve cv = bk::carve(bk::geometry(w, G, M, bk::csr_chunk_groups(w), bk::kSbIl), 1);
-  return cv.nrec <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 region grid)
+  return cv.nrec_all <= 0xFFFFFFFFull ? cv.total : 0;  // 0: no workspace fits (u32 record index)
 }
 
 extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
@@ -413,9 +444,9 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax), bk::kSbIl);
   geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
   const bk::Carve cv = bk::carve(geo, 1);
-  QB_REQUIRE(cv.nrec <= 0xFFFFFFFFull,
+  QB_REQUIRE(cv.nrec_all <= 0xFFFFFFFFull,
              "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
-             (unsigned long long)M, (unsigned long long)cv.nrec);
+             (unsigned long long)M, (unsigned long long)cv.nrec_all);
   QB_REQUIRE(workspace && workspace_bytes >= cv.total,
              "workspace too small: need %zu bytes (qb_csr_tracker_workspace_bytes)", cv.total);
   QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
@@ -447,7 +478,8 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
                           advanced_out,
                           reinterpret_cast<u8*>(ws + cv.chunk_flags),
                           reinterpret_cast<u32*>(ws + cv.flags),
-                          shards};
+                          shards,
+                          reinterpret_cast<const u32*>(ws + cv.ptab)};
   const bk::SlowArgs sa{rec_group, rec_flags, ri, rtm, reinterpret_cast<u32*>(ws + cv.flags) + 16,
                         bk::slow_blocks()};
   u64* stt = reinterpret_cast<u64*>(stats);

@@ -240,6 +240,12 @@ class LeaderGroups:
                   self._ws.data_ptr(), self._ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
         if not fetch:
             return ob, stats
+        return self.fetch_outbox(ob, stats, nchunks)
+
+    def fetch_outbox(self, ob, stats, nchunks: int) -> "LeaderStepResult":
+        """The device outbox of a step_outbox(..., fetch=False) call read back
+        into group order on the host (a LeaderStepResult)."""
+        G = self.G
         cnt = _to_np(ob["count"], np.uint32, G).astype(np.int64)
         slots = ob["slots"].cpu().numpy().view(MSG_DTYPE).reshape(OUTBOX_SLOTS, G)
         chunks = ob["chunks"].cpu().numpy().view(MSG_DTYPE) if nchunks else None
@@ -251,13 +257,24 @@ class LeaderGroups:
         for k in range(OUTBOX_SLOTS):        # row k of every group with > k messages
             sel = np.nonzero(cnt > k)[0]
             msgs[off[sel] + k] = slots[k, sel]
-        for g in np.nonzero(cnt > OUTBOX_SLOTS)[0]:   # the overflow chains (rare)
-            c = int(head[g])
-            for k in range(OUTBOX_SLOTS, int(cnt[g])):
-                j = k - OUTBOX_SLOTS
-                if j and j % OUTBOX_CHUNK == 0:
-                    c = int(nxt[c])
-                msgs[off[g] + k] = chunks[c * OUTBOX_CHUNK + j % OUTBOX_CHUNK]
+        # the overflow chains, one chunk level at a time over every group
+        # whose chain reaches it (vectorised: a hot batch gives many groups
+        # hundreds of messages each)
+        sel = np.nonzero(cnt > OUTBOX_SLOTS)[0]
+        c = head[sel].astype(np.int64)
+        j0 = 0
+        while sel.size:
+            n_here = np.minimum(cnt[sel] - OUTBOX_SLOTS - j0, OUTBOX_CHUNK)
+            for k in range(OUTBOX_CHUNK):
+                m = n_here > k
+                if not m.any():
+                    break
+                msgs[off[sel[m]] + OUTBOX_SLOTS + j0 + k] = chunks[c[m] * OUTBOX_CHUNK + k]
+            j0 += OUTBOX_CHUNK
+            more = cnt[sel] > OUTBOX_SLOTS + j0
+            sel = sel[more]
+            if sel.size:
+                c = nxt[c[more]].astype(np.int64)
         st = stats.cpu().tolist()
         return LeaderStepResult(
             msgs=msgs, msg_total=int(off[-1]), msg_off=off.astype(np.uint32),

@@ -231,9 +231,10 @@ def test_streaming_workload_vs_c_oracle(outbox):
 def test_skewed_batch_overflows_reserved_regions(outbox):
     """A batch concentrated on two super-buckets (the first 65536 of 1M
     groups) plus 10 % of the rest: their runs outgrow the reserved regions
-    (capacity ~2x an even share), the excess goes to the overflow area and
-    the flagged chunks collect it — every state array and message against
-    the C oracle, the bucketing's bad-group count included."""
+    (capacity ~2x an even share), the excess continues in the regions'
+    overflow pool parts and the chunk placement reads them as extra run-table
+    rows — every state array and message against the C oracle, the
+    bucketing's bad-group count included."""
     import torch
     from etcd_amd.quorum.leader import LeaderInbox, streaming_inbox, synth_streaming
     from tests import oracle_c as oc
@@ -301,6 +302,56 @@ def test_dense_batch_many_run_table_rows_vs_c_oracle():
            "hint": ib.hint.cpu().numpy().view(np.uint64),
            "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
     msgs, total, sd, gf, stats = oc.leader_step(host, 32, 0, 0, rec, threads=16, msg_cap=6 * M)
+    dev = lg.numpy()
+    for name in host:
+        assert np.array_equal(dev[name], host[name]), name
+    assert res.msg_total == total
+    assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))
+    assert np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)
+    assert res.stats["applied"] == int(stats[0]) == M
+    torch.cuda.synchronize()
+
+
+@pytest.mark.timeout(600)
+def test_dense_batch_overflow_pool_windows_vs_c_oracle():
+    """64 streaming batches concatenated into one call over 64K groups (64
+    records per group, 4M records): every region receives about twice its
+    capacity (which the run table's 256 rows bound), so each region's excess
+    continues in ~32 overflow pool parts and a chunk reads ~256 pool rows in
+    four 64-row windows.  ADVICE r4: the round-4 overflow area was scanned
+    whole by every flagged chunk (quadratic: 256 chunks x 2M overflow
+    records here); the pool keeps the step linear — timed, and every state
+    array and message against the C oracle."""
+    import time
+
+    import torch
+    from etcd_amd.quorum.leader import LeaderInbox, streaming_inbox, synth_streaming
+    from tests import oracle_c as oc
+    G, R = 1 << 16, 64
+    lg, base = synth_streaming(G, device="cuda")
+    host = {k: v.copy() for k, v in lg.numpy().items()}
+    parts = [streaming_inbox(G, base, k, device="cuda") for k in range(R)]
+    cols = {n: torch.cat([getattr(p_, n) for p_ in parts]) for n in
+            ("group", "flags", "index", "term", "hint", "log_term")}
+    del parts
+    ib = LeaderInbox(**{n: cols[n] for n in ("group", "flags", "index", "term", "hint",
+                                             "log_term")})
+    M = R * G
+    ib._m = M
+    nchunks = M // 8 + 1024
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ob, st = lg.step_outbox(ib, nchunks=nchunks, fetch=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert dt < 2.0, f"leader step over {M} records took {dt:.2f} s"
+    res = lg.fetch_outbox(ob, st, nchunks)
+    rec = {n: cols[n].cpu().numpy() for n in cols}
+    rec = {"group": rec["group"].view(np.uint32), "flags": rec["flags"],
+           "index": rec["index"].view(np.uint64), "term": rec["term"].view(np.uint64),
+           "hint": rec["hint"].view(np.uint64), "log_term": rec["log_term"].view(np.uint64)}
+    msgs, total, sd, gf, stats = oc.leader_step(host, 32, 0, 0, rec, threads=16,
+                                                msg_cap=res.msg_total + 1)
     dev = lg.numpy()
     for name in host:
         assert np.array_equal(dev[name], host[name]), name

@@ -416,9 +416,11 @@ def test_step_skewed_batch_overflows_reserved_regions(hot_frac):
     """K3 reserves each super-bucket's records in regions of twice the mean
     share (qb_bucket.h Geometry::cap); a batch concentrated on one
     super-bucket (hot_frac of 2M records on the 64K groups of super-bucket 0,
-    the rest uniform) overflows them.  The records that do not fit flag
-    their chunks (kChunkOverflow) and those chunks take the exact slow path:
-    the result is still the sequential oracle's, stats included."""
+    the rest uniform) overflows them.  The records past a region's cap
+    continue in its overflow pool parts (round 5; round 4 sent their chunks
+    to the slow path): at hot_frac 1 each region holds ~56 pool parts, so a
+    chunk reads ~450 pool rows in several 64-row windows — the result is the
+    sequential oracle's, stats included."""
     n, G, M = 5, 1 << 20, 1 << 21
     rng = np.random.default_rng(77)
     st = _random_state(rng, n, G)

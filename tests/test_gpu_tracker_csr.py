@@ -415,8 +415,10 @@ def test_csr_step_compact_record_escape_boundaries(max_slots, what):
 @pytest.mark.timeout(300)
 def test_csr_step_skewed_batch_overflows_reserved_regions():
     """The CSR step with a batch concentrated on one super-bucket (1.5M of 2M
-    records on the groups of super-bucket 0): overflowed chunks take the
-    slow path, the result equals the sequential oracle's."""
+    records on the groups of super-bucket 0): the regions' excess continues
+    in overflow pool parts, whose chunks the first apply launch defers to
+    the second (the one with the pool-window loop); the result equals the
+    sequential oracle's."""
     G, M = 1 << 20, 1 << 21
     rng = np.random.default_rng(78)
     off, cfg, sizes, st = _state(rng, "ragged", G)
