@@ -111,7 +111,20 @@ struct Pool {
   u32* owner_k;   // [npool] its index in the region's overflow
   u32 kmax, npool;
   u64 base;       // record index of pool part 0 (after the region grid)
+  u32* sbflag;    // [NSB] 0, or 1 + the super-bucket's index in `heavy` (zeroed per call)
+  u32* heavy;     // [NSB] super-buckets with a region past its cap, in K3's order
+  u32* nheavy;    // their count (zeroed per call)
 };
+// K3: super-bucket sb's region just grew past its cap — list sb once as heavy
+// (its chunks are applied first, by the heavy apply launch, which reads pool
+// rows).
+__device__ __forceinline__ void mark_heavy(const Pool& p, u32 sb) {
+  if (atomicCAS(p.sbflag + sb, 0u, 0xFFFFFFFFu) == 0u) {
+    const u32 i = atomicAdd(p.nheavy, 1u);
+    p.heavy[i] = sb;
+    __hip_atomic_store(p.sbflag + sb, i + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 __host__ __device__ __forceinline__ u32 pool_parts_of(u32 fill, u32 cap) {
   return fill > cap ? (fill - cap + u32(kTile) - 1u) / u32(kTile) : 0u;
 }
@@ -284,8 +297,9 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
 // Workspace carve (all offsets 256-byte aligned).  [shards, zero_end) is
 // zeroed by one memset per call (bucket_records).
 struct Carve {
-  size_t shards, flags, counts, chunk_flags, ptab, user, zero_end, owner, chunk_start, buf1, buf2,
-      cl, total;
+  size_t shards, flags, counts, chunk_flags, ptab, sbflag, ext, user, zero_end, owner, heavy,
+      side_idx, side_tc, chunk_start, buf1, buf2, cl, total;
+  u64 nside;   // dedup side-table entries (compact form: kDedupSlots per chunk-start row)
   u64 nrec;    // records of the region grid (pool part 0 starts here)
   u64 nrec_all;  // records per column of buf1 / buf2: the region grid + the pool
 };
@@ -296,6 +310,23 @@ inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 // with the rest by bucket_records' memset.  Both forms' columns hold the
 // region grid followed by the overflow pool (Pool).
 constexpr u32 kFlagPoolCtr = 2;  // flag word: pool parts drawn
+constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions overflowed
+// K4 dedup (compact form, round 5): a chunk's run of at least kHeavyRun
+// records in one part (a hot group: an even batch puts ~32 records of a chunk
+// in a part) has its records with equal lg | slot | reject | term folded into
+// one — the largest index and the count — through an LDS table of
+// kDedupSlots entries.  A folded record is a compact escape whose payload
+// holds kDedupFlag | its side-table entry (row * kDedupSlots + table slot):
+// side_idx = the largest index, side_tc = term | count << kDedupCountShift.
+// K5 applies it as `count` records of that class (MaybeUpdate is a max, the
+// RecentActive bit an or; batch order only matters in a chunk with a
+// higher-term record, which still goes to the slow path, which re-reads the
+// original batch).  Escape payloads (batch positions) stay below 2^32.
+constexpr u32 kHeavyRun = 512;
+constexpr u32 kDedupSlots = 256;
+constexpr u64 kDedupFlag = 1ull << 39;
+constexpr u32 kDedupCountShift = 12;
+constexpr u32 kExtClasses = 4;  // stale, applied, rejected, non-member
 inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   Carve c{};
   size_t o = 0;
@@ -304,11 +335,21 @@ inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   c.counts = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards);  // region fills
   c.chunk_flags = o;  o += up256(u64(g.NC) + 1);  // u8 per chunk (chunk_slow)
   c.ptab = o;  o += up256(sizeof(u32) * u64(g.NSB) * kRegionShards * g.kmax);  // pool part table
+  // per super-bucket: 0, or 1 + its index in the heavy list (a region of it
+  // overflowed into the pool; K3)
+  c.sbflag = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 1));
+  // per chunk: the records K4's dedup folded away, by class (stale, applied,
+  // rejected, non-member) — added to the stats by K5 unless the chunk is slow
+  c.ext = o;  o += ncols == 1 ? up256(sizeof(u32) * kExtClasses * (u64(g.NC) + 1)) : 0;
   c.user = o;  o += up256(user);
   c.zero_end = o;
   c.owner = o;  o += 2 * up256(sizeof(u32) * (u64(g.npool) + 1));
+  c.heavy = o;  o += up256(sizeof(u32) * (u64(g.NSB) + 1));  // the heavy super-buckets (K3)
   // one row per part of the region grid (NSB x 8 x ppx), then one per pool part
   const u64 nrows = g.region_rows() + g.npool;
+  c.nside = ncols == 1 ? nrows * kDedupSlots : 0;
+  c.side_idx = o;  o += up256(sizeof(u64) * (c.nside ? c.nside : 1));
+  c.side_tc = o;  o += up256(sizeof(u32) * (c.nside ? c.nside : 1));
   c.chunk_start = o;  o += up256(sizeof(u32) * nrows * (kChunksPerSb + 1));
   // (columns of at least one record: K5's branch-free loads read record 0 of
   // an empty chunk)
@@ -330,7 +371,26 @@ inline Pool pool_at(char* ws, const Carve& c, const Geometry& g) {
   p.kmax = g.kmax;
   p.npool = g.npool;
   p.base = c.nrec;
+  p.sbflag = reinterpret_cast<u32*>(ws + c.sbflag);
+  p.heavy = reinterpret_cast<u32*>(ws + c.heavy);
+  p.nheavy = reinterpret_cast<u32*>(ws + c.flags) + kFlagHeavyCtr;
   return p;
+}
+// The K4 dedup side table (compact form) and what K4 needs to class the
+// records it folds away (the slow path, which re-reads the batch, ignores
+// ext for its chunks).
+struct Side {
+  u64* idx;
+  u32* tc;
+  u32* ext;                // [NC][kExtClasses] (zeroed per call)
+  const u64* group_term;   // the caller's, for the class of a folded record
+  const u32* off;          // CSR: slot offsets (a slot past the group's count has
+                           // no Progress); null for the FIXED layout
+};
+inline Side side_at(char* ws, const Carve& c, const u64* group_term = nullptr,
+                    const u32* off = nullptr) {
+  return Side{reinterpret_cast<u64*>(ws + c.side_idx), reinterpret_cast<u32*>(ws + c.side_tc),
+              reinterpret_cast<u32*>(ws + c.ext), group_term, off};
 }
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
@@ -536,7 +596,8 @@ using RunTableOf = RunTableT<MANY ? kMaxRows : 64u>;
 // parts (Pool), sorted by K4 like region parts: cs row region_rows() + id.
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool compact);
+                   hipStream_t st, bool compact, const u64* group_term = nullptr,
+                   const u32* csr_off = nullptr);
 
 
 }  // namespace bk

@@ -429,78 +429,104 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     if (t < 64) rt.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
     __syncthreads();
   };
-  if (onepass) {
-    u32 b[kRegRecs];
-#pragma unroll
-    for (u32 r = 0; r < kRegRecs; ++r) {
-      const u32 f = t + r * kBlock;
-      b[r] = f < total1 ? rt.locate(f) : 0u;
-    }
-#pragma unroll
-    for (u32 r = 0; r < kRegRecs; ++r) {
-      if (t + r * kBlock < total1) {
-        rv[r] = recs.mr[b[r]];
-        rt32[r] = recs.term32[b[r]];
-        ri[r] = recs.index[b[r]];
-      }
-    }
-#pragma unroll
-    for (u32 r = 0; r < kRegRecs; ++r)
-      if (t + r * kBlock < total1) atomicAdd(&cur[u32(rv[r]) & 1023u], 1u);
-  } else {
-    each([&](u64 v, u32, u64) { atomicAdd(&cur[u32(v) & 1023u], 1u); });
-  }
-  __syncthreads();
-  const u32 x = cur[t];
-  u32 inc = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u32 y = u32(__shfl_up(int(inc), o, 64));
-    if ((t & 63u) >= u32(o)) inc += y;
-  }
-  if ((t & 63u) == 63u) wsum[t >> 6] = inc;
-  __syncthreads();
-  u32 ntot = 0;  // the chunk's records: its region runs plus its pool runs (workgroup-uniform)
-#pragma unroll
-  for (u32 w = 0; w < kBlock / 64; ++w) {
-    if (w < (t >> 6)) inc += wsum[w];
-    ntot += wsum[w];
-  }
-  const u32 base = s_bpre + clo, start = inc - x;
-  const u64 g = u64(c) * kCh + t;
-  if (g < geo.G) cnt[g] = base + start;
-  if (c + 1 == geo.NC && t == 0) cnt[geo.G] = base + ntot;
-  cur[t] = start;
-  __syncthreads();  // every group's cur[] start is written
   // the full term (a kTermEscape term32 is read from the batch by ridx)
   auto full_term = [&](u64 v, u32 t32) -> u64 {
     return t32 != bk::kTermEscape ? u64(t32) : in.term[u32(v >> 32)];
   };
-  if (ntot <= kStageRecs) {
-    // Common case: the chunk's records are placed in LDS, each group's run
-    // is put in batch order there (runs of <= kLdsSortMax), and the chunk
-    // is written out with coalesced stores.
-    ChunkStage& cs_ = chunk_stage();
-    if (onepass) {
+  ChunkStage& cs_ = chunk_stage();
+  // Two passes over the chunk's records — count per group, then place — with
+  // ONE inlined walk (`each`): three walks (count, LDS placement, HBM
+  // placement) with the pool windows held 90 VGPRs against 68 before them.
+  // Common case: the records are placed in LDS, each group's run is put in
+  // batch order there (runs of <= kLdsSortMax), and the chunk is written
+  // out with coalesced stores; a chunk of more than kStageRecs records is
+  // placed in HBM directly.
+  u32 x = 0, start = 0, base = 0, ntot = 0;
+  bool staged = true;
+#pragma clang loop unroll(disable)
+  for (u32 pass = 0; pass < 2u; ++pass) {
+    if (pass == 1u) {  // the counts' scan: each group's run start
+      __syncthreads();
+      x = cur[t];
+      u32 inc = x;
 #pragma unroll
-      for (u32 r = 0; r < kRegRecs; ++r) {
-        if (t + r * kBlock < total1) {
-          const u64 v = rv[r];
-          const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
-          cs_.mr[e] = v;
-          cs_.term[e] = full_term(v, rt32[r]);
-          cs_.index[e] = ri[r];
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = u32(__shfl_up(int(inc), o, 64));
+        if ((t & 63u) >= u32(o)) inc += y;
+      }
+      if ((t & 63u) == 63u) wsum[t >> 6] = inc;
+      __syncthreads();
+      ntot = 0;  // the chunk's records: its region runs plus its pool runs (workgroup-uniform)
+#pragma unroll
+      for (u32 w = 0; w < kBlock / 64; ++w) {
+        if (w < (t >> 6)) inc += wsum[w];
+        ntot += wsum[w];
+      }
+      base = s_bpre + clo;
+      start = inc - x;
+      const u64 g = u64(c) * kCh + t;
+      if (g < geo.G) cnt[g] = base + start;
+      if (c + 1 == geo.NC && t == 0) cnt[geo.G] = base + ntot;
+      cur[t] = start;
+      staged = ntot <= kStageRecs;
+      __syncthreads();  // every group's cur[] start is written
+    }
+    if (onepass) {
+      if (pass == 0u) {
+        u32 b[kRegRecs];
+#pragma unroll
+        for (u32 r = 0; r < kRegRecs; ++r) {
+          const u32 f = t + r * kBlock;
+          b[r] = f < total1 ? rt.locate(f) : 0u;
+        }
+#pragma unroll
+        for (u32 r = 0; r < kRegRecs; ++r) {
+          if (t + r * kBlock < total1) {
+            rv[r] = recs.mr[b[r]];
+            rt32[r] = recs.term32[b[r]];
+            ri[r] = recs.index[b[r]];
+          }
+        }
+#pragma unroll
+        for (u32 r = 0; r < kRegRecs; ++r)
+          if (t + r * kBlock < total1) atomicAdd(&cur[u32(rv[r]) & 1023u], 1u);
+      } else {  // (staged: total1 <= kStageRecs)
+#pragma unroll
+        for (u32 r = 0; r < kRegRecs; ++r) {
+          if (t + r * kBlock < total1) {
+            const u64 v = rv[r];
+            const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
+            cs_.mr[e] = v;
+            cs_.term[e] = full_term(v, rt32[r]);
+            cs_.index[e] = ri[r];
+          }
         }
       }
     } else {
       each([&](u64 v, u32 t32, u64 index) {
         const u32 e = atomicAdd(&cur[u32(v) & 1023u], 1u);
-        cs_.mr[e] = v;
-        cs_.term[e] = full_term(v, t32);
-        cs_.index[e] = index;
+        if (pass == 0u) return;  // (count)
+        if (staged) {
+          cs_.mr[e] = v;
+          cs_.term[e] = full_term(v, t32);
+          cs_.index[e] = index;
+          return;
+        }
+        const u32 k = base + e, i = u32(v >> 32);
+        const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
+        perm[k] = i;
+        rc.flags[k] = fl;
+        rc.term[k] = full_term(v, t32);
+        rc.index[k] = index;
+        if (fl & QB_REC_REJECT) {
+          rc.hint[k] = in.hint ? in.hint[i] : 0ull;
+          rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
+        }
       });
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  if (staged) {
     if (x > 1 && x <= kLdsSortMax) {
       for (u32 a = start + 1; a < start + x; ++a) {
         const u64 v = cs_.mr[a], tv = cs_.term[a], iv = cs_.index[a];
@@ -534,22 +560,8 @@ __global__ __launch_bounds__(kBlock) void k_ld_chunk_runs(bk::Geometry geo, bk::
     if (x > kLdsSortMax) gather_run(in, perm, base + start, x, rc);
     return;
   }
-  each([&](u64 v, u32 t32, u64 index) {
-    const u32 k = base + atomicAdd(&cur[u32(v) & 1023u], 1u);
-    const u32 i = u32(v >> 32);
-    const u8 fl = u8(u32(v) >> 17);  // the record's flags byte (qb_bucket.h)
-    perm[k] = i;
-    rc.flags[k] = fl;
-    rc.term[k] = full_term(v, t32);
-    rc.index[k] = index;
-    if (fl & QB_REC_REJECT) {
-      rc.hint[k] = in.hint ? in.hint[i] : 0ull;
-      rc.log_term[k] = in.log_term ? in.log_term[i] : 0ull;
-    }
-  });
   // A group with several records: its run (placed in arbitrary order) is
   // put in batch order and its fields gathered again in that order.
-  __syncthreads();  // the chunk's runs are complete (workgroup-visible)
   if (x > 1) order_run(in, perm, base + start, x, rc);
 }
 

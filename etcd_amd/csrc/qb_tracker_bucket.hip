@@ -234,6 +234,8 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     const u32 gs = atomicAdd(&counts[r], nbin);
     gstart[b] = gs;  // region-relative
     if (gs + nbin > geo.cap) {  // the run's tail continues in pool parts (<= 2)
+      if constexpr (COMPACT)
+        if (gs <= geo.cap) mark_heavy(pool, b);  // (the one run that crosses the cap)
       const u32 lo = gs > geo.cap ? gs : geo.cap;
       const u32 k0 = (lo - geo.cap) >> kTileShift, k1 = (gs + nbin - 1u - geo.cap) >> kTileShift;
       const u32 a = pool_acquire(pool, r, k0);
@@ -411,7 +413,7 @@ __device__ __forceinline__ u32 pool_part_records(const Geometry& geo, const Pool
 template <bool WIDE>
 __device__ __forceinline__ bool k4_item(const Geometry& geo, const Pool& pool,
                                         const u32* __restrict__ counts, u32 kparts, u32& lo,
-                                        u32& nrec, u64& row) {
+                                        u32& nrec, u64& row, u32& sb) {
   if (blockIdx.x < kparts) {
     u32 r, j;
     if constexpr (WIDE) {
@@ -444,6 +446,7 @@ __device__ __forceinline__ bool k4_item(const Geometry& geo, const Pool& pool,
     }
     lo = r * geo.cap + j * u32(kTile);
     row = u64(r) * geo.ppx + j;
+    sb = r / kRegionShards;
     return true;
   }
   const u32 drawn = *pool.ctr;
@@ -453,6 +456,7 @@ __device__ __forceinline__ bool k4_item(const Geometry& geo, const Pool& pool,
   lo = u32(pool.base + u64(pid) * kTile);
   nrec = pool_part_records(geo, pool, counts, pid);
   row = geo.region_rows() + pid;
+  sb = pool.owner_r[pid] / kRegionShards;
   return true;
 }
 
@@ -461,9 +465,9 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
                                                                 Cols in, Cols out,
                                                                 u32* __restrict__ cs, Pool pool,
                                                                 u32 kparts) {
-  u32 lo, nrec;
+  u32 lo, nrec, sb;
   u64 row;
-  if (k4_item<true>(geo, pool, counts, kparts, lo, nrec, row))
+  if (k4_item<true>(geo, pool, counts, kparts, lo, nrec, row, sb))
     split_wide_part(in, out, cs, lo, nrec, row);
 }
 
@@ -473,8 +477,112 @@ __global__ __launch_bounds__(kPartThreads) void k_bk_split_wide(Geometry geo,
 // instead of two (round 3: fixed tick 583.5 -> 572.2 us).
 constexpr int kSplitThreads = 512;
 constexpr int kSplitPer = kTile / kSplitThreads;
-__device__ __forceinline__ void split_compact_part(Cols in, Cols out, u32* __restrict__ cs, u32 lo,
-                                                   u32 nrec, u64 row) {
+// A part holding a chunk run of >= kHeavyRun records (a hot group): after
+// the part is sorted by chunk-low into stage[] (its registers are dead by
+// then, so this path costs the common one no VGPRs), each such run's records
+// with equal lg | slot | reject | term are folded into one (qb_bucket.h,
+// kDedupFlag) — the largest index and the count, in the side table at row *
+// kDedupSlots + its LDS table slot — and the part is written out with the
+// new run lengths.  Escapes, and records that find no table slot within 8
+// probes, stay as they are.  start[] holds the exclusive bin starts (nrec
+// records), and stays the old starts until the recount.
+__device__ __forceinline__ u32 bin_of(const u32* start, u32 e) {
+  u32 a = 0;  // start[a] <= e, 128 bins
+#pragma unroll
+  for (u32 st = 64; st >= 1; st >>= 1) a = start[a + st] <= e ? a + st : a;
+  return a;
+}
+__device__ __forceinline__ void dedup_compact_part(const Geometry& geo, Cols out,
+                                                   u32* __restrict__ cs, u32 lo, u32 nrec, u64 row,
+                                                   u32 sb, Side side, const u64* stage, u32* start,
+                                                   u32* wsum) {
+  const RecFmt fmt = geo.fmt;
+  __shared__ u32 hkey[kDedupSlots];
+  __shared__ u64 hmax[kDedupSlots];
+  __shared__ u32 hcnt[kDedupSlots];
+  __shared__ u32 cnt2[kChunksPerSb + 1];
+  constexpr u32 kEmpty = 0xFFFFFFFFu;  // (a key's top bit is 0: chunk-low < 128)
+  for (u32 i = threadIdx.x; i < kDedupSlots; i += kSplitThreads) {
+    hkey[i] = kEmpty;
+    hmax[i] = 0;
+    hcnt[i] = 0;
+  }
+  if (threadIdx.x <= kChunksPerSb) cnt2[threadIdx.x] = 0;
+  __syncthreads();
+  u32 keep = 0;  // bit j: position threadIdx.x + j * kSplitThreads stays a record of its own
+  for (u32 j = 0; j < u32(kSplitPer); ++j) {
+    const u32 e = threadIdx.x + j * kSplitThreads;
+    if (e >= nrec) break;
+    const u32 b = bin_of(start, e);
+    const u32 nb = (b + 1 < kChunksPerSb ? start[b + 1] : nrec) - start[b];
+    const u64 v = stage[e];
+    bool merged = false;
+    if (nb >= kHeavyRun && fmt.term(v) != fmt.tesc()) {
+      const u32 key = (b << kRecHdrBits) | (u32(v) & ((1u << kRecHdrBits) - 1u));
+      const u32 h = (key * 2654435761u) >> 24;
+      for (u32 q = 0; q < 8 && !merged; ++q) {
+        const u32 sl = (h + q) & (kDedupSlots - 1u);
+        const u32 old = atomicCAS(&hkey[sl], kEmpty, key);
+        if (old == kEmpty || old == key) {
+          atomicMax(&hmax[sl], v >> kRecHdrBits);
+          atomicAdd(&hcnt[sl], 1u);
+          merged = true;
+        }
+      }
+    }
+    if (!merged) {
+      keep |= 1u << j;
+      atomicAdd(&cnt2[b], 1u);
+    }
+  }
+  __syncthreads();  // the table is complete
+  const u32 hk = threadIdx.x < kDedupSlots ? hkey[threadIdx.x] : kEmpty;
+  if (hk != kEmpty) atomicAdd(&cnt2[hk >> kRecHdrBits], 1u);
+  __syncthreads();
+  const u32 total = tile_scan_bins(cnt2, kChunksPerSb, wsum);  // cnt2 = the new bin starts
+  if (threadIdx.x <= kChunksPerSb)
+    cs[row * (kChunksPerSb + 1) + threadIdx.x] =
+        lo + (threadIdx.x < kChunksPerSb ? cnt2[threadIdx.x] : total);
+  __syncthreads();  // (cnt2 is a placement cursor from here on)
+  for (u32 j = 0; j < u32(kSplitPer); ++j) {
+    const u32 e = threadIdx.x + j * kSplitThreads;
+    if (e >= nrec) break;
+    if (!((keep >> j) & 1u)) continue;
+    out.mr[lo + atomicAdd(&cnt2[bin_of(start, e)], 1u)] = stage[e];
+  }
+  if (hk != kEmpty) {
+    const u32 n = hcnt[threadIdx.x];
+    const u64 mx = hmax[threadIdx.x], hdr = hk & ((1u << kRecHdrBits) - 1u);
+    u64 rec = hdr | (mx << kRecHdrBits);  // a single record: itself
+    if (n > 1) {
+      const u64 si = row * kDedupSlots + threadIdx.x;
+      const u32 t = fmt.term(hdr);
+      side.idx[si] = mx;
+      side.tc[si] = t | (n << kDedupCountShift);
+      const u64 tmask = u64(fmt.tesc()) << fmt.term_shift();
+      rec = (hdr & ~tmask) | tmask | ((si | kDedupFlag) << kRecHdrBits);
+      // the n - 1 records folded away, in the class K5 gives the record that
+      // stands for them (a higher term sends the chunk to the slow path,
+      // which counts every record itself: nothing to add)
+      const u32 c = geo.chunk_of_sb_cl(sb, hk >> kRecHdrBits);
+      const u64 g = u64(c) * geo.CH + fmt.lg(hdr);
+      const u32 s = fmt.slot(hdr);
+      u32 cls = 4;  // none
+      if (side.off && s >= side.off[g + 1] - side.off[g]) {
+        cls = 3;  // non-member (CSR: raft.go:1100-1104)
+      } else {
+        const u64 gt = side.group_term[g];
+        cls = u64(t) < gt ? 0u : u64(t) > gt ? 4u : fmt.rej(hdr) ? 2u : 1u;
+      }
+      if (cls < kExtClasses) atomicAdd(&side.ext[u64(c) * kExtClasses + cls], n - 1u);
+    }
+    out.mr[lo + atomicAdd(&cnt2[hk >> kRecHdrBits], 1u)] = rec;
+  }
+}
+
+__device__ __forceinline__ void split_compact_part(const Geometry& geo, Cols in, Cols out,
+                                                   u32* __restrict__ cs, u32 lo, u32 nrec, u64 row,
+                                                   u32 sb, Side side) {
   __shared__ u64 stage[kTile];
   __shared__ u32 start[kChunksPerSb];
   __shared__ u32 wsum[kSplitThreads / 64];
@@ -494,9 +602,14 @@ __device__ __forceinline__ void split_compact_part(Cols in, Cols out, u32* __res
     const u32 k = threadIdx.x + j * kSplitThreads;
     rk[j] = k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u;
   }
-  __syncthreads();
+  // a chunk with >= kHeavyRun records in this part (a hot group): the dedup
+  // pass below (rare; block-uniform)
+  // (needs the group terms to class what it folds: the step entry points
+  // pass them, the bucket-only one does not)
+  const bool heavy = __syncthreads_or(threadIdx.x < kChunksPerSb && side.group_term &&
+                                      start[threadIdx.x] >= kHeavyRun);
   tile_scan_bins(start, kChunksPerSb, wsum);
-  if (threadIdx.x <= kChunksPerSb)
+  if (!heavy && threadIdx.x <= kChunksPerSb)
     cs[row * (kChunksPerSb + 1) + threadIdx.x] =
         lo + (threadIdx.x < kChunksPerSb ? start[threadIdx.x] : nrec);
 #pragma unroll
@@ -505,18 +618,25 @@ __device__ __forceinline__ void split_compact_part(Cols in, Cols out, u32* __res
     if (k < nrec) stage[start[vc[j]] + rk[j]] = vm[j];
   }
   __syncthreads();
+  if (heavy) {
+    dedup_compact_part(geo, out, cs, lo, nrec, row, sb, side, stage, start, wsum);
+    return;
+  }
   for (u32 e = threadIdx.x; e < nrec; e += kSplitThreads) out.mr[lo + e] = stage[e];
 }
 
-__global__ __launch_bounds__(kSplitThreads) void k_bk_split_compact(
+// (the dedup path's registers would otherwise cost the common path its
+// residency: 70 VGPRs / 102 SGPRs unbounded, 56 / 75 without the path)
+__global__ __launch_bounds__(kSplitThreads)
+__attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_split_compact(
     Geometry geo, const u32* __restrict__ counts, Cols in, Cols out, u32* __restrict__ cs,
-    Pool pool, u32 kparts) {
+    Pool pool, u32 kparts, Side side) {
   // part p = region r's j-th kTile records (the region grid, qb_bucket.h),
   // then the overflow pool's parts
-  u32 lo, nrec;
+  u32 lo, nrec, sb;
   u64 row;
-  if (k4_item<false>(geo, pool, counts, kparts, lo, nrec, row))
-    split_compact_part(in, out, cs, lo, nrec, row);
+  if (k4_item<false>(geo, pool, counts, kparts, lo, nrec, row, sb))
+    split_compact_part(geo, in, out, cs, lo, nrec, row, sb, side);
 }
 
 // ---------------------------------------------------------------- K5 ----
@@ -541,14 +661,14 @@ __host__ __device__ constexpr u32 k5_block(int n) {
 // SGPRs held K5 at 3 workgroups per CU where its VGPRs and LDS allow 4;
 // capped at 80 (a few SGPRs spill to VGPR lanes): -11 us per 16M-group tick.
 template <int N, bool NEXT, bool MANY>
-__global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) void k_bk_apply(
-    Geometry geo, Cols recs, const u32* __restrict__ counts, const u32* __restrict__ cs,
-    const u64* __restrict__ rec_index, const u64* __restrict__ rec_term,
+__device__ __forceinline__ void apply_chunk(
+    const u32 c, const bool skip_heavy, const Geometry& geo, const Cols& recs,
+    const u32* __restrict__ counts, const u32* __restrict__ cs, const EscArgs& esc,
     const u64* __restrict__ group_term, const u64* __restrict__ term_start,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
     u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
     u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards,
-    const u32* __restrict__ ptab) {
+    const u32* __restrict__ ptab, const HeavyArgs& hv) {
   constexpr u32 CH = chunk_groups(N);
   constexpr u32 B = k5_block(N);
   constexpr u32 GPT = CH / B;  // groups per thread in the commit phase
@@ -559,9 +679,6 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   __shared__ u64 gterm[CH];
   __shared__ u32 act[CH];
   __shared__ u32 slow;
-  // Chunks in reverse order: K4 wrote the last super-buckets last, so their
-  // runs are the ones still in the 256 MB MALL when K5 starts.
-  const u32 c = gridDim.x - 1u - blockIdx.x;
   const u64 g0 = u64(c) * CH;
   const u32 ng = u32(geo.G - g0 < CH ? geo.G - g0 : CH);
   // Load order: the group terms and this chunk's run table first, then the
@@ -576,6 +693,13 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   // a record of this chunk that did not fit its reserved region (K3): the
   // whole chunk goes to the slow path
   const bool overflow = chunk_slow[c] == kChunkOverflow;
+  // (the linear order's workgroup of a chunk the leading workgroups take:
+  // its super-bucket is among the first hv.blocks / 128 heavy ones — read
+  // with the run table's loads, tested once the table is built)
+  const u32 hf = skip_heavy ? hv.sbflag[sb] : 0u;
+  const bool heavy_sb = hf != 0u && hf - 1u < hv.blocks / kChunksPerSb;
+  // the records K4's dedup folded away (stale, applied, rejected)
+  const u32 extv = esc.side.ext[u64(c) * kExtClasses + (threadIdx.x & 3u)];
   u64 gtr[GPT];
 #pragma unroll
   for (u32 k = 0; k < GPT; ++k) {
@@ -613,6 +737,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   // loaded before the first is classified.
   u32 total = rt.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
   __syncthreads();
+  if (heavy_sb) return;  // block-uniform: the heavy workgroups apply this chunk
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
@@ -636,11 +761,9 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
         const u64 x = rec[r];
         const u32 lg = fmt.lg(x), s = fmt.slot(x);
         u64 t = fmt.term(x), idx = fmt.payload(x);
-        if (t == fmt.tesc()) {  // escape: the exact values from the batch
-          const u32 ridx = u32(idx);
-          idx = rec_index[ridx];
-          t = rec_term[ridx];
-        }
+        // escape: the exact values from the batch, or a folded record's from
+        // the side table
+        if (t == fmt.tesc()) unescape(esc, t, idx);
         const u64 gt = gterm[lg];
         if (t > gt) {
           slow = 1;  // higher term: step-down order (raft.go:875-879)
@@ -699,6 +822,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   // published after it (a flush with barriers of its own at the end cost
   // 15 us per 16M-group tick)
   tally.stage(tl);
+  if (threadIdx.x < 3 && extv) atomicAdd(&tl[threadIdx.x], extv);  // K4's folded records
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
 #pragma unroll
@@ -747,8 +871,38 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
   }
 }
 
+template <int N, bool NEXT, bool MANY>
+__global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) void k_bk_apply(
+    Geometry geo, Cols recs, const u32* __restrict__ counts, const u32* __restrict__ cs,
+    EscArgs esc, const u64* __restrict__ group_term, const u64* __restrict__ term_start,
+    u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
+    u64* __restrict__ committed, u32* __restrict__ stepdown_at, u8* __restrict__ advanced,
+    u8* __restrict__ chunk_slow, u32* __restrict__ any_slow, u64* __restrict__ shards,
+    const u32* __restrict__ ptab, HeavyArgs hv) {
+  // One chunk per workgroup, one call site (a second call site or a loop
+  // over chunks doubled the body's registers): the leading hv.blocks
+  // workgroups take chunk i % 128 of the i / 128-th heavy super-bucket (the
+  // first hv.blocks / 128 of them; later ones stay in the linear order), the
+  // rest the chunks in reverse order — K4 wrote the last super-buckets last,
+  // so their runs are the ones still in the 256 MB MALL when K5 starts.
+  u32 c;
+  const bool lead = blockIdx.x < hv.blocks;
+  if (lead) {
+    const u32 i = blockIdx.x;
+    if (i >= *hv.nheavy * kChunksPerSb) return;  // (all of them in a balanced batch)
+    c = geo.chunk_of_sb_cl(hv.heavy[i / kChunksPerSb], i % kChunksPerSb);
+    if (c >= geo.NC) return;
+  } else {
+    c = geo.NC - 1u - (blockIdx.x - hv.blocks);
+  }
+  apply_chunk<N, NEXT, MANY>(c, !lead, geo, recs, counts, cs, esc, group_term, term_start, match,
+                             next, active, committed, stepdown_at, advanced, chunk_slow, any_slow,
+                             shards, ptab, hv);
+}
+
 struct ApplyArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
+  Side side;           // K4's folded records
   const u64 *gt, *ts;
   u64 *match, *next;
   u16* active;
@@ -759,19 +913,22 @@ struct ApplyArgs {
   u32* any_slow;
   u64* stats;
   const u32* ptab;  // the overflow pool's part table
+  HeavyArgs hv;
 };
 
 template <int N, bool MANY>
 void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                        const ApplyArgs& a, hipStream_t st) {
+  const EscArgs esc{a.ri, a.rt, a.side};
+  const dim3 grid(a.hv.blocks + geo.NC);
   if (a.next)
-    hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
-                       counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab);
+    hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), grid, dim3(k5_block(N)), 0, st, geo, recs, counts,
+                       cs, esc, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown,
+                       a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab, a.hv);
   else
-    hipLaunchKernelGGL((k_bk_apply<N, false, MANY>), dim3(geo.NC), dim3(k5_block(N)), 0, st, geo, recs,
-                       counts, cs, a.ri, a.rt, a.gt, a.ts, a.match, a.next, a.active, a.committed,
-                       a.stepdown, a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab);
+    hipLaunchKernelGGL((k_bk_apply<N, false, MANY>), grid, dim3(k5_block(N)), 0, st, geo, recs, counts,
+                       cs, esc, a.gt, a.ts, a.match, a.next, a.active, a.committed, a.stepdown,
+                       a.adv, a.chunk_slow, a.any_slow, a.stats, a.ptab, a.hv);
 }
 template <int N>
 void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
@@ -813,7 +970,7 @@ namespace bk {
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
-                   hipStream_t st, bool compact) {
+                   hipStream_t st, bool compact, const u64* group_term, const u32* csr_off) {
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
   u8* chunk_flags = reinterpret_cast<u8*>(ws + cv.chunk_flags);
@@ -841,7 +998,7 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
                        buf1, counts, shards, chunk_flags, pool);
     QB_CHECK_LAUNCH("k_bk_scatter");
     hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts + pblocks), dim3(kSplitThreads), 0, st, geo,
-                       counts, buf1, buf2, cs, pool, kparts);
+                       counts, buf1, buf2, cs, pool, kparts, side_at(ws, cv, group_term, csr_off));
     QB_CHECK_LAUNCH("k_bk_split_compact");
     return QB_OK;
   }
@@ -892,11 +1049,14 @@ int fixed_tracker_check(uint32_t n, uint64_t G, uint64_t M, const void* workspac
 }
 }  // namespace
 
-extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
-                                           const uint32_t* rec_group, const uint8_t* rec_flags,
-                                           const uint64_t* rec_index, const uint64_t* rec_term,
-                                           void* workspace, size_t workspace_bytes,
-                                           void* stream) {
+namespace {
+// The bucket half; group_term (nullable) lets K4 fold a hot group's records
+// (the dedup needs the group terms to class what it folds away): the step
+// passes it, the bucket-only entry point cannot.
+int fixed_bucket(uint32_t n, uint64_t G, uint64_t M, const uint32_t* rec_group,
+                 const uint8_t* rec_flags, const uint64_t* rec_index, const uint64_t* rec_term,
+                 const uint64_t* group_term, void* workspace, size_t workspace_bytes,
+                 void* stream) {
   if (G == 0) return QB_OK;
   QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
              "record pointer is NULL");
@@ -909,7 +1069,17 @@ extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
   return bk::bucket_records(geo, cv, ws, rec_group, rec_flags, reinterpret_cast<const u64*>(rec_index),
                             reinterpret_cast<const u64*>(rec_term),
                             reinterpret_cast<u64*>(ws + cv.shards), as_stream(stream),
-                            /*compact=*/true);
+                            /*compact=*/true, reinterpret_cast<const u64*>(group_term));
+}
+}  // namespace
+
+extern "C" int qb_dev_fixed_tracker_bucket(uint32_t n, uint64_t G, uint64_t M,
+                                           const uint32_t* rec_group, const uint8_t* rec_flags,
+                                           const uint64_t* rec_index, const uint64_t* rec_term,
+                                           void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  return fixed_bucket(n, G, M, rec_group, rec_flags, rec_index, rec_term, nullptr, workspace,
+                      workspace_bytes, stream);
 }
 
 extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
@@ -939,8 +1109,10 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
+  const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::ApplyArgs a{reinterpret_cast<const u64*>(rec_index),
                         reinterpret_cast<const u64*>(rec_term),
+                        bk::side_at(ws, cv),
                         reinterpret_cast<const u64*>(group_term),
                         reinterpret_cast<const u64*>(term_start),
                         reinterpret_cast<u64*>(match),
@@ -952,7 +1124,9 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
                         reinterpret_cast<u8*>(ws + cv.chunk_flags),
                         reinterpret_cast<u32*>(ws + cv.flags),
                         shards,
-                        reinterpret_cast<const u32*>(ws + cv.ptab)};
+                        reinterpret_cast<const u32*>(ws + cv.ptab),
+                        bk::HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
+                                      geo.NC < bk::kHeavyBlocks ? geo.NC : bk::kHeavyBlocks}};
   bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, counts, cs, a,
                      st);
   QB_CHECK_LAUNCH("k_bk_apply");
@@ -976,8 +1150,8 @@ extern "C" int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
   if (G == 0) return QB_OK;
   QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
              "required state pointer is NULL");
-  const int rc = qb_dev_fixed_tracker_bucket(n, G, M, rec_group, rec_flags, rec_index, rec_term,
-                                             workspace, workspace_bytes, stream);
+  const int rc = fixed_bucket(n, G, M, rec_group, rec_flags, rec_index, rec_term, group_term,
+                              workspace, workspace_bytes, stream);
   if (rc != QB_OK) return rc;
   return qb_dev_fixed_tracker_apply(n, G, M, rec_group, rec_flags, rec_index, rec_term, group_term,
                                     term_start, match, next, active, committed, stepdown_at,

@@ -50,20 +50,21 @@ constexpr u8 kChunkDeferred = 2;  // chunk_slow value: run too long for the firs
 // CAPW: LDS slots per group; SECOND: the launch for the deferred chunks.
 #define QB_CSR_APPLY_PARAMS                                                                      \
   Geometry geo, Cols recs, const u32 *__restrict__ counts, const u32 *__restrict__ cs,            \
-      const u64 *__restrict__ rec_index, const u64 *__restrict__ rec_term,                        \
+      EscArgs esc,                                                                                 \
       const u32 *__restrict__ off, const u32 *__restrict__ cfg,                                   \
       const u64 *__restrict__ group_term, const u64 *__restrict__ term_start,                     \
       u64 *__restrict__ match, u64 *__restrict__ next, u16 *__restrict__ active,                  \
       u64 *__restrict__ committed, u32 *__restrict__ stepdown_at, u8 *__restrict__ advanced,      \
       u8 *__restrict__ chunk_slow, u32 *__restrict__ any_slow, u64 *__restrict__ shards,          \
-      const u32 *__restrict__ ptab
+      const u32 *__restrict__ ptab, HeavyArgs hv
 #define QB_CSR_APPLY_ARGS                                                                      \
-  geo, recs, counts, cs, rec_index, rec_term, off, cfg, group_term, term_start, match, next, active, committed,          \
-      stepdown_at, advanced, chunk_slow, any_slow, shards, ptab
+  geo, recs, counts, cs, esc, off, cfg, group_term, term_start, match, next, active, committed,  \
+      stepdown_at, advanced, chunk_slow, any_slow, shards, ptab, hv
 
 // One chunk c (the whole workgroup).
 template <int WMAX, int CAPW, bool NEXT, bool SECOND, bool MANY>
-__device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS) {
+__device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_heavy,
+                                                QB_CSR_APPLY_PARAMS) {
   constexpr u32 CH = csr_chunk_groups(WMAX);
   constexpr u32 B = csr_block();
   constexpr u32 GPT = CH / B;          // groups per thread in the commit phase
@@ -86,6 +87,12 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   // a record of this chunk that did not fit its reserved region (K3): the
   // whole chunk goes to the slow path (checked before any deferral)
   const bool overflow = chunk_slow[c] == kChunkOverflow;
+  // (the linear order's workgroup of a chunk the leading workgroups take:
+  // see k_bk_apply; read with the first loads, tested once the table is built)
+  const u32 hf = skip_heavy ? hv.sbflag[sb] : 0u;
+  const bool heavy_sb = hf != 0u && hf - 1u < hv.blocks / kChunksPerSb;
+  // the records K4's dedup folded away (stale, applied, rejected, non-member)
+  const u32 extv = esc.side.ext[u64(c) * kExtClasses + (threadIdx.x & 3u)];
   // Load order: (1) slot offsets, group terms and the run table's rows (the
   // part table by scalar load); (2) the old slot run and the commit inputs;
   // (3) the records.  Vector loads retire in order, so each wait of the
@@ -161,6 +168,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   // second launch) only a table breaking its max_slots bound gets here, and
   // the chunk takes the slow path (exact per-record semantics, global
   // atomics) — no chunk is left deferred without a launch to apply it.
+  if (heavy_sb) return;  // block-uniform: a leading workgroup applies this chunk
   if constexpr (!SECOND && CAPW < WMAX) {
     if (!fits && !overflow) {  // block-uniform, before anything is written
       if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
@@ -169,16 +177,6 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
   u32 total = rtab.template finish<MANY>(rq, cs, counts, sb, geo.ppx, geo.cap, cl);
   __syncthreads();
-  // records in the overflow pool: applied by the launch that carries the
-  // pool loop (below); the first launch defers the chunk to it, before
-  // anything is written (block-uniform: rtab.npool is published)
-  constexpr bool kPoolHere = SECOND || CAPW >= WMAX;
-  if constexpr (!kPoolHere) {
-    if (rtab.npool && !overflow) {
-      if (threadIdx.x == 0) chunk_slow[c] = kChunkDeferred;
-      return;
-    }
-  }
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
@@ -205,11 +203,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
           non = true;                                     // no Progress: raft.go:1100-1104
         } else {
           u64 t = fmt.term(x), idx = fmt.payload(x);
-          if (t == fmt.tesc()) {  // escape: the exact values from the batch
-            const u32 ridx = u32(idx);
-            idx = rec_index[ridx];
-            t = rec_term[ridx];
-          }
+          // escape: the exact values from the batch, or a folded record's
+          // from the side table
+          if (t == fmt.tesc()) unescape(esc, t, idx);
           u64 gt = gterm[lg];
           if (gt == 0xFFFFFFFFull) gt = group_term[g0 + lg];  // (terms past 32 bits)
           if (t > gt) {
@@ -245,26 +241,22 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
     apply(f0, total);
   }
   // The chunk's records in the overflow pool (a skewed batch; none
-  // otherwise): windows of 64 pool rows through the same table.  Only the
-  // instantiation that applies deferred chunks (or has no second launch)
-  // carries this loop: it cost the first launch 14 VGPRs (occupancy 8 -> 7),
-  // so that launch defers a chunk with pool rows (above).
-  if constexpr (kPoolHere) {
-    for (u32 w = 0; w * 64u < rtab.npool; ++w) {  // block-uniform (LDS, published before)
-      __syncthreads();  // every reader of the previous table is done
-      if (threadIdx.x < 64) rtab.pool_window(w, cs, ptab, geo.kmax, geo.region_rows(), sb, cl);
-      __syncthreads();
-      const u32 tot = rtab.pre[rtab.nr];
-      for (u32 f0 = 0; f0 < tot; f0 += B * kRecPer) {
-        load(f0, tot);
+  // otherwise): windows of 64 pool rows through the same table.
+  for (u32 w = 0; w * 64u < rtab.npool; ++w) {  // block-uniform (LDS, published before)
+    __syncthreads();  // every reader of the previous table is done
+    if (threadIdx.x < 64) rtab.pool_window(w, cs, ptab, geo.kmax, geo.region_rows(), sb, cl);
+    __syncthreads();
+    const u32 tot = rtab.pre[rtab.nr];
+    for (u32 f0 = 0; f0 < tot; f0 += B * kRecPer) {
+      load(f0, tot);
 #pragma unroll
-        for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
-        apply(f0, tot);
-      }
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+      apply(f0, tot);
     }
   }
   if (!fits && threadIdx.x == 0) slow = 1;
   tally.stage(tl);  // the counts are final; published after the barrier
+  if (threadIdx.x < 4 && extv) atomicAdd(&tl[threadIdx.x], extv);  // K4's folded records
   __syncthreads();
   if (slow) {  // block-uniform: state left for k_bk_slow, counts discarded
     for (u32 lg = threadIdx.x; lg < ng; lg += B) stepdown_at[g0 + lg] = 0xFFFFFFFFu;
@@ -325,10 +317,22 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, QB_CSR_APPLY_PARAMS
   }
 }
 
+// One chunk per workgroup: the leading hv.blocks workgroups take the heavy
+// super-buckets' chunks (k_bk_apply), the rest the linear order.
 template <int WMAX, int CAPW, bool NEXT, bool MANY>
 __global__ __launch_bounds__(csr_block()) __attribute__((amdgpu_num_sgpr(80))) void k_csr_apply(
     QB_CSR_APPLY_PARAMS) {
-  csr_apply_chunk<WMAX, CAPW, NEXT, false, MANY>(blockIdx.x, QB_CSR_APPLY_ARGS);
+  u32 c;
+  const bool lead = blockIdx.x < hv.blocks;
+  if (lead) {
+    const u32 i = blockIdx.x;
+    if (i >= *hv.nheavy * kChunksPerSb) return;  // (all of them in a balanced batch)
+    c = geo.chunk_of_sb_cl(hv.heavy[i / kChunksPerSb], i % kChunksPerSb);
+    if (c >= geo.NC) return;
+  } else {
+    c = blockIdx.x - hv.blocks;
+  }
+  csr_apply_chunk<WMAX, CAPW, NEXT, false, MANY>(c, !lead, QB_CSR_APPLY_ARGS);
 }
 
 // The deferred chunks: a workgroup per kDeferSpan consecutive chunks reads
@@ -348,12 +352,14 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY
   __syncthreads();
   for (u64 m = mask; m; m &= m - 1) {  // block-uniform
     __syncthreads();  // the previous chunk's readers of the LDS state are done
-    csr_apply_chunk<WMAX, CAPW, NEXT, true, MANY>(c0 + u32(__builtin_ctzll(m)), QB_CSR_APPLY_ARGS);
+    csr_apply_chunk<WMAX, CAPW, NEXT, true, MANY>(c0 + u32(__builtin_ctzll(m)), false,
+                                                  QB_CSR_APPLY_ARGS);
   }
 }
 
 struct CsrStepArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
+  Side side;           // K4's folded records
   const u32 *off, *cfg;
   const u64 *gt, *ts;
   u64 *match, *next;
@@ -365,20 +371,22 @@ struct CsrStepArgs {
   u32* any_slow;
   u64* shards;
   const u32* ptab;  // the overflow pool's part table
+  HeavyArgs hv;
 };
 
 template <int WMAX, bool SECOND, bool MANY>
 void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                        const CsrStepArgs& a, hipStream_t st) {
   constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
-  const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : geo.NC);
+  const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : a.hv.blocks + geo.NC);
+  const EscArgs esc{a.ri, a.rt, a.side};
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX, MANY>                        \
                              : k_csr_apply<WMAX, CAPW, NX, MANY>),                                 \
-                     grid, dim3(csr_block()), 0, st, geo, recs, counts, cs, a.ri, a.rt, a.off, a.cfg, \
+                     grid, dim3(csr_block()), 0, st, geo, recs, counts, cs, esc, a.off, a.cfg,     \
                      a.gt, a.ts,                                                                   \
                      a.match, a.next, a.active, a.committed, a.stepdown, a.adv, a.chunk_slow,      \
-                     a.any_slow, a.shards, a.ptab)
+                     a.any_slow, a.shards, a.ptab, a.hv)
   if (a.next) QB_CSR_LAUNCH(true);
   else QB_CSR_LAUNCH(false);
 #undef QB_CSR_LAUNCH
@@ -461,11 +469,14 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
   {
     const int rc = bk::bucket_records(geo, cv, ws, rec_group, rec_flags, ri, rtm, shards, st,
-                                      /*compact=*/true);
+                                      /*compact=*/true, reinterpret_cast<const u64*>(group_term),
+                                      off);
     if (rc != QB_OK) return rc;
   }
+  const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::CsrStepArgs a{ri,
                           rtm,
+                          bk::side_at(ws, cv),
                           off,
                           cfg,
                           reinterpret_cast<const u64*>(group_term),
@@ -479,7 +490,9 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
                           reinterpret_cast<u8*>(ws + cv.chunk_flags),
                           reinterpret_cast<u32*>(ws + cv.flags),
                           shards,
-                          reinterpret_cast<const u32*>(ws + cv.ptab)};
+                          reinterpret_cast<const u32*>(ws + cv.ptab),
+                          bk::HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
+                                        geo.NC < bk::kHeavyBlocks ? geo.NC : bk::kHeavyBlocks}};
   const bk::SlowArgs sa{rec_group, rec_flags, ri, rtm, reinterpret_cast<u32*>(ws + cv.flags) + 16,
                         bk::slow_blocks()};
   u64* stt = reinterpret_cast<u64*>(stats);

@@ -15,6 +15,41 @@
 namespace qb {
 namespace bk {
 
+// The heavy super-buckets' chunks (a region of theirs overflowed into the
+// pool: K3's list) are applied first, by the first kHeavyBlocks workgroups
+// of the apply grid (one chunk each: the first 8 heavy super-buckets), so
+// their long record passes overlap the other chunks instead of trailing them
+// (the reverse chunk order put the chunks of super-bucket 0 last: a 30 %
+// skew on it measured 838 us per tick with the pool alone); the workgroup
+// that would have taken such a chunk in the linear order returns once it has
+// read its super-bucket's flag.
+constexpr u32 kHeavyBlocks = 1024;
+struct HeavyArgs {
+  const u32* sbflag;
+  const u32* heavy;
+  const u32* nheavy;
+  u32 blocks;  // leading workgroups of the grid that take the heavy chunks
+};
+// K4's folded records (kDedupFlag) and the escapes: the exact index and term
+// — the side table or the original batch.
+struct EscArgs {
+  const u64 *ri, *rt;  // the original batch
+  Side side;
+};
+// (A folded record counts once here; K4 added the records it folded away to
+// the chunk's ext counters by class, which K5 adds unless the chunk is slow.)
+__device__ __forceinline__ void unescape(const EscArgs& e, u64& t, u64& idx) {
+  if (idx & kDedupFlag) {
+    const u64 si = idx & (kDedupFlag - 1ull);
+    idx = e.side.idx[si];
+    t = e.side.tc[si] & ((1u << kDedupCountShift) - 1u);
+  } else {
+    const u32 ridx = u32(idx);
+    idx = e.ri[ridx];
+    t = e.rt[ridx];
+  }
+}
+
 // Counters of block b go to shard b % kShards (QB_STAT_COUNT u64 each, one
 // cache line), folded into the caller's stats by k_stats_fold.
 __device__ __forceinline__ u64* shard_of(u64* shards) {

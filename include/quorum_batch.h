@@ -327,7 +327,9 @@ int qb_dev_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M,
 
 /* qb_dev_fixed_tracker_step in two halves, for a caller that pipelines
  * ticks: _bucket sorts a batch by group into a workspace (reads only the
- * batch: K3-K4, no leader state), _apply applies that workspace's batch to
+ * batch: K3-K4, no leader state — so, unlike the step, it does not fold a
+ * hot group's repeated records, which needs the group terms), _apply
+ * applies that workspace's batch to
  * the state (K5 + the exact slow path; the same batch pointers, which the
  * slow path re-reads).  step == bucket then apply on one stream.  With two
  * workspaces on two streams, tick k+1's bucketing can run while tick k is

@@ -474,3 +474,54 @@ def test_step_dense_batch_many_parts_per_region():
     want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
                      "bad_group", "after_stepdown"), stats.tolist()))
     assert {k: got[k] for k in want} == want
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("higher", [0.0, 0.0005])
+def test_step_hot_groups_fold_in_k4(higher):
+    """Hot groups: 35 % of 2M records on one group and 15 % on eight more,
+    the rest uniform over 1M groups — their chunks' runs in a K4 part pass
+    kHeavyRun, so K4 folds records with equal lg | slot | reject | term into
+    one (side table, counts classed into the chunk's ext counters by the
+    group term) and their super-buckets' regions overflow into the pool
+    (heavy chunks applied by the leading workgroups).  Hot records include
+    stale terms, rejects, terms past the compact field (escapes, never
+    folded; the state's 1 % of groups above 2^63 escape by index); with
+    `higher`, some chunks go to the slow
+    path and must not count their folded records twice.  State and every
+    stat counter equal the sequential oracle's."""
+    n, G, M = 5, 1 << 20, 1 << 21
+    rng = np.random.default_rng(81)
+    st = _random_state(rng, n, G)
+    st["term"][:] = np.where(rng.random(G) < 0.5, 9, 5000).astype(np.uint64)  # > 2047: escapes
+    tr = _tracker_from(n, st, track_next=False)
+    st.pop("next")
+    group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, st, higher=higher,
+                                                         reject=0.05, stale=0.05)
+    hot = rng.permutation(G)[:9].astype(np.uint32)
+    u = rng.random(M)
+    pick = np.where(u < 0.35, 0, np.where(u < 0.5, 1 + rng.integers(0, 8, size=M), -1))
+    group = np.where(pick >= 0, hot[np.maximum(pick, 0)], group).astype(np.uint32)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 4000, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    v = rng.random(M)
+    term = st["term"][group] - (v < 0.05).astype(np.uint64) + (v > 1 - higher).astype(np.uint64)
+    stats = oc.appresp_sequential(n, G, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    _compare(tr, st, n, G)
+    got = tr.stats_dict()
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert {k: got[k] for k in want} == want
+    # the same batch again on the same tracker (the workspace reused: ext
+    # counters, side table, pool and heavy list start over; nothing raised;
+    # the caller re-arms the groups that stepped down)
+    st["stepped_down"][:] = 0
+    stats = oc.appresp_sequential(n, G, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    _compare(tr, st, n, G)
+    got = tr.stats_dict()
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert {k: got[k] for k in want} == want

@@ -460,3 +460,37 @@ def test_csr_step_dense_batch_many_parts_per_region():
     want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
                      "bad_group", "after_stepdown"), stats.tolist()))
     assert tr.stats_dict() == want
+
+
+@pytest.mark.timeout(300)
+def test_csr_step_hot_groups_fold_in_k4():
+    """The CSR step with hot groups (40 % of 2M records on one group, 15 % on
+    eight more): K4 folds their repeated records, classing what it folds by
+    the group term and, for a slot past the group's count, as non-member —
+    state and every stat counter equal the sequential oracle's."""
+    G, M = 1 << 20, 1 << 21
+    rng = np.random.default_rng(79)
+    off, cfg, sizes, st = _state(rng, "ragged", G)
+    st.pop("next")
+    tr = _tracker(off, cfg, st, track_next=False)
+    group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, higher=0.0002)
+    hot = rng.permutation(G)[:9].astype(np.uint32)
+    u = rng.random(M)
+    pick = np.where(u < 0.4, 0, np.where(u < 0.55, 1 + rng.integers(0, 8, size=M), -1))
+    group = np.where(pick >= 0, hot[np.maximum(pick, 0)], group).astype(np.uint32)
+    s_g = sizes[group]
+    # slots up to s_g + 1: the last is no member (a non-member slot, folded too)
+    slot = (rng.integers(0, 1 << 30, size=M) % (s_g + 1)).astype(np.uint8)
+    last = st["last_index"][group]
+    lag = rng.integers(0, 4000, size=M).astype(np.uint64)
+    index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
+    v = rng.random(M)
+    term = st["term"][group] - (v < 0.05).astype(np.uint64)
+    rej = rng.random(M) < 0.05
+    flags = (slot | (rej.astype(np.uint8) << 7)).astype(np.uint8)
+    stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), st, threads=16)
+    tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+    _compare(tr, st, G)
+    want = dict(zip(("applied", "rejected", "stale_term", "non_member", "higher_term",
+                     "bad_group", "after_stepdown"), stats.tolist()))
+    assert tr.stats_dict() == want
