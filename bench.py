@@ -1304,7 +1304,9 @@ def next_rows():
     """SURVEY §8f rows and configs[0] (tools/bench_configs.py, GPU side only:
     one device time per row) for the default run's line: the leader inbox
     step (4M groups), ReadIndex acks (4M leaders), wire ingest (16M messages,
-    group-row table), a conf change over 8M groups, and the configs[0]
+    group-row table), a conf change over 8M groups, the composed wire ->
+    tracker tick (16M groups, 16M encoded MsgAppResp per tick; its own
+    decode + state parity in the row), and the configs[0]
     plumbing (the faithful C restatement's ns/op beside the device's ns per
     group).  Their parity is the GPU suite's (tests/test_gpu_leader.py,
     test_gpu_wire.py, test_gpu_confchange.py: bit-exact vs the oracles)."""
@@ -1322,7 +1324,8 @@ def next_rows():
     for name, fn in (("leader", lambda: bc.leader_config(1 << 22, 20, **kw)),
                      ("readindex", lambda: bc.readindex_config(1 << 22, 20, **kw)),
                      ("wire", lambda: bc.wire_config(1 << 24, 20, rows=True, **kw)),
-                     ("confchange", lambda: bc.confchange_config(1 << 23, 20, **kw))):
+                     ("confchange", lambda: bc.confchange_config(1 << 23, 20, **kw)),
+                     ("wire-tracker", lambda: bc.wire_tracker_config(1 << 24, 10, **kw))):
         try:
             fn()
         except Exception as ex:  # reported; the headline stands

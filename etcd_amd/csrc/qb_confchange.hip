@@ -20,8 +20,11 @@
 //
 // Per group (one thread): the old slots and the changes are replayed on a
 // small working table in LDS (IDs + role bitmasks over table entries), then
-// the surviving entries are sorted by ID into the new slots.  Two passes
-// (count, then write after a scan of the counts) recompute the same replay.
+// the surviving entries are sorted by ID into the new slots.  The count pass
+// replays and orders each group and leaves a slot code word (which old slot
+// or change entry each new slot comes from); after a scan of the counts the
+// placement pass writes the new slots from the codes without a replay (round
+// 4 replayed twice: count, then write).
 //
 // Table size (round 3): the replay is latency-bound and its occupancy is set
 // by the table's LDS (24 entries x 8 B x 128 threads = 24 KB per workgroup:
@@ -83,6 +86,7 @@ struct Args {
   u8* err;
   u64* err_id;
   u32* any_big;  // workspace word: a group needs the kTab table
+  u64* codes;    // workspace [G]: each group's slot codes (k_cc_count -> k_cc_move)
 };
 
 // A group's table can exceed kSmall entries only when its old slots plus its
@@ -128,9 +132,13 @@ __device__ int check_invariants(const Tab& t, const Roles& r, bool autoleave, u6
 // Replays group g's operation.  On success fills the table/roles of the new
 // config and returns 0; otherwise an error code (the table then holds the
 // old config).  Roles.fresh marks entries whose Progress is (re)created.
+// chg (kSmall tables only): for an entry the change list created, the index
+// within the list of the change that last (re)created it, four bits per entry
+// (a kSmall group has at most 8 changes), so the placement pass can read the
+// entry's ID without a replay.
 template <int TAB>
 __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autoleave, u64* bad,
-                      int* n_old) {
+                      int* n_old, u32* chg = nullptr) {
   const u32 s0 = A.off[g], s1 = A.off[g + 1];
   const u32 ns = s1 - s0;
   const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
@@ -205,6 +213,8 @@ __device__ int replay(const Args& A, u64 g, const Tab& t, Roles& r, bool& autole
             r.in &= b, r.out &= b, r.lnext &= b, r.lrn &= b, r.islrn &= b, r.fresh &= b;
           }
           t.id(x) = id;
+          if constexpr (TAB <= 8)
+            if (chg) *chg = (*chg & ~(0xFu << (4 * x))) | ((k - k0) << (4 * x));
         }
         const u32 b = 1u << x;
         r.prs |= b;
@@ -285,84 +295,34 @@ __device__ __forceinline__ void for_my_groups(const Args& A, F&& f) {
   }
 }
 
-template <int TAB, bool BIG>
-__global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
-  __shared__ u64 tabs[TAB][kBlk];
-  for_my_groups<BIG>(A, [&](u64 g) {
-    Tab t = tab_of(tabs);
-    Roles r;
-    bool al;
-    u64 bad = 0;
-    int n_old;
-    const int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
-    A.new_cnt[g] = rc ? u32(n_old) : u32(__popc(r.prs));
-    A.err[g] = u8(rc);
-    if (A.err_id) A.err_id[g] = rc ? bad : 0;
-  });
-}
-
-// The per-group pass only stores: new IDs, masks, and initProgress for fresh
-// slots.  A carried slot (checkAndCopy's shallow copy) is marked in the new
-// pstate (kCarried, never a valid QB_PR_* byte) with its old slot index in
-// the new infl_pos; k_cc_copy then moves the Progress row and ring with one
-// thread per new slot and overwrites both.  Keeping the copy out of the
-// replay kernel keeps that kernel's LDS to the working tables (occupancy) and
-// gives the byte moving a full-occupancy streaming launch of its own.
+// Markers (the kTab groups' write pass): a carried slot (checkAndCopy's
+// shallow copy) is marked in the new pstate (kCarried, never a valid QB_PR_*
+// byte) with its old slot index in the new infl_pos, a fresh slot
+// (initProgress) kFresh with its group; k_cc_move reads them and writes the
+// Progress row and ring.  Keeping the copy out of the replay kernels keeps
+// their LDS to the working tables (occupancy) and gives the byte moving a
+// full-occupancy streaming launch of its own.
 constexpr u8 kCarried = 0xFF;
-// A fresh slot (initProgress) is marked kFresh with its group in the new
-// infl_pos; k_cc_copy materialises it.  So every new slot's row is written
-// by the copy kernel, whole lines per wave (round 2: the write pass storing
-// fresh rows itself left scattered partial lines; 2565 -> 2220 us).
 constexpr u8 kFresh = 0xFE;
 
-template <int TAB>
-__device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
-  Tab t = tab_of(tabs);
-  Roles r;
-  bool al;
-  u64 bad = 0;
-  int n_old;
-  int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
-  const u32 s0 = A.off[g];
-  // the group's offset: its local prefix plus its scan block's sum (round 4:
-  // the scan's add-back pass folded here, which also stores the offset);
-  // its end from its own count (the next group's entry may already hold its
-  // final offset)
-  const u64 d0 = u64(A.new_cnt[g]) + A.nbsum[g / scan::kScanPer];
-  const u64 d1 = d0 + (rc ? u32(n_old) : u32(__popc(r.prs)));
-  A.new_cnt[g] = u32(d0);
-  if (d1 > A.S_cap) return;  // the caller's capacity is exceeded (reported by new_off[G])
-  if (rc) {  // the old config is kept
-    r = Roles{};
-    r.n = n_old;
-    r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
-    const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
-    r.in = c & 0xFFFFu;
-    r.out = c >> 16;
-    r.lnext = e & 0xFFFFu;
-    al = (e >> 16) & 1u;
-  }
-  u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
-  auto emit = [&](u32 j, int best) {
-    const u32 b = 1u << best;
-    if (r.in & b) ncfg_in |= 1u << j;
-    if (r.out & b) ncfg_out |= 1u << j;
-    if (r.lnext & b) nlnext |= 1u << j;
-    const u64 d = d0 + j;
-    const bool carried = best < n_old && !(r.fresh & b);
-    A.n_ids[d] = t.id(best);
-    if (carried) {  // carried Progress: k_cc_copy
-      A.n_pstate[d] = kCarried;
-      A.n_infl_pos[d] = s0 + u32(best);
-    } else {  // initProgress (confchange.go:258-281): materialised by k_cc_copy
-      A.n_pstate[d] = kFresh;
-      A.n_infl_pos[d] = u32(g);
-    }
-  };
-  // Surviving entries in ascending ID order.  The old slots are already
-  // ascending (the CSR slot order) and the appended entries few, so they are
-  // merged (one LDS read per output); an input table that is not ascending
-  // takes the selection over all entries instead.
+// A failed change keeps the old config: its roles, read back from cfg / ext.
+__device__ __forceinline__ void kept_roles(const Args& A, u64 g, int n_old, Roles& r, bool& al) {
+  r = Roles{};
+  r.n = n_old;
+  r.prs = n_old >= 32 ? ~0u : ((1u << n_old) - 1u);
+  const u32 c = A.cfg[g], e = A.ext ? A.ext[g] : 0u;
+  r.in = c & 0xFFFFu;
+  r.out = c >> 16;
+  r.lnext = e & 0xFFFFu;
+  al = (e >> 16) & 1u;
+}
+
+// The surviving entries in ascending ID order: emit(j, entry) for the new
+// slot j.  The old slots are already ascending (the CSR slot order) and the
+// appended entries few, so they are merged (one LDS read per output); an
+// input table that is not ascending takes the selection over all entries.
+template <class E>
+__device__ __forceinline__ void order_out(const Tab& t, const Roles& r, int n_old, E&& emit) {
   bool asc = true;
   {
     u64 prev = 0;
@@ -414,60 +374,275 @@ __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
       emit(j, best);
     }
   }
+}
+
+// Slot codes (round 5).  The kSmall count pass orders the new slots itself
+// and leaves one byte per new slot (8 per group, 0xFF past the last) in the
+// workspace, with the new cfg / ext written directly: the placement pass
+// (k_cc_move) then needs no replay — it reads the code word, the group's
+// offset and the IDs the codes name.  Code: bits 0-3 the entry's source (an
+// old slot index, or with kCodeAppended the change list index that created
+// it), kCodeFresh an initProgress slot.
+constexpr u8 kCodeAppended = 0x10, kCodeFresh = 0x20, kCodeNone = 0xFF;
+// A kTab group's code word: kBigCode | its slot count (k_cc_write places it
+// and leaves markers, as round 4 did for every group).
+constexpr u64 kBigCode = 0xFEull << 56;
+
+template <int TAB, bool BIG>
+__global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
+  __shared__ u64 tabs[TAB][kBlk];
+  for_my_groups<BIG>(A, [&](u64 g) {
+    Tab t = tab_of(tabs);
+    Roles r;
+    bool al;
+    u64 bad = 0;
+    int n_old;
+    u32 chg = 0;
+    const int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old, BIG ? nullptr : &chg);
+    A.new_cnt[g] = rc ? u32(n_old) : u32(__popc(r.prs));
+    A.err[g] = u8(rc);
+    if (A.err_id) A.err_id[g] = rc ? bad : 0;
+    if constexpr (BIG) {
+      A.codes[g] = kBigCode | (rc ? u32(n_old) : u32(__popc(r.prs)));  // (k_cc_move reads its markers)
+    } else {
+      if (rc) kept_roles(A, g, n_old, r, al);
+      u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
+      u64 code = ~0ull;  // kCodeNone in every byte
+      order_out(t, r, n_old, [&](u32 j, int best) {
+        const u32 b = 1u << best;
+        if (r.in & b) ncfg_in |= 1u << j;
+        if (r.out & b) ncfg_out |= 1u << j;
+        if (r.lnext & b) nlnext |= 1u << j;
+        u32 c;
+        if (best < n_old) c = u32(best) | ((r.fresh & b) ? kCodeFresh : 0u);
+        else c = ((chg >> (4 * best)) & 0xFu) | kCodeAppended | kCodeFresh;
+        code = (code & ~(0xFFull << (8 * j))) | (u64(c) << (8 * j));
+      });
+      A.codes[g] = code;
+      A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
+      A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
+    }
+  });
+}
+
+// The kTab groups (old slots + changes > kSmall; grid-strided, none at all in
+// the usual batch): the write pass replays the change again.
+template <int TAB>
+__device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
+  Tab t = tab_of(tabs);
+  Roles r;
+  bool al;
+  u64 bad = 0;
+  int n_old;
+  int rc = replay<TAB>(A, g, t, r, al, &bad, &n_old);
+  const u32 s0 = A.off[g];
+  // the group's offset: its local prefix plus its scan block's sum (round 4:
+  // the scan's add-back pass folded here, which also stores the offset);
+  // its end from its own count (the next group's entry may already hold its
+  // final offset)
+  const u64 d0 = u64(A.new_cnt[g]) + A.nbsum[g / scan::kScanPer];
+  const u64 d1 = d0 + (rc ? u32(n_old) : u32(__popc(r.prs)));
+  A.new_cnt[g] = u32(d0);
+  if (d1 > A.S_cap) return;  // the caller's capacity is exceeded (reported by new_off[G])
+  if (rc) kept_roles(A, g, n_old, r, al);
+  u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
+  order_out(t, r, n_old, [&](u32 j, int best) {
+    const u32 b = 1u << best;
+    if (r.in & b) ncfg_in |= 1u << j;
+    if (r.out & b) ncfg_out |= 1u << j;
+    if (r.lnext & b) nlnext |= 1u << j;
+    const u64 d = d0 + j;
+    const bool carried = best < n_old && !(r.fresh & b);
+    A.n_ids[d] = t.id(best);
+    if (carried) {  // carried Progress: k_cc_move
+      A.n_pstate[d] = kCarried;
+      A.n_infl_pos[d] = s0 + u32(best);
+    } else {  // initProgress (confchange.go:258-281): materialised by k_cc_move
+      A.n_pstate[d] = kFresh;
+      A.n_infl_pos[d] = u32(g);
+    }
+  });
   A.n_cfg[g] = ncfg_in | (ncfg_out << 16);
   A.n_ext[g] = nlnext | (al ? 1u << 16 : 0u);
 }
 
-template <int TAB, bool BIG>
+template <int TAB>
 __global__ __launch_bounds__(kBlk) void k_cc_write(Args A) {
   __shared__ u64 tabs[TAB][kBlk];
-  for_my_groups<BIG>(A, [&](u64 g) { write_group<TAB>(A, g, tabs); });
+  for_my_groups<true>(A, [&](u64 g) { write_group<TAB>(A, g, tabs); });
 }
 
-// One thread per new slot d < min(new_off[G], S_cap), grid-stride: a carried
-// slot's match / next / pendingSnapshot / inflight position / state byte and
-// its ring come from the old slot; a fresh slot's ring is zeroed.  A slot of
-// a group past the capacity was never written: the source bound keeps any
-// stale marker from reading outside the old arrays.
-__global__ __launch_bounds__(256) void k_cc_copy(Args A) {
-  const u64 total = A.new_cnt[A.G];
-  const u64 end = total < A.S_cap ? total : A.S_cap;
+// Placement and copy in one pass (round 5; round 4 wrote each new slot's ID
+// and a marker from a per-group thread — 64 lanes storing 6-slot runs, partial
+// lines — and a per-slot copy kernel read the markers back).  A wave takes 64
+// consecutive groups: each lane its group's offset (stored as new_off[g]),
+// count and code word, staged in LDS with the owner lane of every slot of the
+// wave's range; then the wave walks the range [D0, D1) one slot per lane, two
+// slots per lane at a time (both slots' loads issued before either's stores:
+// the outputs could alias the inputs as far as the compiler knows), and
+// writes ID, Progress row and ring with whole-line stores.  A kTab group
+// (k_cc_write placed it and left markers) is read from its markers.  A group
+// past the caller's capacity is not written.
+constexpr u32 kMoveSpan = 64 * QB_MAX_SLOTS;  // slots of a wave's 64 groups, at most
+struct MoveStage {
+  u32 d0[4][64];
+  u32 s0[4][64];
+  u32 k0[4][64];
+  u64 code[4][64];
+  u8 owner[4][kMoveSpan];
+};
+// One slot's sources (resolved from LDS) and values (loaded).
+struct Mv {
+  bool write, ok, fresh, marker;
+  u32 src, p;
+  u64 id, m, nx, ps, r[4];
+  u32 ip;
+  u8 st;
+};
+__global__ __launch_bounds__(256) void k_cc_move(Args A) {
+  __shared__ MoveStage ms;
+  const u32 w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const u64 g0 = (u64(blockIdx.x) * 4 + w) * 64;
+  const u64 g = g0 + lane;
+  const bool live = g < A.G;
+  u64 code = 0;
+  u32 d0 = 0, n = 0, s0 = 0, k0 = 0;
+  if (live) {
+    code = A.codes[g];
+    s0 = A.off[g];
+    k0 = A.cc_off[g];
+    if ((code & (0xFFull << 56)) == kBigCode) {
+      n = u32(code);
+      d0 = A.new_cnt[g];  // (k_cc_write stored the final offset)
+    } else {
+      const u64 none = code & 0x8080808080808080ull;  // kCodeNone bytes (a code is < 0x80)
+      n = none ? u32(__builtin_ctzll(none)) / 8 : 8u;
+      d0 = A.new_cnt[g] + A.nbsum[g / scan::kScanPer];
+      A.new_cnt[g] = d0;
+    }
+  }
+  // the wave's slot range [D0, dlast); lanes past G: empty groups at its end
+  const u32 nlive = g0 >= A.G ? 0u : u32(A.G - g0 < 64 ? A.G - g0 : 64);
+  const u32 dlast = nlive ? u32(__shfl(int(d0 + n), int(nlive - 1), 64)) : 0u;
+  const u32 D0 = u32(__shfl(int(d0), 0, 64));
+  if (!live) {
+    d0 = dlast;
+    n = 0;
+  }
+  ms.d0[w][lane] = d0;
+  ms.s0[w][lane] = s0;
+  ms.k0[w][lane] = k0;
+  ms.code[w][lane] = code;
+  // the owner lane of every slot of the range (a new config has at most
+  // QB_MAX_SLOTS slots; a failed change keeps its old slots, and a wave whose
+  // range exceeds the table finds its owners by a binary search instead)
+  const bool wide = dlast - D0 > kMoveSpan;  // (wave-uniform)
+  if (!wide)
+    for (u32 j = 0; j < n; ++j) ms.owner[w][d0 - D0 + j] = u8(lane);
+  __syncthreads();
+  const u64 cap = A.S_cap;
   const u32 old_total = A.off[A.G];
   const u32 K = A.K;
-  for (u64 d = u64(blockIdx.x) * 256 + threadIdx.x; d < end; d += u64(gridDim.x) * 256) {
-    const u8 mk = A.n_pstate[d];
-    const bool carried = mk == kCarried, fresh = mk == kFresh;
-    const u32 src = carried || fresh ? A.n_infl_pos[d] : 0u;
-    const bool ok = carried && src < old_total;
-    if (ok) {
-      const u64 m = A.match[src], nx = A.next[src], ps = A.psnap[src];
-      const u32 ip = A.infl_pos[src];
-      const u8 st = A.pstate[src];
-      A.n_match[d] = m;
-      A.n_next[d] = nx;
-      A.n_psnap[d] = ps;
-      A.n_infl_pos[d] = ip;
-      A.n_pstate[d] = st;
-    } else if (fresh) {  // initProgress (confchange.go:258-281); src = the group
+  auto resolve = [&](u32 p, Mv& v) {
+    v.write = false;
+    v.marker = false;
+    v.p = p;
+    if (p >= dlast) return;
+    u32 q = 0;
+    if (!wide) {
+      q = ms.owner[w][p - D0];
+    } else {  // the last lane whose offset is <= p
+#pragma unroll
+      for (u32 step = 32; step; step >>= 1)
+        if (ms.d0[w][q + step] <= p) q += step;
+    }
+    const u64 c = ms.code[w][q];
+    const u32 qd0 = ms.d0[w][q];
+    if ((c & (0xFFull << 56)) == kBigCode) {
+      if (u64(qd0) + u32(c) > cap) return;  // past the capacity: not written
+      v.write = true;
+      v.marker = true;  // (sources from k_cc_write's markers, below)
+      return;
+    }
+    const u64 none = c & 0x8080808080808080ull;
+    const u32 cn = none ? u32(__builtin_ctzll(none)) / 8 : 8u;
+    if (u64(qd0) + cn > cap) return;  // past the capacity: not written
+    const u32 b = u32(c >> (8 * (p - qd0))) & 0xFFu, sl = b & 0xFu;
+    v.write = true;
+    v.fresh = (b & kCodeFresh) != 0;
+    v.src = v.fresh ? u32(g0 + q) : ms.s0[w][q] + sl;
+    v.ok = !v.fresh && v.src < old_total;
+    // the ID's position, in the ID field until the loads
+    v.id = (b & kCodeAppended) ? (1ull << 63) | (ms.k0[w][q] + sl) : u64(ms.s0[w][q] + sl);
+  };
+  auto load = [&](Mv& v) {
+    if (!v.write) return;
+    if (v.marker) {  // a kTab group's slot: k_cc_write stored its ID and marker
+      const u8 mk = A.n_pstate[v.p];
+      v.src = A.n_infl_pos[v.p];
+      v.fresh = mk == kFresh;
+      v.ok = mk == kCarried && v.src < old_total;
+    } else {
+      v.id = (v.id >> 63) ? A.cc_node[u32(v.id)] : A.ids[u32(v.id)];
+    }
+    if (v.ok) {
+      v.m = A.match[v.src];
+      v.nx = A.next[v.src];
+      v.ps = A.psnap[v.src];
+      v.ip = A.infl_pos[v.src];
+      v.st = A.pstate[v.src];
+    } else if (v.fresh) {
+      v.nx = A.last_index[v.src];
+    }
+    if (K <= 4) {
+      const u64* sr = A.infl_buf + u64(v.src) * K;
+#pragma unroll
+      for (u32 k = 0; k < 4; ++k) v.r[k] = (v.ok && k < K) ? sr[k] : 0ull;
+    }
+  };
+  auto store = [&](const Mv& v) {
+    if (!v.write) return;
+    const u64 d = v.p;
+    if (!v.marker) A.n_ids[d] = v.id;
+    if (v.ok) {
+      A.n_match[d] = v.m;
+      A.n_next[d] = v.nx;
+      A.n_psnap[d] = v.ps;
+      A.n_infl_pos[d] = v.ip;
+      A.n_pstate[d] = v.st;
+    } else if (v.fresh) {  // initProgress (confchange.go:258-281)
       A.n_match[d] = 0;
-      A.n_next[d] = A.last_index[src];
+      A.n_next[d] = v.nx;
       A.n_psnap[d] = 0;
       A.n_infl_pos[d] = 0;
       A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
     }
-    if (K) {
-      const u64* sr = A.infl_buf + u64(src) * K;
-      u64* dr = A.n_infl_buf + d * K;
+    u64* dr = A.n_infl_buf + d * K;
+    if (K <= 4) {
+#pragma unroll
+      for (u32 k = 0; k < 4; ++k)
+        if (k < K) dr[k] = v.r[k];
+    } else {
+      const u64* sr = A.infl_buf + u64(v.src) * K;
       u32 k = 0;
       for (; k + 4 <= K; k += 4) {
-        u64 v[4];
+        u64 x[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = ok ? sr[k + q] : 0ull;
+        for (int q = 0; q < 4; ++q) x[q] = v.ok ? sr[k + q] : 0ull;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dr[k + q] = v[q];
+        for (int q = 0; q < 4; ++q) dr[k + q] = x[q];
       }
-      for (; k < K; ++k) dr[k] = ok ? sr[k] : 0ull;
+      for (; k < K; ++k) dr[k] = v.ok ? sr[k] : 0ull;
     }
+  };
+  for (u32 p = D0 + lane; p < dlast; p += 128) {
+    Mv a, b;
+    resolve(p, a);
+    resolve(p + 64, b);
+    load(a);
+    load(b);
+    store(a);
+    store(b);
   }
 }
 
@@ -476,9 +651,13 @@ __global__ __launch_bounds__(256) void k_cc_copy(Args A) {
 
 using namespace qb;
 
+namespace {
+// the scan's block sums, the any_big word, the slot codes
+size_t cc_codes_at(uint64_t G) { return ((scan::blocks(G) + 1) * sizeof(u32) + 255) / 256 * 256 + 256; }
+}  // namespace
+
 extern "C" size_t qb_conf_change_workspace_bytes(uint64_t G) {
-  // the scan's block sums, then the any_big word
-  return (scan::blocks(G) + 1) * sizeof(u32) + 256 + 256;
+  return cc_codes_at(G) + G * sizeof(u64) + 256;
 }
 
 extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_change_out* out,
@@ -532,6 +711,7 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
   hipStream_t st = as_stream(stream);
   const size_t scan_bytes = (scan::blocks(G) + 1) * sizeof(u32);
   A.any_big = reinterpret_cast<u32*>(static_cast<char*>(workspace) + (scan_bytes + 255) / 256 * 256);
+  A.codes = reinterpret_cast<u64*>(static_cast<char*>(workspace) + cc_codes_at(G));
   {
     const hipError_t e = hipMemsetAsync(A.any_big, 0, sizeof(u32), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(any_big)");
@@ -549,10 +729,9 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
     A.nbsum = bsum;
   }
   QB_CHECK_LAUNCH("scan(conf change)");
-  hipLaunchKernelGGL((cc::k_cc_write<cc::kSmall, false>), dim3(grid), dim3(cc::kBlk), 0, st, A);
-  hipLaunchKernelGGL((cc::k_cc_write<cc::kTab, true>), dim3(big_grid), dim3(cc::kBlk), 0, st, A);
+  hipLaunchKernelGGL(cc::k_cc_write<cc::kTab>, dim3(big_grid), dim3(cc::kBlk), 0, st, A);
   QB_CHECK_LAUNCH("k_cc_write");
-  hipLaunchKernelGGL(cc::k_cc_copy, dim3(2048), dim3(256), 0, st, A);
-  QB_CHECK_LAUNCH("k_cc_copy");
+  hipLaunchKernelGGL(cc::k_cc_move, dim3(unsigned((G + 255) / 256)), dim3(256), 0, st, A);
+  QB_CHECK_LAUNCH("k_cc_move");
   return QB_OK;
 }

@@ -574,6 +574,7 @@ struct Group {
   u32 mask_in, mask_out;
   u32 meta;
   u64 term, committed;
+  u64 first, last;      // the log view's first / last index (requested with the group's fields)
   u32 nruns;
   u32 nmsg, stored;     // messages generated / stored (the pool can run out)
   u32 chunk;            // current overflow chunk
@@ -583,9 +584,12 @@ struct Group {
 __device__ __forceinline__ u32 leader_slot(const Group& G_) { return G_.meta & 0xFFu; }
 // Read-only log-view fields are re-read where used (L1 hits) instead of being
 // held in registers for the whole step: this kernel is latency-bound and its
-// occupancy is set by its VGPR count.
-#define LG_FIRST(A, G_) U((A).lg.first_index)[(G_).g]
-#define LG_LAST(A, G_) U((A).lg.last_index)[(G_).g]
+// occupancy is set by its VGPR count.  First / last index are the exception
+// (round 5): requested with the group's fields, before the slot stage's
+// barrier, so the commit check's log_term and the first MsgApp do not wait
+// on a round trip of their own (118 VGPRs: still 4 waves per SIMD).
+#define LG_FIRST(A, G_) ((G_).first)
+#define LG_LAST(A, G_) ((G_).last)
 #define LG_SNAP_I(A, G_) U((A).lg.snap_index)[(G_).g]
 #define LG_SNAP_T(A, G_) U((A).lg.snap_term)[(G_).g]
 #define LG_MAX_ENTS(A, G_) U((A).lg.max_ents)[(G_).g]
@@ -1063,7 +1067,8 @@ struct StepCounts {
 // of every workgroup.
 struct Pre {
   u32 cfg, meta, f0;
-  u64 term, committed, t0;
+  u64 term, committed, t0, i0;
+  u64 first, last;  // the log view's first / last index (held by Group)
 };
 template <bool S>
 __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1, u32 s0, u32 s1, u32 sb,
@@ -1079,6 +1084,8 @@ __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1,
   G_.meta = pre.meta;
   G_.term = pre.term;
   G_.committed = pre.committed;
+  G_.first = pre.first;
+  G_.last = pre.last;
   G_.nruns = (G_.meta >> 16) & 0xFu;
   G_.nmsg = 0;
   G_.stored = 0;
@@ -1112,9 +1119,9 @@ __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1,
     if (kind == QB_IN_APP_RESP) {
       const u64 hint = reject ? A.rec.hint[k] : 0;
       const u64 ht = reject ? A.rec.log_term[k] : 0;
-      app_resp<S>(A, G_, slot, p, A.rec.index[k], reject, hint, ht, gfl);
+      app_resp<S>(A, G_, slot, p, k == r0 ? pre.i0 : A.rec.index[k], reject, hint, ht, gfl);
     } else if (kind == QB_IN_HEARTBEAT_RESP) {
-      heartbeat_resp<S>(A, G_, slot, p, A.rec.index[k]);
+      heartbeat_resp<S>(A, G_, slot, p, k == r0 ? pre.i0 : A.rec.index[k]);
     } else if (kind == QB_IN_SNAP_STATUS) {
       snap_status(p, reject);
     } else if (st_state(p.st()) == QB_PR_REPLICATE) {  // MsgUnreachable
@@ -1167,6 +1174,9 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
     pre.committed = A.lg.committed[g];
     pre.t0 = A.rec.term[r0];
     pre.f0 = A.rec.flags[r0];
+    pre.i0 = A.rec.index[r0];
+    pre.first = U(A.lg.first_index)[g];
+    pre.last = U(A.lg.last_index)[g];
   }
   SlotStage& ss = slot_stage();
   if (staged) {

@@ -96,9 +96,10 @@ class ConfigTable:
         return out
 
     def change(self, op: Sequence[int], ccs: Sequence[Sequence[Tuple[int, int]]],
-               last_index: Sequence[int]):
+               last_index: Sequence[int], out=None):
         """Apply op[g] with ccs[g] = [(ConfChangeType, NodeID), ...] to every
-        group; returns (new ConfigTable, err u8[G], err_id u64[G])."""
+        group; returns (new ConfigTable, err u8[G], err_id u64[G]).  ``out``:
+        as ``change_soa``."""
         G = self.G
         cc_off = np.zeros(G + 1, np.uint32)
         cc_off[1:] = np.cumsum([len(c) for c in ccs])
@@ -106,12 +107,14 @@ class ConfigTable:
         return self.change_soa(np.asarray(op, np.uint8), cc_off,
                                np.array([t for t, _ in flat], np.uint8),
                                np.array([n for _, n in flat], np.uint64),
-                               np.asarray(last_index, np.uint64))
+                               np.asarray(last_index, np.uint64), out=out)
 
-    def change_soa(self, op, cc_off, cc_type, cc_node, last_index, fetch_errors=True):
+    def change_soa(self, op, cc_off, cc_type, cc_node, last_index, fetch_errors=True, out=None):
         """As ``change`` with the operation already in SoA form (numpy arrays
         or device tensors): op[G] u8, cc_off[G+1] u32, cc_type / cc_node per
-        change, last_index[G] u64."""
+        change, last_index[G] u64.  ``out`` (optional): caller-owned output
+        tensors (the keys below; per-slot arrays of equal length = the slot
+        capacity, infl_buf capacity x K)."""
         dev = self.t["off"].device
         G = self.G
 
@@ -134,6 +137,9 @@ class ConfigTable:
              "infl_buf": torch.empty(max(1, cap * K), dtype=torch.int64, device=dev),
              "err": torch.empty(G, dtype=torch.uint8, device=dev),
              "err_id": torch.empty(G, dtype=torch.int64, device=dev)}
+        if out is not None:
+            o = out
+            cap = o["ids"].numel()
         i = _In(G=G, inflight_cap=K, reserved=0)
         for k, v in (("op", d_op), ("cc_off", d_ccoff), ("cc_type", d_cct), ("cc_node", d_ccn),
                      ("last_index", d_last)):

@@ -140,3 +140,43 @@ def synth_response_stream(M: int, G: int, seed: int = 0x5EED0008, hb_frac: float
     ss = np.tile(np.arange(5, dtype=np.uint64), G)
     ids = np.uint64(16384) + ss * np.uint64(200000) + (gg % np.uint64(100000))
     return buf, moff, grp, off, ids
+
+
+def _dev_varint(v: torch.Tensor, n: int) -> list:
+    """Varint bytes (exactly n) of an int64 device tensor, one u8 column each."""
+    cols = []
+    for k in range(n):
+        b = (v >> (7 * k)) & 0x7F
+        if k < n - 1:
+            b = b | 0x80
+        cols.append(b.to(torch.uint8))
+    return cols
+
+
+def encode_appresp(to: torch.Tensor, frm: torch.Tensor, term: torch.Tensor,
+                   index: torch.Tensor, reject: torch.Tensor):
+    """Device-side gogoproto encoding of M MsgAppResp messages with one fixed
+    layout (raft.pb.go Message.Marshal field order: Type, To, From, Term,
+    LogTerm 0, Index, Commit 0, the empty non-nullable Snapshot, Reject,
+    RejectHint 0) — the composed wire -> tracker workload's generator.  Node
+    IDs and terms must need 3-byte varints ([2^14, 2^21)), indexes 6-byte
+    ones ([2^35, 2^42)).  Returns (bytes u8, nbytes, msg_off int64 [M+1])."""
+    lo, hi = 1 << 14, 1 << 21
+    for t, what, a, b in ((to, "to", lo, hi), (frm, "frm", lo, hi), (term, "term", lo, hi),
+                          (index, "index", 1 << 35, 1 << 42)):
+        if t.numel() and (int(t.min()) < a or int(t.max()) >= b):
+            raise ValueError(f"encode_appresp: {what} outside [{a}, {b})")
+    M = to.numel()
+    dev = to.device
+
+    def col(byte):
+        return torch.full((M,), byte, dtype=torch.uint8, device=dev)
+    cols = [col(0x08), col(4), col(0x10), *_dev_varint(to, 3), col(0x18), *_dev_varint(frm, 3),
+            col(0x20), *_dev_varint(term, 3), col(0x28), col(0), col(0x30),
+            *_dev_varint(index, 6), col(0x40), col(0), col(0x4A), col(len(_EMPTY_SNAPSHOT))]
+    cols += [col(b) for b in _EMPTY_SNAPSHOT]
+    cols += [col(0x50), reject.to(torch.uint8), col(0x58), col(0)]
+    L = len(cols)
+    buf = torch.stack(cols, dim=1).reshape(-1)
+    moff = torch.arange(M + 1, dtype=torch.int64, device=dev) * L
+    return buf, M * L, moff

@@ -105,7 +105,7 @@ def test_default_run_secondary_configs_wiring():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_configs as bc
     for name, nargs in (("leader_config", 2), ("readindex_config", 2), ("wire_config", 2),
-                        ("confchange_config", 2)):
+                        ("confchange_config", 2), ("wire_tracker_config", 2)):
         sig = inspect.signature(getattr(bc, name))
         required = [p for p in sig.parameters.values() if p.default is inspect.Parameter.empty]
         assert len(required) == nargs, name

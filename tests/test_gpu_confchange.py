@@ -193,3 +193,72 @@ def test_quick_simple_equals_joint_on_device():
             assert _render(a[g]) == _render(b[g]), g
     want = [_render(_simple_chain(base[g], inputs[g][1])) for g in range(G)]
     assert [_render(x) for x in CP.unpack(t1.numpy(), 10)] == want
+
+
+@pytest.mark.parametrize("short", [1, 7, 0.5])
+def test_short_capacity_writes_nothing_past_it(short):
+    """qb_dev_conf_change with slot_cap below new_off[G] (include/
+    quorum_batch.h: nothing past the capacity is written): new_off, err and
+    cfg equal a full-capacity call's, every group that fits is placed exactly
+    (IDs, Progress rows, rings), and no per-slot entry at or past slot_cap
+    changes (the outputs are sentinel-filled)."""
+    import torch
+    from etcd_amd import _lib
+    r = random.Random(21)
+    G, K = 700, 4
+    orc = [CC.Tracker.empty(K) for _ in range(G)]
+    table = _table(orc, K=K)
+    for _ in range(2):  # a populated start
+        op = [CP.random_op(r, t) for t in orc]
+        ccs = [CP.random_ccs(r) for _ in orc]
+        last = [r.randint(0, 1000) for _ in orc]
+        table, _, _ = table.change(op, ccs, last)
+        orc = [CP.oracle_apply(t, o_, c, l)[0] for t, o_, c, l in zip(orc, op, ccs, last)]
+    op = [CP.random_op(r, t) for t in orc]
+    ccs = [CP.random_ccs(r) for _ in orc]
+    last = [r.randint(0, 1000) for _ in orc]
+    full, err_f, _ = table.change(op, ccs, last)
+    ref = full.numpy()
+    S_new = int(ref["off"][G])
+    cap = max(1, int(S_new * short)) if isinstance(short, float) else S_new - short
+    dev = table.t["off"].device
+    sent = {"ids": -7, "match": -7, "next": -7, "pending_snapshot": -7, "pstate": 0xAB,
+            "infl_pos": -7}
+    pad = 64
+    o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
+         "cfg": torch.empty(G, dtype=torch.int32, device=dev),
+         "ext": torch.empty(G, dtype=torch.int32, device=dev),
+         "err": torch.empty(G, dtype=torch.uint8, device=dev),
+         "err_id": torch.empty(G, dtype=torch.int64, device=dev)}
+    for k, dt in (("ids", torch.int64), ("match", torch.int64), ("next", torch.int64),
+                  ("pending_snapshot", torch.int64), ("pstate", torch.uint8),
+                  ("infl_pos", torch.int32)):
+        o[k] = torch.full((cap + pad,), sent[k], dtype=dt, device=dev)
+    o["infl_buf"] = torch.full(((cap + pad) * K,), -7, dtype=torch.int64, device=dev)
+    o_cap = dict(o)  # views of the first cap entries: the call's capacity
+    for k in sent:
+        o_cap[k] = o[k][:cap]
+    o_cap["infl_buf"] = o["infl_buf"][:cap * K]
+    with pytest.raises(_lib.QuorumBatchError):
+        table.change(op, ccs, last, out=o_cap)
+    torch.cuda.synchronize()
+    new_off = o["new_off"].cpu().numpy().view(np.uint32)
+    assert np.array_equal(new_off, ref["off"].astype(np.uint32))
+    assert np.array_equal(o["err"].cpu().numpy(), err_f)
+    okg = [g for g in range(G) if not err_f[g]]
+    assert np.array_equal(o["cfg"].cpu().numpy()[okg], ref["cfg"][okg])
+    h = {k: o[k].cpu().numpy() for k in list(sent) + ["infl_buf"]}
+    fits = 0
+    for g in range(G):
+        a, b = int(new_off[g]), int(new_off[g + 1])
+        if b > cap:
+            break
+        fits += 1
+        for k in sent:
+            assert np.array_equal(h[k][a:b], np.asarray(ref[k][a:b]).astype(h[k].dtype)), (g, k)
+        assert np.array_equal(h["infl_buf"][a * K:b * K],
+                              np.asarray(ref["infl_buf"][a * K:b * K]).astype(np.int64)), g
+    assert fits > 0
+    for k in sent:
+        assert (h[k][cap:] == np.array(sent[k]).astype(h[k].dtype)).all(), k
+    assert (h["infl_buf"][cap * K:] == -7).all()

@@ -124,3 +124,46 @@ def test_response_stream_full_size_vs_c_oracle(rows):
     assert np.array_equal(ib.flags.cpu().numpy(), want["flags"])
     for col in ("index", "term", "hint", "log_term"):
         assert np.array_equal(getattr(ib, col).cpu().numpy().view(np.uint64), want[col]), col
+
+
+def test_ingest_then_tracker_step_vs_c_oracles():
+    """The composed per-tick chain (bench next_rows "wire -> tracker tick"):
+    device-encoded MsgAppResp bytes, decoded by the device and by the C
+    restatement of Message.Unmarshal (oracle/wire_oracle.c); the device's
+    records through qb_dev_fixed_tracker_step over three ticks, against the
+    sequential C oracle of stepLeader's MsgAppResp case on the C decoder's
+    records: match, committed, active, stepped-down identical."""
+    import os
+    import sys
+    import torch
+    from etcd_amd.quorum import batch, wire
+    from tests import oracle_c as oc
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import bench_configs as bc
+    G, n = 1 << 16, 5
+    tr, snap, ticks, rows, off, ids = bc.wire_tracker_tick(G, 3, dev_=torch.device("cuda"))
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)
+    st = {"match": u64(tr.match).copy(), "active": tr.active.cpu().numpy().view(np.uint16)[:G].copy(),
+          "term": u64(tr.term).copy(), "term_start": u64(tr.term_start).copy(),
+          "committed": u64(tr.committed).copy(), "stepped_down": np.zeros(G, np.uint8)}
+    h_off = off.cpu().numpy().view(np.uint32)
+    h_ids = u64(ids)
+    for buf, nbytes, moff, grp, _direct in ticks:
+        ib, status, _ = wire.ingest(buf, nbytes, moff, grp, off, ids, rows=rows)
+        assert int(status.max().item()) == 0
+        want = oc.ingest(buf.cpu().numpy(), u64(moff), grp.cpu().numpy().view(np.uint32),
+                         h_off, h_ids, threads=8)
+        assert np.array_equal(ib.group.cpu().numpy().view(np.uint32), want["group"])
+        assert np.array_equal(ib.flags.cpu().numpy(), want["flags"])
+        assert np.array_equal(u64(ib.index), want["index"])
+        assert np.array_equal(u64(ib.term), want["term"])
+        tr.step(batch.AppRespBatch(ib.group, ib.flags, ib.index, ib.term))
+        oc.appresp_sequential(n, G, (want["group"], want["flags"], want["index"], want["term"]),
+                              st, threads=8)
+    assert np.array_equal(u64(tr.match), st["match"])
+    assert np.array_equal(u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    sd = tr.stepdown_at.cpu().numpy().view(np.uint32)
+    assert np.array_equal(sd != 0xFFFFFFFF, st["stepped_down"] != 0)
+    assert int((st["committed"] > 0).sum()) > G // 2  # commits advanced
