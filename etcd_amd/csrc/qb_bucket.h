@@ -36,9 +36,12 @@ constexpr int kShards = 256;         // stat counter shards (one 64-byte line ea
 // A record whose index >= 2^40 or whose term does not fit tb bits is an
 // escape: its term field is all ones and the index field holds the record's
 // batch position, from which K5 reads the exact index and term in the
-// original batch.  Raft indexes below 2^40 and terms below 1023 keep every
-// record in 8 bytes; an escape costs K5 two 8-byte gathers, never a wrong
-// answer.  (Round 2's packed form moved index + meta|term32, 16 bytes, four
+// original batch — or, in a K3 tile most of whose records escape (a stream
+// of terms >= 1023), kEscColumn | its buf1 position, where K3 wrote them in
+// the escape column (whole lines: the tile's runs).  Raft indexes below
+// 2^40 and terms below 1023 keep every record in 8 bytes; an escape costs K5
+// two 8-byte gathers (or one 16-byte read beside its neighbours), never a
+// wrong answer.  (Round 2's packed form moved index + meta|term32, 16 bytes, four
 // times per record: K3 write, K4 read + write, K5 read.)
 struct Cols {
   u64* index;
@@ -298,7 +301,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
 // zeroed by one memset per call (bucket_records).
 struct Carve {
   size_t shards, flags, counts, chunk_flags, ptab, sbflag, ext, user, zero_end, owner, heavy,
-      side_idx, side_tc, chunk_start, buf1, buf2, cl, total;
+      side_idx, side_tc, chunk_start, buf1, buf2, cl, esc, total;
   u64 nside;   // dedup side-table entries (compact form: kDedupSlots per chunk-start row)
   u64 nrec;    // records of the region grid (pool part 0 starts here)
   u64 nrec_all;  // records per column of buf1 / buf2: the region grid + the pool
@@ -325,6 +328,9 @@ constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions over
 constexpr u32 kHeavyRun = 512;
 constexpr u32 kDedupSlots = 256;
 constexpr u64 kDedupFlag = 1ull << 39;
+// An escape of an escape-dense K3 tile: payload = kEscColumn | its buf1
+// position, its exact index and term in the escape column there.
+constexpr u64 kEscColumn = 1ull << 38;
 constexpr u32 kDedupCountShift = 12;
 constexpr u32 kExtClasses = 4;  // stale, applied, rejected, non-member
 inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
@@ -359,6 +365,9 @@ inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   c.buf1 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.buf2 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.cl = o;  o += ncols == 1 ? up256(nrec) : 0;
+  // compact form: the escape column — an escape's exact (index, term) at its
+  // buf1 position, written by K3 for escape-dense tiles only
+  c.esc = o;  o += ncols == 1 ? up256(2 * sizeof(u64) * nrec) : 0;
   c.total = o;
   return c;
 }
@@ -400,9 +409,11 @@ inline Cols cols_at(char* base, u64 M, int ncols = 3) {
               reinterpret_cast<u64*>(base + 2 * col), nullptr, nullptr, 0};
 }
 // The compact form's columns: the u64 records at `base`, the chunk-low bytes
-// at `cl` (K3's output only; K4's output needs none).
-inline Cols compact_at(char* base, char* cl) {
-  return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u8*>(cl), 1};
+// at `cl` and the escape column at `esc` (K3's output only; K4's output needs
+// neither).
+inline Cols compact_at(char* base, char* cl, char* esc = nullptr) {
+  return Cols{reinterpret_cast<u64*>(esc), nullptr, reinterpret_cast<u64*>(base), nullptr,
+              reinterpret_cast<u8*>(cl), 1};
 }
 
 

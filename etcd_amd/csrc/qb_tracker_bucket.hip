@@ -138,8 +138,10 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   u32* pid0 = dyn + 2 * geo.NSB;  // NSB: pool parts of the run past the cap
   u32* pid1 = dyn + 3 * geo.NSB;
   __shared__ TileLds L;
+  __shared__ u32 s_nesc;  // compact: this tile's escapes
   const u32 tile = geo.tile();
   if (tile >= geo.NT) return;
+  if (threadIdx.x == 0) s_nesc = 0;  // (ordered before its use by the barriers below)
   const u64 t0 = u64(tile) * kTile;
   const u32 nrec = u32(geo.M - t0 < u64(kTile) ? geo.M - t0 : u64(kTile));
   u32 g[kPer], f[kPer];
@@ -252,6 +254,7 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   if constexpr (COMPACT) {
     // after the scan each record is stored at its sorted LDS slot with its
     // bin and chunk-low, and the output pass reads the slots in order
+    u32 mesc = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const u32 b = bj[j] & 0xFFFFu;
@@ -260,9 +263,43 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
       L.stage[e] = vj[j];
       L.bin[e] = u16(b);
       L.cl[e] = u8(bj[j] >> 16);
+      mesc += geo.fmt.term(vj[j]) == geo.fmt.tesc();
     }
+    if (mesc) atomicAdd(&s_nesc, mesc);
     __syncthreads();
     const u32 x = blockIdx.x % kRegionShards;
+    if (2 * s_nesc > nvalid) {  // (block-uniform)
+      // A tile most of whose records escape (terms past the record's term
+      // field, indexes >= 2^40): each escape's exact index and term go to
+      // the escape column at the record's own position — lines the tile's
+      // runs fill — read back from this tile's batch lines (L2 hits), and
+      // the record's payload becomes that position with kEscColumn.  K5
+      // then reads the pair beside the region's other records instead of
+      // two random gathers from the batch (a stream whose every term is
+      // >= 1023: 1053 -> ~810 us per 16M-record tick).  A tile of rare
+      // escapes keeps the batch position: scattered 16-byte column stores
+      // (partial lines) cost K3 and K5 ~20 us each at 1 % escapes.
+      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+        const u32 b = L.bin[e];
+        const u32 gs = gstart[b];
+        const u32 rel = gs + (e - start[b]);
+        const u64 d = rel < geo.cap ? u64(b * kRegionShards + x) * geo.cap + rel
+                                    : region_dst(geo, pool, b, x, rel, gs, pid0[b], pid1[b]);
+        if (d == ~0ull) {
+          chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
+          continue;
+        }
+        u64 v = L.stage[e];
+        if (geo.fmt.term(v) == geo.fmt.tesc()) {
+          const u32 bp = u32(v >> kRecHdrBits);
+          *reinterpret_cast<ulonglong2*>(out.index + 2 * d) = ulonglong2{ri[bp], rt[bp]};
+          v = (v & ((1ull << kRecHdrBits) - 1ull)) | ((d | kEscColumn) << kRecHdrBits);
+        }
+        out.mr[d] = v;
+        out.cl[d] = L.cl[e];
+      }
+      return;
+    }
     for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
       const u32 b = L.bin[e];
       const u32 gs = gstart[b];
@@ -642,7 +679,8 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_split_
 // ---------------------------------------------------------------- K5 ----
 // Records arrive compact (one u64 each, RecFmt: lg, slot, reject, term,
 // index; an escape record carries its batch position and K5 reads its exact
-// index and term from the original batch).  A chunk none of whose records is
+// index and term from the original batch — or, from an escape-dense K3 tile,
+// its buf1 position with kEscColumn and K5 reads them from the escape column).  A chunk none of whose records is
 // above its group's term (the steady state) is applied here.  A chunk with a
 // higher-term record (the sequential leader steps down there and ignores what
 // follows, raft.go:875-879: batch order matters) is "slow": K5 leaves its
@@ -902,6 +940,7 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
 
 struct ApplyArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
+  const u64* esc;      // the escape column (escapes of escape-dense K3 tiles)
   Side side;           // K4's folded records
   const u64 *gt, *ts;
   u64 *match, *next;
@@ -919,7 +958,7 @@ struct ApplyArgs {
 template <int N, bool MANY>
 void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                        const ApplyArgs& a, hipStream_t st) {
-  const EscArgs esc{a.ri, a.rt, a.side};
+  const EscArgs esc{a.ri, a.rt, a.esc, a.side};
   const dim3 grid(a.hv.blocks + geo.NC);
   if (a.next)
     hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), grid, dim3(k5_block(N)), 0, st, geo, recs, counts,
@@ -992,7 +1031,8 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   const unsigned pblocks = geo.npool;
   const Pool pool = pool_at(ws, cv, geo);
   if (compact) {
-    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl), buf2 = compact_at(ws + cv.buf2, nullptr);
+    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.esc),
+               buf2 = compact_at(ws + cv.buf2, nullptr);
     hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads),
                        4 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
                        buf1, counts, shards, chunk_flags, pool);
@@ -1112,6 +1152,7 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::ApplyArgs a{reinterpret_cast<const u64*>(rec_index),
                         reinterpret_cast<const u64*>(rec_term),
+                        reinterpret_cast<const u64*>(ws + cv.esc),
                         bk::side_at(ws, cv),
                         reinterpret_cast<const u64*>(group_term),
                         reinterpret_cast<const u64*>(term_start),

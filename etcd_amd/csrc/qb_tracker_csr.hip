@@ -359,6 +359,7 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY
 
 struct CsrStepArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
+  const u64* esc;      // the escape column (escapes of escape-dense K3 tiles)
   Side side;           // K4's folded records
   const u32 *off, *cfg;
   const u64 *gt, *ts;
@@ -379,7 +380,7 @@ void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const 
                        const CsrStepArgs& a, hipStream_t st) {
   constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : a.hv.blocks + geo.NC);
-  const EscArgs esc{a.ri, a.rt, a.side};
+  const EscArgs esc{a.ri, a.rt, a.esc, a.side};
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX, MANY>                        \
                              : k_csr_apply<WMAX, CAPW, NX, MANY>),                                 \
@@ -476,6 +477,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::CsrStepArgs a{ri,
                           rtm,
+                          reinterpret_cast<const u64*>(ws + cv.esc),
                           bk::side_at(ws, cv),
                           off,
                           cfg,

@@ -149,12 +149,13 @@ def test_appresp_then_commit_vs_sequential(mode, n, G, M, kw):
         seq["stepped_down"][:] = 0
 
 
-@pytest.mark.parametrize("term_base", [0xFFFFFFFF - 5, 1 << 40, (1 << 64) - 16])
+@pytest.mark.parametrize("term_base", [20000, 0xFFFFFFFF - 5, 1 << 40, (1 << 64) - 16])
 def test_step_wide_terms_vs_sequential(term_base):
-    """Terms around and past 2^32: the bucketed step carries the term as u32
-    with an escape to the original batch (qb_bucket.h: term_to32); group
-    terms straddle the escape value so equal / stale / higher records land on
-    both sides of it."""
+    """Terms past the compact record's term field (>= 1023: every record an
+    escape, so every K3 tile is escape-dense and writes the escape column),
+    around and past 2^32 (qb_bucket.h: term_to32); group terms straddle the
+    escape value so equal / stale / higher records land on both sides of
+    it."""
     n, G, M = 5, 70001, 70001
     rng = np.random.default_rng(term_base % 1000003)
     st = _random_state(rng, n, G, term_base)
@@ -163,6 +164,32 @@ def test_step_wide_terms_vs_sequential(term_base):
     for step in range(3):
         group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, stale=0.05,
                                                              higher=0.01)
+        stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
+        tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
+        _compare(tr, seq, n, G)
+        got = tr.stats_dict()
+        assert got["applied"] == stats[0] and got["stale_term"] == stats[2]
+        assert got["higher_term"] == stats[4] and got["after_stepdown"] == stats[6]
+        tr.stepdown_at.fill_(-1)
+        seq["stepped_down"][:] = 0
+
+
+@pytest.mark.parametrize("frac", [0.3, 0.5, 0.7])
+def test_step_mixed_escape_density(frac):
+    """A fraction of the groups at terms >= 1023 (their records escape): K3
+    tiles on both sides of the escape-dense threshold in one batch, so
+    escapes read from the batch and from the escape column meet in the same
+    chunks (qb_bucket.h kEscColumn)."""
+    n, G, M = 5, 70001, 140002
+    rng = np.random.default_rng(int(frac * 1000))
+    st = _random_state(rng, n, G)
+    hi = rng.random(G) < frac
+    st["term"] = np.where(hi, st["term"] + np.uint64(40000), st["term"]).astype(np.uint64)
+    tr = _tracker_from(n, st)
+    seq = {k: v.copy() for k, v in st.items()}
+    for step in range(3):
+        group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, seq, stale=0.05,
+                                                             higher=0.005)
         stats = oc.appresp_sequential(n, G, (group, flags, index, term), seq)
         tr.step(batch.AppRespBatch.from_numpy(group, slot, index, term, rej, device=DEV))
         _compare(tr, seq, n, G)

@@ -112,7 +112,7 @@ def test_csr_step_vs_sequential(kind, G, M, kw):
         seq["stepped_down"][:] = 0
 
 
-@pytest.mark.parametrize("term_base", [0xFFFFFFFF - 5, (1 << 64) - 16])
+@pytest.mark.parametrize("term_base", [20000, 0xFFFFFFFF - 5, (1 << 64) - 16])
 def test_csr_step_wide_terms(term_base):
     """Group terms straddling the u32 escape (qb_bucket.h term_to32)."""
     G = M = 20000
