@@ -1308,8 +1308,12 @@ def next_rows():
     tracker tick (16M groups, 16M encoded MsgAppResp per tick; its own
     decode + state parity in the row), and the configs[0]
     plumbing (the faithful C restatement's ns/op beside the device's ns per
-    group).  Their parity is the GPU suite's (tests/test_gpu_leader.py,
-    test_gpu_wire.py, test_gpu_confchange.py: bit-exact vs the oracles)."""
+    group).  Each row carries its own parity (round 5): the leader and
+    ReadIndex workloads at 256K groups through both output forms vs the C
+    oracle, the wire decode of all 16M messages vs the C decoder, the conf
+    change's whole result checked on the device, the composed row's decode
+    and state; the GPU suite covers the rest (tests/test_gpu_leader.py,
+    test_gpu_wire.py, test_gpu_confchange.py)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     import bench_configs as bc
     rows = []

@@ -370,6 +370,49 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
         raise AssertionError(f"wire -> tracker tick: {bad} mismatches")
 
 
+def leader_row_parity(kind, Gs=1 << 18):
+    """The row's own parity (bench next_rows): the same workload generator at
+    Gs groups through both entry points (the group-ordered array and the
+    outbox), every state array, message, step-down entry and group flag
+    against the C oracle (oracle/leader_oracle.c, the stepLeader loop one
+    record at a time); the streaming leader for two consecutive batches.
+    Returns "bit-exact" or the mismatching fields."""
+    from etcd_amd.quorum.leader import (readindex_inbox, streaming_inbox, synth_readindex,
+                                        synth_streaming)
+    from tests import oracle_c as oc
+    bad = []
+    for outbox in (False, True):
+        if kind == "leader":
+            lg, base = synth_streaming(Gs, device=dev)
+            inboxes = [streaming_inbox(Gs, base, k, device=dev) for k in range(2)]
+            Q, cap = 0, 6 * Gs
+        else:
+            lg, last_ctx, _ = synth_readindex(Gs, 4, device=dev)
+            inboxes = [readindex_inbox(Gs, last_ctx, device=dev)]
+            Q, cap = 4, 8 * Gs
+        host = {k: v.copy() for k, v in lg.numpy().items()}
+        for k, ib in enumerate(inboxes):
+            res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=cap)
+            rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
+                   "index": ib.index.cpu().numpy().view(np.uint64),
+                   "term": ib.term.cpu().numpy().view(np.uint64),
+                   "hint": ib.hint.cpu().numpy().view(np.uint64),
+                   "log_term": ib.log_term.cpu().numpy().view(np.uint64)}
+            msgs, total, sd, gf, _ = oc.leader_step(host, lg.inflight_cap, Q, 0, rec, threads=16,
+                                                    msg_cap=cap)
+            dev_state = lg.numpy()
+            bad += [f"{'outbox' if outbox else 'ordered'} step {k}: {n}" for n in host
+                    if not np.array_equal(dev_state[n], host[n])]
+            if res.msg_total != total or not np.array_equal(res.msgs.view(np.uint8),
+                                                            msgs.view(np.uint8)):
+                bad.append(f"{'outbox' if outbox else 'ordered'} step {k}: messages")
+            if not (np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)):
+                bad.append(f"{'outbox' if outbox else 'ordered'} step {k}: stepdown / flags")
+        del lg
+    torch.cuda.empty_cache()
+    return "bit-exact" if not bad else "MISMATCH " + "; ".join(bad[:6])
+
+
 def leader_config(G, reps, warm=4, shuffle=True, *, reporter=None, gpu_only=None):
     """§8f rows 1-2: the leader inbox step (qb_dev_leader_step) on streaming
     MsgAppResp batches (one per group per step), group-steps/s."""
@@ -422,8 +465,13 @@ def leader_config(G, reps, warm=4, shuffle=True, *, reporter=None, gpu_only=None
                "form": "qb_dev_leader_step_outbox (per-group outbox); ordered_* = "
                        "qb_dev_leader_step (group-ordered array)"}
     if not shuffle or gpu_only:
+        extra = {"unit": "group-steps/s", "msgs_per_step": msgs, **ordered}
+        if shuffle and reporter is not report:  # the default run's next_rows: the row's own parity
+            extra["parity"] = leader_row_parity("leader")
+            extra["parity_check"] = ("the same stream at 256K groups, two batches, ordered and "
+                                     "outbox forms vs the C oracle: state, messages, step-downs")
         reporter("leader inbox step" + ("" if shuffle else ", records in group order (lab)"), G, t,
-                 algo, {"unit": "group-steps/s", "msgs_per_step": msgs, **ordered})
+                 algo, extra)
         return
     # CPU beside it: the C restatement (oracle/leader_oracle.c, the Go
     # stepLeader loop one record at a time) on a bounded sample of the same
@@ -485,8 +533,22 @@ def wire_config(M, reps, G=None, rows=False, *, reporter=None, gpu_only=None):
     # 1, index/term/hint/log_term 32, status 1, type 1
     algo = nb + M * (8 + 4 + 40) + M * (4 + 1 + 32 + 1 + 1)
     if gpu_only:
-        reporter("wire ingest" + (" (group rows)" if rows else ""), M, t, algo,
-               {"unit": "messages/s", "bytes_per_message": nb / M})
+        extra = {"unit": "messages/s", "bytes_per_message": nb / M}
+        if reporter is not report:  # the default run's next_rows: the row's own parity
+            ib, status, mtype = wire.ingest(d_buf, nb, d_moff, d_grp, d_off, d_ids, rows=d_rows)
+            want = oc.ingest(buf, moff, grp, off, ids, threads=16)
+            got = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
+                   "index": ib.index.cpu().numpy().view(np.uint64)[:M],
+                   "term": ib.term.cpu().numpy().view(np.uint64)[:M],
+                   "hint": ib.hint.cpu().numpy().view(np.uint64)[:M],
+                   "log_term": ib.log_term.cpu().numpy().view(np.uint64)[:M],
+                   "status": status.cpu().numpy()}
+            bad = [n for n in got if not np.array_equal(got[n][:M], want[n])]
+            extra["parity"] = "bit-exact" if not bad else "MISMATCH " + ", ".join(bad)
+            extra["parity_check"] = (f"all {M} messages decoded by the device and by the C "
+                                     "restatement of Message.Unmarshal + ingest "
+                                     "(oracle/wire_oracle.c): every record column and status")
+        reporter("wire ingest" + (" (group rows)" if rows else ""), M, t, algo, extra)
         return
     import time
     Ms = 1 << 22
@@ -507,6 +569,42 @@ def wire_config(M, reps, G=None, rows=False, *, reporter=None, gpu_only=None):
                              "value_1thread": cpu[1],
                              "sample": f"{Ms} messages of the same stream, C restatement of "
                                        "gogoproto Message.Unmarshal + ingest (oracle/wire_oracle.c)"}})
+
+
+def _confchange_row_parity(table, op, cc_off, cc_type, cc_node, last, t, K):
+    """The conf change row's expected result, checked whole on the device:
+    every group's Simple(AddLearnerNode 6) over voters 1-5."""
+    from etcd_amd.quorum.leader import PR_RECENT_ACTIVE
+    nt, err, _ = table.change_soa(op, cc_off, cc_type, cc_node, last, fetch_errors=False)
+    G = table.G
+    S = 6 * G
+    bad = []
+    ar = torch.arange(S, device=dev)
+    slot, g = ar % 6, ar // 6
+    carried = slot < 5
+    src = g * 5 + slot.clamp(max=4)
+    checks = {
+        "err": bool((err != 0).any()),
+        "off": not torch.equal(nt.t["off"].long()[: G + 1],
+                               torch.arange(0, S + 1, 6, device=dev)),
+        "ids": not torch.equal(nt.t["ids"][:S], slot + 1),
+        "cfg": not torch.equal(nt.t["cfg"][:G], t["cfg"]),
+        "ext": not torch.equal(nt.t["ext"][:G], t["ext"]),
+        "match": not torch.equal(nt.t["match"][:S], torch.where(carried, t["match"][src], 0)),
+        "next": not torch.equal(nt.t["next"][:S], torch.where(carried, t["next"][src], last[g])),
+        "pending_snapshot": not torch.equal(nt.t["pending_snapshot"][:S],
+                                            torch.where(carried, t["pending_snapshot"][src], 0)),
+        "pstate": not torch.equal(nt.t["pstate"][:S].long(),
+                                  torch.where(carried, t["pstate"][src].long(),
+                                              torch.full_like(ar, PR_RECENT_ACTIVE))),
+        "infl_pos": not torch.equal(nt.t["infl_pos"][:S].long(),
+                                    torch.where(carried, t["infl_pos"][src].long(), 0)),
+        "infl_buf": not torch.equal(nt.t["infl_buf"][: S * K].view(S, K),
+                                    torch.where(carried[:, None], t["infl_buf"].view(-1, K)[src], 0)),
+    }
+    bad = [k for k, v in checks.items() if v]
+    del nt
+    return "bit-exact" if not bad else "MISMATCH " + ", ".join(bad)
 
 
 def confchange_config(G, reps, *, reporter=None, gpu_only=None):
@@ -545,7 +643,14 @@ def confchange_config(G, reps, *, reporter=None, gpu_only=None):
     pr = 29 + 8 * K
     algo = G * (4 + 40 + 8 + 1 + 4 + 9 + 8 + 5 * pr + 4 + 48 + 8 + 6 * pr + 9)
     if gpu_only:
-        reporter("conf change", G, tt, algo, {"unit": "groups/s"})
+        extra = {"unit": "groups/s"}
+        if reporter is not report:  # the default run's next_rows: the row's own parity
+            extra["parity"] = _confchange_row_parity(table, op, cc_off, cc_type, cc_node, last, t, K)
+            extra["parity_check"] = (f"all {G} groups: Simple(AddLearnerNode 6) on voters 1-5 gives "
+                                     "slots 1-6, the voter mask unchanged, slots 1-5's Progress "
+                                     "and rings carried, slot 6 initProgress (confchange.go:"
+                                     "258-281), no error — checked on the device")
+        reporter("conf change", G, tt, algo, extra)
         return
     n = 20000
     trs = []
@@ -616,9 +721,12 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
           "check_quorum_groups_per_s": (1 << 24) / tq,
           "check_quorum_GBs": (1 << 24) * 7 / tq / 1e9}
     if gpu_only:
-        reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo,
-                 {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq,
-                  **ordered})
+        extra = {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq, **ordered}
+        if reporter is not report:  # the default run's next_rows: the row's own parity
+            extra["parity"] = leader_row_parity("readindex")
+            extra["parity_check"] = ("the same workload at 256K groups, ordered and outbox forms "
+                                     "vs the C oracle: queues, released reads, every message")
+        reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo, extra)
         return
     # CPU beside it: the C restatement on 1M groups of the same workload
     import time
