@@ -281,3 +281,40 @@ def test_descriptor_fixture_regenerates_from_reference():
     schema = mk.decoded_schema(fdp)
     mk.cross_check(fdp, schema)
     assert {k: {int(n): v for n, v in fs.items()} for k, fs in schema.items()} == _fixture_schema()
+
+
+def test_device_side_appresp_encoder_matches_marshal():
+    """wire.encode_appresp (the composed wire -> tracker workload's generator,
+    run here on CPU tensors) writes exactly the bytes the raftpb restatement's
+    Marshal writes for the same MsgAppResp (which test_encoder_matches_google_
+    protobuf pins to Google's runtime), and the C ingest decodes them back to
+    the columns they came from; out-of-range fields are refused."""
+    import numpy as np
+    import torch
+    from etcd_amd.quorum import wire
+    from tests import oracle_c as oc
+    rng = np.random.default_rng(3)
+    M, G = 300, 50
+    ids = (16384 + np.arange(5)[None, :] * 200000 + (np.arange(G) % 100000)[:, None]).reshape(-1)
+    grp = rng.integers(0, G, M)
+    slot = rng.integers(1, 5, M)
+    to = torch.from_numpy(ids[grp * 5].astype(np.int64))
+    frm = torch.from_numpy(ids[grp * 5 + slot].astype(np.int64))
+    term = torch.from_numpy(rng.integers(1 << 14, 1 << 21, M).astype(np.int64))
+    index = torch.from_numpy(rng.integers(1 << 35, 1 << 42, M).astype(np.int64))
+    rej = torch.from_numpy(rng.random(M) < 0.3)
+    buf, nb, moff = wire.encode_appresp(to, frm, term, index, rej)
+    b = buf.numpy().tobytes()
+    for i in range(M):
+        want = W.marshal_message(4, int(to[i]), int(frm[i]), int(term[i]), 0, int(index[i]),
+                                 reject=bool(rej[i]))
+        assert b[int(moff[i]):int(moff[i + 1])] == want, i
+    off = (np.arange(G + 1) * 5).astype(np.uint32)
+    got = oc.ingest(buf.numpy(), moff.numpy().view(np.uint64), grp.astype(np.uint32), off,
+                    ids.astype(np.uint64))
+    assert (got["status"] == 0).all()
+    assert np.array_equal(got["flags"], (slot | (rej.numpy().astype(np.int64) << 7)).astype(np.uint8))
+    assert np.array_equal(got["index"], index.numpy().view(np.uint64))
+    assert np.array_equal(got["term"], term.numpy().view(np.uint64))
+    with pytest.raises(ValueError):
+        wire.encode_appresp(to, frm, term, index - (1 << 35), rej)
