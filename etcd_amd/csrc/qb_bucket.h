@@ -316,7 +316,10 @@ constexpr u32 kFlagPoolCtr = 2;  // flag word: pool parts drawn
 constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions overflowed
 // K4 dedup (compact form, round 5): a chunk's run of at least kHeavyRun
 // records in one part (a hot group: an even batch puts ~32 records of a chunk
-// in a part) has its records with equal lg | slot | reject | term folded into
+// in a part; a batch capped at raft's 4 x 512 in-flight acks per group per
+// tick stays below it — folding there cost K4 ~24 us for no K5 gain, so the
+// threshold is 2048, not round 5's first 512) has its records with equal
+// lg | slot | reject | term folded into
 // one — the largest index and the count — through an LDS table of
 // kDedupSlots entries.  A folded record is a compact escape whose payload
 // holds kDedupFlag | its side-table entry (row * kDedupSlots + table slot):
@@ -324,8 +327,9 @@ constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions over
 // K5 applies it as `count` records of that class (MaybeUpdate is a max, the
 // RecentActive bit an or; batch order only matters in a chunk with a
 // higher-term record, which still goes to the slow path, which re-reads the
-// original batch).  Escape payloads (batch positions) stay below 2^32.
-constexpr u32 kHeavyRun = 512;
+// original batch).  Escape payloads (batch positions, or kEscColumn | a buf1
+// position) stay below 2^39.
+constexpr u32 kHeavyRun = 2048;
 constexpr u32 kDedupSlots = 256;
 constexpr u64 kDedupFlag = 1ull << 39;
 // An escape of an escape-dense K3 tile: payload = kEscColumn | its buf1
