@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
     } else {
       if (rc) kept_roles(A, g, n_old, r, al);
       u32 ncfg_in = 0, ncfg_out = 0, nlnext = 0;
-      u64 code = ~0ull;  // kCodeNone in every byte
+      u64 code = 0x0101010101010101ull * kCodeNone;  // kCodeNone in every byte
       order_out(t, r, n_old, [&](u32 j, int best) {
         const u32 b = 1u << best;
         if (r.in & b) ncfg_in |= 1u << j;
