@@ -1303,13 +1303,14 @@ def eval_main(args, world, rank, dev, barrier):
 def next_rows():
     """SURVEY §8f rows and configs[0] (tools/bench_configs.py, GPU side only:
     one device time per row) for the default run's line: the leader inbox
-    step (4M groups), ReadIndex acks (4M leaders), wire ingest (16M messages,
+    step (4M groups), ReadIndex acks (4M leaders; local answers as
+    ReadStates, the all-message form beside it), wire ingest (16M messages,
     group-row table), a conf change over 8M groups, the composed wire ->
     tracker tick (16M groups, 16M encoded MsgAppResp per tick; its own
     decode + state parity in the row), and the configs[0]
     plumbing (the faithful C restatement's ns/op beside the device's ns per
     group).  Each row carries its own parity (round 5): the leader and
-    ReadIndex workloads at 256K groups through both output forms vs the C
+    ReadIndex workloads at 256K groups through every output form vs the C
     oracle, the wire decode of all 16M messages vs the C decoder, the conf
     change's whole result checked on the device, the composed row's decode
     and state; the GPU suite covers the rest (tests/test_gpu_leader.py,

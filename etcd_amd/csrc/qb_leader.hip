@@ -61,6 +61,10 @@ struct Msg {
   u16 reserved;
 };
 static_assert(sizeof(Msg) == sizeof(qb_msg_out), "qb_msg_out layout");
+struct ReadSt {
+  u64 index, ctx;
+};
+static_assert(sizeof(ReadSt) == sizeof(qb_read_state), "qb_read_state layout");
 
 inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -162,6 +166,8 @@ struct Args {
   u64* shards;        // [64][QB_LSTAT_COUNT]
   u32* stepdown_at;
   u8* gflags;
+  ReadSt* rs;         // outbox read_states: [readq_cap][G] (null: ReadStates are messages)
+  u32* rcnt;          // ReadStates per group
 };
 
 // ------------------------------------------------------------ L1 / L3 ----
@@ -578,6 +584,7 @@ struct Group {
   u32 nruns;
   u32 nmsg, stored;     // messages generated / stored (the pool can run out)
   u32 chunk;            // current overflow chunk
+  u32 nrs;              // ReadStates stored (the outbox's read_states)
   bool dropped;
 };
 
@@ -992,7 +999,9 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const PrT<S>&
     for (u32 i = 0; i < 4; ++i) {
       if (k0 + i > found) break;
       const u32 from = mt[i] >> 16;
-      if (from == kNoSlot || from == leader_slot(G_))
+      if ((from == kNoSlot || from == leader_slot(G_)) && A.rs)  // r.readStates
+        A.rs[u64(G_.nrs++) * A.lg.G + G_.g] = ReadSt{ix[i], cx[i]};
+      else if (from == kNoSlot || from == leader_slot(G_))
         emit(A, G_, QB_READ_STATE, kNoSlot, ix[i], 0, 0, cx[i]);
       else
         emit(A, G_, QB_MSG_READ_INDEX_RESP, from, ix[i], 0, 0, cx[i]);
@@ -1057,7 +1066,7 @@ __device__ void snap_status(const P& p, bool reject) {
 }
 
 struct StepCounts {
-  u32 applied = 0, stale = 0, higher = 0, non = 0, after = 0, msgs = 0, stored = 0;
+  u32 applied = 0, stale = 0, higher = 0, non = 0, after = 0, msgs = 0, stored = 0, reads = 0;
 };
 
 // One group's records [r0, r1) of the gathered columns, in batch order (raft.go:847-921 term
@@ -1090,6 +1099,7 @@ __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1,
   G_.nmsg = 0;
   G_.stored = 0;
   G_.chunk = 0;
+  G_.nrs = 0;
   G_.dropped = false;
   for (u32 k = r0; k < r1; ++k) {
     if (stepdown != kNone) {
@@ -1133,6 +1143,7 @@ __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1,
   A.lg.meta[g] = G_.meta;
   n.msgs = G_.nmsg;
   n.stored = G_.stored;
+  n.reads = G_.nrs;
 }
 
 // One thread per group.  The workgroup's groups own one contiguous slot span
@@ -1159,6 +1170,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
     // No records for any group of the workgroup: only the outputs.
     if (live) {
       A.mcnt[g] = 0;
+      if (A.rcnt) A.rcnt[g] = 0;
       if (A.stepdown_at) A.stepdown_at[g] = kNone;
       if (A.gflags) A.gflags[g] = 0;
     }
@@ -1198,6 +1210,7 @@ __global__ __launch_bounds__(kBlock) void k_ld_step(Args A) {
       else step_group<false>(A, g, r0, r1, s0, s1, sb, pre, stepdown, gfl, n);
     }
     if (!A.mbs) A.mcnt[g] = n.stored;  // (ordered: the prefix below)
+    if (A.rcnt) A.rcnt[g] = n.reads;
     if (A.stepdown_at) A.stepdown_at[g] = stepdown;
     if (A.gflags) A.gflags[g] = gfl;
   }
@@ -1390,6 +1403,8 @@ struct MsgSink {
   ld::Msg* chunks;
   u64 nchunks;
   u32* chunks_used;  // outbox only
+  ld::ReadSt* rs;    // outbox only, nullable
+  u32* rcnt;
 };
 
 int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, const ld::Carve& c,
@@ -1480,6 +1495,8 @@ int leader_step_impl(const qb_leader_groups* lg, const qb_leader_inbox* in, cons
   A.shards = shards;
   A.stepdown_at = stepdown_at;
   A.gflags = gflags;
+  A.rs = sink->rs;
+  A.rcnt = sink->rcnt;
   hipLaunchKernelGGL(ld::k_ld_step, dim3(grid_for(G)), dim3(kBlock), 0, st, A);
   QB_CHECK_LAUNCH("k_ld_step");
   if (msg_total) {  // the group-ordered array: the workgroups' totals scanned, then the copy
@@ -1540,7 +1557,8 @@ extern "C" int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_in
   char* ws = static_cast<char*>(workspace);
   const MsgSink sink{reinterpret_cast<ld::Msg*>(ws + c.fix), reinterpret_cast<u32*>(ws + c.mcnt),
                      reinterpret_cast<u32*>(ws + c.chead), reinterpret_cast<u32*>(ws + c.cnext),
-                     reinterpret_cast<ld::Msg*>(ws + c.chunks), c.nchunks, nullptr};
+                     reinterpret_cast<ld::Msg*>(ws + c.chunks), c.nchunks, nullptr, nullptr,
+                     nullptr};
   return leader_step_impl(lg, in, c, &sink, msgs, msg_cap, msg_total, msg_off, stepdown_at, gflags,
                           stats, ws, as_stream(stream));
 }
@@ -1557,12 +1575,15 @@ extern "C" int qb_dev_leader_step_outbox(const qb_leader_groups* lg, const qb_le
   QB_REQUIRE(out->nchunks == 0 || (out->chunks && out->chunk_next),
              "qb_dev_leader_step_outbox: chunks / chunk_next are required when nchunks > 0");
   QB_REQUIRE(out->nchunks < (1ull << 32), "qb_dev_leader_step_outbox: nchunks must be < 2^32");
+  QB_REQUIRE(!out->read_states || out->read_count,
+             "qb_dev_leader_step_outbox: read_count is required with read_states");
   const ld::Carve c = ld::carve(lg->G, in->M, /*outbox=*/true);
   QB_REQUIRE(workspace && workspace_bytes >= c.total,
              "qb_dev_leader_step_outbox: workspace needs %zu bytes", c.total);
   const MsgSink sink{reinterpret_cast<ld::Msg*>(out->slots), out->count, out->chunk_head,
                      out->chunk_next, reinterpret_cast<ld::Msg*>(out->chunks), out->nchunks,
-                     out->chunks_used};
+                     out->chunks_used, reinterpret_cast<ld::ReadSt*>(out->read_states),
+                     out->read_states ? out->read_count : nullptr};
   return leader_step_impl(lg, in, c, &sink, nullptr, 0, nullptr, nullptr, stepdown_at, gflags,
                           stats, static_cast<char*>(workspace), as_stream(stream));
 }

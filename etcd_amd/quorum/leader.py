@@ -40,6 +40,8 @@ LSTAT_NAMES = ("applied", "stale_term", "higher_term", "non_member", "after_step
 MSG_DTYPE = np.dtype([("index", "<u8"), ("log_term", "<u8"), ("commit", "<u8"), ("aux", "<u8"),
                       ("group", "<u4"), ("to", "u1"), ("type", "u1"), ("reserved", "<u2")])
 assert MSG_DTYPE.itemsize == 40
+# struct qb_read_state: a local read's answer (raft.go:1737-1745 ReadState)
+READ_STATE_DTYPE = np.dtype([("index", "<u8"), ("ctx", "<u8")])
 
 _P = C.c_void_p
 
@@ -61,7 +63,8 @@ OUTBOX_CHUNK = 32   # QB_LEADER_OUTBOX_CHUNK
 class LeaderOutboxC(C.Structure):
     """struct qb_leader_outbox (include/quorum_batch.h)."""
     _fields_ = [("slots", _P), ("count", _P), ("chunk_head", _P), ("chunk_next", _P),
-                ("chunks", _P), ("nchunks", C.c_uint64), ("chunks_used", _P)]
+                ("chunks", _P), ("nchunks", C.c_uint64), ("chunks_used", _P),
+                ("read_states", _P), ("read_count", _P)]
 
 
 class LeaderInboxC(C.Structure):
@@ -138,6 +141,10 @@ class LeaderStepResult:
     stepdown_at: np.ndarray  # [G] u32 (0xFFFFFFFF = none)
     gflags: np.ndarray      # [G] u8
     stats: Dict[str, int]
+    # step_outbox(read_states=True): the local reads' answers, group order
+    # (Ready.ReadStates), and each group's first; else None
+    read_states: Optional[np.ndarray] = None  # READ_STATE_DTYPE
+    read_off: Optional[np.ndarray] = None     # [G+1]
 
 
 class LeaderGroups:
@@ -210,12 +217,16 @@ class LeaderGroups:
             stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)})
 
     def step_outbox(self, inbox: LeaderInbox, nchunks: Optional[int] = None,
-                    stats: Optional[torch.Tensor] = None, fetch: bool = True):
+                    stats: Optional[torch.Tensor] = None, fetch: bool = True,
+                    read_states: bool = False):
         """One batch through qb_dev_leader_step_outbox: the messages stay in
         the per-group outbox (8 k-major slots per group + 32-message overflow
-        chunks) the step writes them to.  fetch: a LeaderStepResult with the
-        outbox read back into group order on the host (msg_total = messages
-        stored); else the device outbox dict and stats."""
+        chunks) the step writes them to.  read_states: the local reads'
+        answers go to the outbox's ReadState area (readq_cap k-major rows)
+        instead of the messages, as the reference's r.readStates.  fetch: a
+        LeaderStepResult with the outbox read back into group order on the
+        host (msg_total = messages stored); else the device outbox dict and
+        stats."""
         lib = _lib.load()
         M, G, dev = inbox.M, self.G, self.device
         need = lib.qb_leader_outbox_workspace_bytes(G, M)
@@ -223,7 +234,7 @@ class LeaderGroups:
             self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=dev)
         if nchunks is None:
             nchunks = M // 8 + 1024
-        ob = self._outbox(nchunks)
+        ob = self._outbox(nchunks, read_states)
         if stats is None:
             stats = torch.zeros(8, dtype=torch.int64, device=dev)
         ls = self._struct()
@@ -234,7 +245,9 @@ class LeaderGroups:
                            chunk_head=ob["chunk_head"].data_ptr(),
                            chunk_next=ob["chunk_next"].data_ptr() if nchunks else None,
                            chunks=ob["chunks"].data_ptr() if nchunks else None, nchunks=nchunks,
-                           chunks_used=ob["chunks_used"].data_ptr())
+                           chunks_used=ob["chunks_used"].data_ptr(),
+                           read_states=ob["read_states"].data_ptr() if read_states else None,
+                           read_count=ob["read_count"].data_ptr() if read_states else None)
         _lib.call("qb_dev_leader_step_outbox", C.byref(ls), C.byref(ib), C.byref(oc),
                   ob["stepdown"].data_ptr(), ob["gflags"].data_ptr(), stats.data_ptr(),
                   self._ws.data_ptr(), self._ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
@@ -276,15 +289,26 @@ class LeaderGroups:
             if sel.size:
                 c = nxt[c[more]].astype(np.int64)
         st = stats.cpu().tolist()
+        rs = roff = None
+        if "read_states" in ob:
+            rcnt = _to_np(ob["read_count"], np.uint32, G).astype(np.int64)
+            rows = ob["read_states"].cpu().numpy().view(READ_STATE_DTYPE).reshape(-1, G)
+            roff = np.zeros(G + 1, np.int64)
+            roff[1:] = np.cumsum(rcnt)
+            rs = np.empty(int(roff[-1]), READ_STATE_DTYPE)
+            for k in range(rows.shape[0]):
+                sel = np.nonzero(rcnt > k)[0]
+                rs[roff[sel] + k] = rows[k, sel]
         return LeaderStepResult(
             msgs=msgs, msg_total=int(off[-1]), msg_off=off.astype(np.uint32),
             stepdown_at=_to_np(ob["stepdown"], np.uint32, G),
             gflags=_to_np(ob["gflags"], np.uint8, G),
-            stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)})
+            stats={k: st[i] for i, k in enumerate(LSTAT_NAMES)},
+            read_states=rs, read_off=roff)
 
-    def _outbox(self, nchunks: int):
+    def _outbox(self, nchunks: int, read_states: bool = False):
         dev, G = self.device, self.G
-        key = ("outbox", nchunks)
+        key = ("outbox", nchunks, read_states)
         if getattr(self, "_ob_key", None) != key:
             self._ob = {"slots": torch.empty(OUTBOX_SLOTS * G * 40, dtype=torch.uint8, device=dev),
                         "count": torch.zeros(G, dtype=torch.int32, device=dev),
@@ -295,6 +319,10 @@ class LeaderGroups:
                         "chunks_used": torch.zeros(1, dtype=torch.int32, device=dev),
                         "stepdown": torch.zeros(G, dtype=torch.int32, device=dev),
                         "gflags": torch.zeros(G, dtype=torch.uint8, device=dev)}
+            if read_states:
+                self._ob["read_states"] = torch.empty(max(self.readq_cap, 1) * G * 16,
+                                                      dtype=torch.uint8, device=dev)
+                self._ob["read_count"] = torch.zeros(G, dtype=torch.int32, device=dev)
             self._ob_key = key
         return self._ob
 

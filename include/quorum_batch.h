@@ -591,9 +591,20 @@ int qb_dev_leader_step(const qb_leader_groups* lg, const qb_leader_inbox* in,
  * not be drawn — all nchunks used — stops there; the rest is counted in
  * QB_LSTAT_MSGS_DROPPED); *chunks_used (device u32) = chunks drawn, at most
  * nchunks (chunks[0 .. chunks_used) hold messages).
+ * read_states (nullable): the local reads' answers kept apart from the
+ * messages, as the reference keeps them (responseToReadIndexReq appends a
+ * ReadState to r.readStates, raft.go:1737-1745; Ready.ReadStates,
+ * node.go:67,580): group g's k-th ReadState is read_states[k * G + g] for
+ * k < read_count[g] (at most lg->readq_cap: a step releases no more reads
+ * than the queue held), oldest first, and no QB_READ_STATE message is
+ * emitted.  NULL keeps them in the messages as QB_READ_STATE (to 0xFF).
  * stepdown_at / gflags / stats as qb_dev_leader_step. */
 #define QB_LEADER_OUTBOX_SLOTS 8
 #define QB_LEADER_OUTBOX_CHUNK 32
+typedef struct qb_read_state {
+  uint64_t index;       /* ReadState.Index                                   */
+  uint64_t ctx;         /* ReadState.RequestCtx (the request's 8-byte context) */
+} qb_read_state;
 typedef struct qb_leader_outbox {
   qb_msg_out* slots;    /* [QB_LEADER_OUTBOX_SLOTS * G], k-major             */
   uint32_t* count;      /* [G] messages per group                            */
@@ -602,6 +613,8 @@ typedef struct qb_leader_outbox {
   qb_msg_out* chunks;   /* [nchunks * QB_LEADER_OUTBOX_CHUNK]                */
   uint64_t nchunks;     /* 0: no overflow (messages past the 8th dropped)    */
   uint32_t* chunks_used; /* device u32                                       */
+  qb_read_state* read_states; /* nullable: [readq_cap * G], k-major          */
+  uint32_t* read_count; /* [G] ReadStates per group (required with read_states) */
 } qb_leader_outbox;
 size_t qb_leader_outbox_workspace_bytes(uint64_t G, uint64_t M);
 int qb_dev_leader_step_outbox(const qb_leader_groups* lg, const qb_leader_inbox* in,

@@ -201,3 +201,22 @@ def test_tracker_region_grid_u32_guard():
                                      dummy, C.c_size_t(1 << 62), None)
     assert rc == _lib.QB_EINVAL
     assert b"region records" in lib.qb_last_error()
+
+
+def test_leader_outbox_binding_layout_matches_header(tmp_path):
+    """The Python binding's qb_leader_outbox / qb_read_state match the
+    header's layout (gcc on the header itself): the ReadState area's two
+    fields sit where the library reads them."""
+    import subprocess
+    from etcd_amd.quorum.leader import READ_STATE_DTYPE, LeaderOutboxC
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "quorum_batch.h"\n'
+                   'int main(void) { printf("%zu %zu %zu %zu\\n", sizeof(qb_leader_outbox), '
+                   'offsetof(qb_leader_outbox, read_states), offsetof(qb_leader_outbox, read_count), '
+                   'sizeof(qb_read_state)); return 0; }\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert got == [C.sizeof(LeaderOutboxC), LeaderOutboxC.read_states.offset,
+                   LeaderOutboxC.read_count.offset, READ_STATE_DTYPE.itemsize]

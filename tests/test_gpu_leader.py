@@ -68,8 +68,20 @@ def test_reference_scenarios_on_device(sc):
         assert LP.state_key(g) == LP.state_key(twin), where
 
 
+def _split_reads(om):
+    """The oracle's messages with its local ReadStates (type 255) taken out
+    into (group, index, ctx) — the outbox's read_states form."""
+    return ([m for m in om if m[1] != 255], [(m[0], m[3], m[6]) for m in om if m[1] == 255])
+
+
+def _dev_reads(res):
+    G = len(res.read_off) - 1
+    grp = np.repeat(np.arange(G), np.diff(res.read_off))
+    return [(int(g), int(r["index"]), int(r["ctx"])) for g, r in zip(grp, res.read_states)]
+
+
 def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_groups=0,
-          hot_frac=0.0, term_base=0, options=0, outbox=False):
+          hot_frac=0.0, term_base=0, options=0, outbox=False, read_states=False):
     rng = np.random.default_rng(seed)
     groups = LP.random_groups(rng, G, inflight_cap, readq_cap, max_slots, term_base)
     for g in groups:
@@ -77,7 +89,10 @@ def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_gro
     recs = LP.random_records(rng, groups, M, hot_groups=hot_groups, hot_frac=hot_frac)
     eng = _engine(groups, inflight_cap, readq_cap, read_only)
     eng.options = options
-    res = eng.step_outbox(_inbox(recs)) if outbox else eng.step(_inbox(recs))
+    if read_states:
+        res = eng.step_outbox(_inbox(recs), read_states=True)
+    else:
+        res = eng.step_outbox(_inbox(recs)) if outbox else eng.step(_inbox(recs))
     orc = copy.deepcopy(groups)
     for g in orc:
         g.msgs = []
@@ -87,6 +102,10 @@ def _fuzz(seed, G, M, inflight_cap, readq_cap, read_only=0, max_slots=9, hot_gro
     for gi in range(G):
         assert LP.state_key(dev[gi]) == LP.state_key(orc[gi]), f"seed {seed} group {gi}"
     om = _orc_msgs(orc)
+    if read_states:
+        om, reads = _split_reads(om)
+        assert reads, "the case releases no local read"
+        assert _dev_reads(res) == reads
     assert res.msg_total == len(om)
     assert _dev_msgs(res) == om
     want_sd = np.array([0xFFFFFFFF if g.stepped_down_at is None else g.stepped_down_at for g in orc],
@@ -147,6 +166,17 @@ def test_fuzz_outbox(seed):
     per-group outbox (8 k-major slots + overflow chunks), read back in group
     order — identical to the oracle (and so to qb_dev_leader_step)."""
     _fuzz(seed, G=400, M=1500, inflight_cap=3, readq_cap=4, outbox=True)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_fuzz_outbox_read_states(seed):
+    """The outbox's ReadState area: the local reads' answers leave the
+    messages (raft.go:1737-1745 appends them to r.readStates), in release
+    order per group; every other message, the state and the flags as the
+    oracle's."""
+    _fuzz(seed, G=400, M=1500, inflight_cap=3, readq_cap=4, read_states=True)
+    _fuzz(seed + 10, G=300, M=5000, inflight_cap=6, readq_cap=16, hot_groups=3, hot_frac=0.5,
+          read_states=True)
 
 
 def test_fuzz_outbox_overflow_chunks():
@@ -362,17 +392,21 @@ def test_dense_batch_overflow_pool_windows_vs_c_oracle():
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("outbox", [False, True])
+@pytest.mark.parametrize("outbox", [False, True, "read_states"])
 def test_readindex_workload_vs_c_oracle(outbox):
     """The ReadIndex bench workload (§8f row 2) at 256K groups: queues,
-    released reads and every message against the C oracle."""
+    released reads and every message against the C oracle (read_states: the
+    outbox's ReadState area holds the local answers)."""
     from etcd_amd.quorum.leader import readindex_inbox, synth_readindex
     from tests import oracle_c as oc
     G, Q = 1 << 18, 4
     lg, last_ctx, _ = synth_readindex(G, Q, device="cuda")
     host = {k: v.copy() for k, v in lg.numpy().items()}
     ib = readindex_inbox(G, last_ctx, device="cuda")
-    res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=8 * G)
+    if outbox == "read_states":
+        res = lg.step_outbox(ib, read_states=True)
+    else:
+        res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=8 * G)
     rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
            "index": ib.index.cpu().numpy().view(np.uint64),
            "term": ib.term.cpu().numpy().view(np.uint64),
@@ -383,5 +417,15 @@ def test_readindex_workload_vs_c_oracle(outbox):
     dev = lg.numpy()
     for name in host:
         assert np.array_equal(dev[name], host[name]), name
+    if outbox == "read_states":
+        local = msgs["type"] == 255
+        assert total == Q * G and res.msg_total == int((~local).sum()) and local.any()
+        assert np.array_equal(res.msgs.view(np.uint8), msgs[~local].view(np.uint8))
+        assert np.array_equal(res.read_states["index"], msgs["index"][local])
+        assert np.array_equal(res.read_states["ctx"], msgs["aux"][local])
+        want_off = np.zeros(G + 1, np.int64)
+        want_off[1:] = np.cumsum(np.bincount(msgs["group"][local], minlength=G))
+        assert np.array_equal(res.read_off, want_off)
+        return
     assert res.msg_total == total == Q * G
     assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))

@@ -381,7 +381,9 @@ def leader_row_parity(kind, Gs=1 << 18):
                                         synth_streaming)
     from tests import oracle_c as oc
     bad = []
-    for outbox in (False, True):
+    forms = (False, True, "read_states") if kind == "readindex" else (False, True)
+    for outbox in forms:
+        name = {False: "ordered", True: "outbox", "read_states": "outbox+read_states"}[outbox]
         if kind == "leader":
             lg, base = synth_streaming(Gs, device=dev)
             inboxes = [streaming_inbox(Gs, base, k, device=dev) for k in range(2)]
@@ -392,7 +394,10 @@ def leader_row_parity(kind, Gs=1 << 18):
             Q, cap = 4, 8 * Gs
         host = {k: v.copy() for k, v in lg.numpy().items()}
         for k, ib in enumerate(inboxes):
-            res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=cap)
+            if outbox == "read_states":
+                res = lg.step_outbox(ib, read_states=True)
+            else:
+                res = lg.step_outbox(ib) if outbox else lg.step(ib, msg_cap=cap)
             rec = {"group": ib.group.cpu().numpy().view(np.uint32), "flags": ib.flags.cpu().numpy(),
                    "index": ib.index.cpu().numpy().view(np.uint64),
                    "term": ib.term.cpu().numpy().view(np.uint64),
@@ -401,13 +406,24 @@ def leader_row_parity(kind, Gs=1 << 18):
             msgs, total, sd, gf, _ = oc.leader_step(host, lg.inflight_cap, Q, 0, rec, threads=16,
                                                     msg_cap=cap)
             dev_state = lg.numpy()
-            bad += [f"{'outbox' if outbox else 'ordered'} step {k}: {n}" for n in host
+            bad += [f"{name} step {k}: {n}" for n in host
                     if not np.array_equal(dev_state[n], host[n])]
+            if outbox == "read_states":  # the local answers as ReadStates, the rest as messages
+                local = msgs["type"] == 255
+                roff = np.zeros(Gs + 1, np.int64)
+                roff[1:] = np.cumsum(np.bincount(msgs["group"][local], minlength=Gs))
+                if not (local.any() and total == len(msgs)
+                        and np.array_equal(res.read_states["index"], msgs["index"][local])
+                        and np.array_equal(res.read_states["ctx"], msgs["aux"][local])
+                        and np.array_equal(res.read_off, roff)):
+                    bad.append(f"{name} step {k}: read states")
+                msgs = msgs[~local]
+                total = len(msgs)
             if res.msg_total != total or not np.array_equal(res.msgs.view(np.uint8),
                                                             msgs.view(np.uint8)):
-                bad.append(f"{'outbox' if outbox else 'ordered'} step {k}: messages")
+                bad.append(f"{name} step {k}: messages")
             if not (np.array_equal(res.stepdown_at, sd) and np.array_equal(res.gflags, gf)):
-                bad.append(f"{'outbox' if outbox else 'ordered'} step {k}: stepdown / flags")
+                bad.append(f"{name} step {k}: stepdown / flags")
         del lg
     torch.cuda.empty_cache()
     return "bit-exact" if not bad else "MISMATCH " + "; ".join(bad[:6])
@@ -700,19 +716,30 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
         ev.close()
         return float(np.median(times)), stats.cpu().tolist()
     t_ord, st = timed(lambda ib: lg.step(ib, msg_cap=8 * G, stats=stats, fetch=False))
-    t, st_ob = timed(lambda ib: lg.step_outbox(ib, stats=stats, fetch=False))
+    t_msg, st_ob = timed(lambda ib: lg.step_outbox(ib, stats=stats, fetch=False))
     assert st_ob[6] == st[6], "outbox and ordered forms generated different message counts"
+    # the row's form: the outbox with its ReadState area — a local read's
+    # answer is a ReadState (raft.go:1737-1745, Ready.ReadStates), not a message
+    t, st_rs = timed(lambda ib: lg.step_outbox(ib, stats=stats, fetch=False, read_states=True))
+    local_reads = (st[6] - st_rs[6]) / reps  # the ReadStates per step (out of the messages)
     # per group-step: 2 records 2 x 21 B, group state 84 B, 5 slots x 29 B,
-    # read queue Q x 20 B read + written, the grouping scan 8 B; Q messages:
-    # the outbox form 40 B each + a 4 B count per group, the ordered form
-    # 40 B x 3 + the count scan 8 B per group
+    # read queue Q x 20 B read + written, the grouping scan 8 B; then the
+    # answers: the row's form 40 B per message + 16 B per ReadState + two 4 B
+    # counts per group; every answer a message (messages_*) 40 B each + a 4 B
+    # count; the ordered form 40 B x 3 + the count scan 8 B per group
     base = G * (42 + 84 + 145 + Q * 20 * 2 + 8)
-    algo = base + G * (4 + Q * 40)
+    algo = base + G * 8 + (st_rs[6] / reps) * 40 + local_reads * 16
+    algo_msg = base + G * (4 + Q * 40)
     algo_ord = base + G * (8 + Q * 40 * 3)
-    ordered = {"ordered_us": t_ord * 1e6, "ordered_algo_bytes": algo_ord,
+    ordered = {"messages_us": t_msg * 1e6, "messages_algo_bytes": algo_msg,
+               "messages_frac": algo_msg / t_msg / 1e9 / HBM_PEAK_GBS,
+               "ordered_us": t_ord * 1e6, "ordered_algo_bytes": algo_ord,
                "ordered_frac": algo_ord / t_ord / 1e9 / HBM_PEAK_GBS,
-               "form": "qb_dev_leader_step_outbox (per-group outbox); ordered_* = "
-                       "qb_dev_leader_step (group-ordered array)"}
+               "read_states_per_step": local_reads,
+               "form": "qb_dev_leader_step_outbox with its ReadState area (local answers as "
+                       "16-byte ReadStates, follower answers as MsgReadIndexResp); messages_* = "
+                       "the same outbox with every answer a message (rounds 4-5's row); "
+                       "ordered_* = qb_dev_leader_step (group-ordered array)"}
     # CheckQuorum: QuorumActive over 16M groups (cfg u32 + active u16 -> u8)
     grp = batch.CsrGroups.synth(0x5EED0003, "ragged", 1 << 24, device=dev)
     active = torch.randint(-(1 << 15), 1 << 15, (1 << 24,), dtype=torch.int16, device=dev)
@@ -724,8 +751,9 @@ def readindex_config(G, reps, Q=4, *, reporter=None, gpu_only=None):
         extra = {"unit": "group-steps/s", "reads_released_per_step": st[6] / reps, **cq, **ordered}
         if reporter is not report:  # the default run's next_rows: the row's own parity
             extra["parity"] = leader_row_parity("readindex")
-            extra["parity_check"] = ("the same workload at 256K groups, ordered and outbox forms "
-                                     "vs the C oracle: queues, released reads, every message")
+            extra["parity_check"] = ("the same workload at 256K groups, ordered, outbox and "
+                                     "outbox + ReadState forms vs the C oracle: queues, released "
+                                     "reads, every message and ReadState")
         reporter("ReadIndex acks (leader step, heartbeat responses)", G, t, algo, extra)
         return
     # CPU beside it: the C restatement on 1M groups of the same workload
