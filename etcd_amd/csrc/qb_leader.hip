@@ -962,7 +962,9 @@ __device__ void heartbeat_resp(const Args& A, Group& G_, u32 slot, const PrT<S>&
   if (A.lg.read_only != QB_READ_ONLY_SAFE || ctx == 0) return;
   // read_only.go:68-79 recvAck
   const u32 cap = A.lg.readq_cap;
-  const u32 qlen = (G_.meta >> 20) & 0x1Fu;
+  // (a count past the queue's capacity is read as the capacity: no access
+  // outside the caller's [readq_cap * G] arrays or the ReadState area)
+  const u32 qlen = min((G_.meta >> 20) & 0x1Fu, cap);
   u64* qctx = U(A.lg.rq_ctx) + G_.g * cap;
   u64* qidx = U(A.lg.rq_index) + G_.g * cap;
   u32* qmeta = A.lg.rq_meta + G_.g * cap;
@@ -1095,7 +1097,7 @@ __device__ __forceinline__ void step_group(const Args& A, u64 g, u32 r0, u32 r1,
   G_.committed = pre.committed;
   G_.first = pre.first;
   G_.last = pre.last;
-  G_.nruns = (G_.meta >> 16) & 0xFu;
+  G_.nruns = min((G_.meta >> 16) & 0xFu, u32(QB_LEADER_MAX_RUNS));  // (the arrays' rows)
   G_.nmsg = 0;
   G_.stored = 0;
   G_.chunk = 0;

@@ -471,9 +471,11 @@ int qb_dev_csr_tally_votes(uint64_t G, const uint32_t* cfg,
 #define QB_PR_RECENT_ACTIVE 0x08u
 
 /* Group meta word: leader slot (bits 0-7), lead transferee slot (8-15,
- * 0xFF = None), term runs (16-19, 1..8), pending ReadIndex requests (20-24),
- * bit 25: MsgReadIndex postponed until the first commit of the term
- * (raft.pendingReadIndexMessages). */
+ * 0xFF = None), term runs (16-19, 1..8), pending ReadIndex requests (20-24,
+ * at most readq_cap), bit 25: MsgReadIndex postponed until the first commit
+ * of the term (raft.pendingReadIndexMessages).  A run count past
+ * QB_LEADER_MAX_RUNS or a request count past readq_cap is read as that bound
+ * (the step never reads or writes outside the caller's arrays). */
 #define QB_META_PENDING_READINDEX (1u << 25)
 
 /* Diagnostic switch: group the records with per-record global atomics (the

@@ -429,3 +429,35 @@ def test_readindex_workload_vs_c_oracle(outbox):
         return
     assert res.msg_total == total == Q * G
     assert np.array_equal(res.msgs.view(np.uint8), msgs.view(np.uint8))
+
+
+def test_meta_counts_past_their_bounds_read_as_the_bounds():
+    """A group meta word whose pending-read count exceeds readq_cap or whose
+    term-run count exceeds QB_LEADER_MAX_RUNS is read as the bound (the
+    header's contract): the step stays inside the caller's arrays and the
+    ReadState area and gives what the bounded word gives."""
+    import torch
+    from etcd_amd.quorum.leader import readindex_inbox, synth_readindex
+    G, Q = 4096, 4
+    outs = []
+    for qbits, rbits in ((Q, 8), (31, 15)):
+        torch.manual_seed(7)
+        lg, last_ctx, _ = synth_readindex(G, Q, device="cuda")
+        m = lg.t["meta"]
+        m.copy_((m & ~((0x1F << 20) | (0xF << 16))) | (qbits << 20) | (rbits << 16))
+        ib = readindex_inbox(G, last_ctx, device="cuda")
+        res = lg.step_outbox(ib, read_states=True)
+        outs.append((res, lg.numpy()))
+    (a, sa), (b, sb) = outs
+    assert a.read_off[-1] > 0 and np.all(np.diff(b.read_off) <= Q)
+    assert np.array_equal(a.msgs.view(np.uint8), b.msgs.view(np.uint8))
+    assert np.array_equal(a.read_states.view(np.uint8), b.read_states.view(np.uint8))
+    assert np.array_equal(a.read_off, b.read_off)
+    for name in sa:
+        x, y = sa[name], sb[name]
+        if name == "meta":  # the count bits of an untouched group stay as written
+            qx, qy = (x >> 20) & 0x1F, np.minimum((y >> 20) & 0x1F, Q)
+            assert np.array_equal(qx, qy), "meta: pending reads"
+            keep = np.array(~(0x1FF << 16) & 0xFFFFFFFF).astype(x.dtype)
+            x, y = x & keep, y & keep
+        assert np.array_equal(x, y), name
