@@ -594,7 +594,19 @@ __global__ __launch_bounds__(256) void k_cc_move(Args A) {
     } else if (v.fresh) {
       v.nx = A.last_index[v.src];
     }
-    if (K <= 4) {
+    if (K == 4) {  // the ring as two 16-byte loads (the kernel is issue-bound on its
+                   // vector-memory instructions: 1 ring instruction pair instead of 4)
+      const ulonglong2* sr = reinterpret_cast<const ulonglong2*>(A.infl_buf + u64(v.src) * 4);
+      ulonglong2 x0 = make_ulonglong2(0, 0), x1 = x0;
+      if (v.ok) {
+        x0 = sr[0];
+        x1 = sr[1];
+      }
+      v.r[0] = x0.x;
+      v.r[1] = x0.y;
+      v.r[2] = x1.x;
+      v.r[3] = x1.y;
+    } else if (K < 4) {
       const u64* sr = A.infl_buf + u64(v.src) * K;
 #pragma unroll
       for (u32 k = 0; k < 4; ++k) v.r[k] = (v.ok && k < K) ? sr[k] : 0ull;
@@ -618,7 +630,11 @@ __global__ __launch_bounds__(256) void k_cc_move(Args A) {
       A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
     }
     u64* dr = A.n_infl_buf + d * K;
-    if (K <= 4) {
+    if (K == 4) {
+      ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dr);
+      d2[0] = make_ulonglong2(v.r[0], v.r[1]);
+      d2[1] = make_ulonglong2(v.r[2], v.r[3]);
+    } else if (K < 4) {
 #pragma unroll
       for (u32 k = 0; k < 4; ++k)
         if (k < K) dr[k] = v.r[k];
