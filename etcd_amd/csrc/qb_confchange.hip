@@ -72,6 +72,10 @@ struct Args {
   const u32* infl_pos;
   const u64* infl_buf;
   u32 K;
+  // K == 4 and both ring buffers 16-byte aligned: the ring moves as 16-byte
+  // words (the ABI promises only 8-byte alignment of u64 arrays;
+  // an unaligned caller's ring takes the 8-byte loop)
+  u32 ring16;
   // new
   u32* new_cnt;  // [G+1] counts, then 4096-block local prefixes; the write pass stores the offsets
   const u32* nbsum;  // the local scan's block sums, scanned (add-back folded into the write pass)
@@ -594,7 +598,7 @@ __global__ __launch_bounds__(256) void k_cc_move(Args A) {
     } else if (v.fresh) {
       v.nx = A.last_index[v.src];
     }
-    if (K == 4) {  // the ring as two 16-byte loads (the kernel is issue-bound on its
+    if (K == 4 && A.ring16) {  // the ring as two 16-byte loads (the kernel is issue-bound on its
                    // vector-memory instructions: 1 ring instruction pair instead of 4)
       const ulonglong2* sr = reinterpret_cast<const ulonglong2*>(A.infl_buf + u64(v.src) * 4);
       ulonglong2 x0 = make_ulonglong2(0, 0), x1 = x0;
@@ -630,7 +634,7 @@ __global__ __launch_bounds__(256) void k_cc_move(Args A) {
       A.n_pstate[d] = QB_PR_PROBE | QB_PR_RECENT_ACTIVE;
     }
     u64* dr = A.n_infl_buf + d * K;
-    if (K == 4) {
+    if (K == 4 && A.ring16) {
       ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dr);
       d2[0] = make_ulonglong2(v.r[0], v.r[1]);
       d2[1] = make_ulonglong2(v.r[2], v.r[3]);
@@ -711,6 +715,8 @@ extern "C" int qb_dev_conf_change(const qb_conf_change_in* in, const qb_conf_cha
   A.infl_pos = in->infl_pos;
   A.infl_buf = reinterpret_cast<const u64*>(in->infl_buf);
   A.K = in->inflight_cap;
+  A.ring16 = (reinterpret_cast<uintptr_t>(in->infl_buf) & 15u) == 0 &&
+             (reinterpret_cast<uintptr_t>(out->infl_buf) & 15u) == 0;
   A.new_cnt = out->new_off;
   A.S_cap = out->slot_cap;
   A.n_ids = reinterpret_cast<u64*>(out->ids);

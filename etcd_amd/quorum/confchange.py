@@ -63,6 +63,54 @@ def _dev(a, dt, device):
     return torch.from_numpy(a.view(_SIGNED[dt]).copy()).to(device)
 
 
+# ``out`` of change_soa: element size per key; per-slot arrays share the slot
+# capacity, infl_buf holds capacity x K, the per-group ones G (new_off G + 1).
+_OUT_ELEM = {"new_off": 4, "cfg": 4, "ext": 4, "err": 1, "err_id": 8, "ids": 8, "match": 8,
+             "next": 8, "pending_snapshot": 8, "pstate": 1, "infl_pos": 4, "infl_buf": 8}
+_OUT_SLOT = ("ids", "match", "next", "pending_snapshot", "pstate", "infl_pos")
+
+
+def _check_out(o: Dict[str, torch.Tensor], G: int, K: int, dev, table) -> int:
+    """Validate caller-owned outputs before their raw pointers reach
+    qb_dev_conf_change: the kernels write slot_cap entries of
+    every per-slot array, slot_cap x K of infl_buf and G (+1) of the per-group
+    ones, so a short, strided, host, wrongly sized or aliased tensor would be
+    an out-of-bounds or self-overwriting device write.  Returns slot_cap =
+    the shortest per-slot array."""
+    missing = [k for k in _OUT_ELEM if k not in o]
+    if missing:
+        raise _lib.QuorumBatchError(f"conf change out: missing {missing}")
+    for k, es in _OUT_ELEM.items():
+        t = o[k]
+        if not isinstance(t, torch.Tensor) or t.device != dev:
+            raise _lib.QuorumBatchError(f"conf change out[{k!r}]: a tensor on {dev} is required")
+        if t.element_size() != es:
+            raise _lib.QuorumBatchError(
+                f"conf change out[{k!r}]: element size {t.element_size()}, expected {es}")
+        if not t.is_contiguous():
+            raise _lib.QuorumBatchError(f"conf change out[{k!r}]: must be contiguous")
+    cap = min(o[k].numel() for k in _OUT_SLOT)
+    if cap < 1:
+        raise _lib.QuorumBatchError("conf change out: per-slot arrays are empty")
+    if o["infl_buf"].numel() < max(1, cap * K):
+        raise _lib.QuorumBatchError(
+            f"conf change out['infl_buf']: {o['infl_buf'].numel()} < slot capacity {cap} x {K}")
+    for k, n in (("new_off", G + 1), ("cfg", G), ("ext", G), ("err", G), ("err_id", G)):
+        if o[k].numel() < n:
+            raise _lib.QuorumBatchError(f"conf change out[{k!r}]: {o[k].numel()} < {n}")
+
+    def span(t):
+        a = t.data_ptr()
+        return a, a + t.numel() * t.element_size()
+    outs = [(k, span(o[k])) for k in _OUT_ELEM]
+    ins = [(k, span(v)) for k, v in table.items()]
+    for i, (ka, (a0, a1)) in enumerate(outs):
+        for kb, (b0, b1) in outs[i + 1:] + ins:
+            if a0 < b1 and b0 < a1:
+                raise _lib.QuorumBatchError(f"conf change out[{ka!r}] overlaps {kb!r}")
+    return cap
+
+
 @dataclass
 class ConfigTable:
     """G groups' configs (CSR slots) and Progress on one device."""
@@ -139,7 +187,7 @@ class ConfigTable:
              "err_id": torch.empty(G, dtype=torch.int64, device=dev)}
         if out is not None:
             o = out
-            cap = o["ids"].numel()
+            cap = _check_out(o, G, K, dev, self.t)
         i = _In(G=G, inflight_cap=K, reserved=0)
         for k, v in (("op", d_op), ("cc_off", d_ccoff), ("cc_type", d_cct), ("cc_node", d_ccn),
                      ("last_index", d_last)):

@@ -742,7 +742,9 @@ typedef struct qb_conf_change_in {
   const uint64_t* pending_snapshot;
   const uint8_t* pstate;
   const uint32_t* infl_pos;
-  const uint64_t* infl_buf;  /* [off[G] * inflight_cap] */
+  const uint64_t* infl_buf;  /* [off[G] * inflight_cap]; 8-byte aligned suffices (16-byte
+                                aligned in and out buffers let inflight_cap 4 move rings
+                                as 16-byte words) */
 } qb_conf_change_in;
 
 typedef struct qb_conf_change_out {

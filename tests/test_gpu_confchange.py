@@ -262,3 +262,183 @@ def test_short_capacity_writes_nothing_past_it(short):
     for k in sent:
         assert (h[k][cap:] == np.array(sent[k]).astype(h[k].dtype)).all(), k
     assert (h["infl_buf"][cap * K:] == -7).all()
+
+
+def _ring_marks(table, K):
+    """Give every old slot a unique nonzero match marker and a ring of
+    (marker, k) words; returns {marker: ring} (test-only identities)."""
+    import torch
+    from etcd_amd.quorum.confchange import ConfigTable
+    a = table.numpy()
+    S = int(a["off"][-1])
+    marks = np.arange(1, S + 1, dtype=np.uint64) * np.uint64(1000)
+    a["match"][:S] = marks
+    ring = (marks[:, None] + np.arange(1, K + 1, dtype=np.uint64)[None, :]).reshape(-1)
+    prog = {k: a[k] for k in ("match", "next", "pending_snapshot", "pstate", "infl_pos")}
+    prog["infl_buf"] = ring if K else np.zeros(1, np.uint64)
+    t = ConfigTable.from_numpy(a["off"], a["ids"], a["cfg"], a["ext"], prog, K)
+    rings = {int(m): ring[i * K:(i + 1) * K] for i, m in enumerate(marks)}
+    return t, rings
+
+
+def _check_rings(new, rings, K):
+    """A carried slot (its old match marker survives) keeps its old ring word
+    for word; a fresh one (initProgress: match 0) has an empty one."""
+    a = new.numpy()
+    S = int(a["off"][-1])
+    for s in range(S):
+        got = a["infl_buf"][s * K:(s + 1) * K]
+        m = int(a["match"][s])
+        want = rings[m] if m in rings else np.zeros(K, np.uint64)
+        assert np.array_equal(got, want), (s, m, got, want)
+
+
+@pytest.mark.parametrize("K", [0, 1, 3, 4, 8])
+def test_ring_sizes_vs_oracle(K):
+    """k_cc_move's K == 4 / K < 4 / K > 4 ring branches (K = 0 with
+    no ring at all) against the oracle's configs and Progress, and every
+    carried ring moved word for word (fresh slots start empty)."""
+    r = random.Random(40 + K)
+    G = 900
+    orc = [CC.Tracker.empty(K) for _ in range(G)]
+    table = _table(orc, K=K)
+    for step in range(6):
+        op = [CP.random_op(r, t) for t in orc]
+        ccs = [CP.random_ccs(r) for _ in orc]
+        last = [r.randint(0, 1000) for _ in orc]
+        marked, rings = _ring_marks(table, K)
+        host = marked.numpy()      # the oracle carries the same markers
+        for g in range(G):
+            for s in range(int(host["off"][g]), int(host["off"][g + 1])):
+                orc[g].prs[int(host["ids"][s])].match = int(host["match"][s])
+        table, err, err_id = marked.change(op, ccs, last)
+        dev = CP.unpack(table.numpy(), K)
+        for g in range(G):
+            nt, e = CP.oracle_apply(orc[g], op[g], ccs[g], last[g])
+            if e is None and sum(1 for _ in nt.prs) > 16:
+                nt, e = orc[g], "engine limit"
+            assert bool(err[g]) == (e is not None), (K, step, g, e)
+            assert _render(dev[g]) == _render(nt), (K, step, g)
+            orc[g] = nt
+        if K:
+            _check_rings(table, rings, K)
+
+
+def test_ring16_unaligned_buffers_take_the_word_loop():
+    """inflight_cap 4 with ring buffers only 8-byte aligned (views
+    one element into larger tensors) gives exactly the aligned call's
+    result."""
+    import torch
+    r = random.Random(77)
+    G, K = 700, 4
+    orc = [CC.Tracker.empty(K) for _ in range(G)]
+    table = _table(orc, K=K)
+    for _ in range(2):
+        op = [CP.random_op(r, t) for t in orc]
+        ccs = [CP.random_ccs(r) for _ in orc]
+        table, _, _ = table.change(op, ccs, [5] * G)
+    table, rings = _ring_marks(table, K)
+    op = [CP.random_op(r, t) for t in orc]
+    ccs = [CP.random_ccs(r) for _ in orc]
+    ref, err_ref, _ = table.change(op, ccs, [9] * G)
+    dev = table.t["off"].device
+    big = torch.zeros(table.t["infl_buf"].numel() + 1, dtype=torch.int64, device=dev)
+    big[1:] = table.t["infl_buf"]
+    table.t["infl_buf"] = big[1:]
+    assert table.t["infl_buf"].data_ptr() % 16 == 8
+    cap = int(ref.numpy()["off"][-1]) + 8
+    o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
+         "cfg": torch.empty(G, dtype=torch.int32, device=dev),
+         "ext": torch.empty(G, dtype=torch.int32, device=dev),
+         "err": torch.empty(G, dtype=torch.uint8, device=dev),
+         "err_id": torch.empty(G, dtype=torch.int64, device=dev),
+         "ids": torch.empty(cap, dtype=torch.int64, device=dev),
+         "match": torch.empty(cap, dtype=torch.int64, device=dev),
+         "next": torch.empty(cap, dtype=torch.int64, device=dev),
+         "pending_snapshot": torch.empty(cap, dtype=torch.int64, device=dev),
+         "pstate": torch.empty(cap, dtype=torch.uint8, device=dev),
+         "infl_pos": torch.empty(cap, dtype=torch.int32, device=dev)}
+    ob = torch.zeros(cap * K + 1, dtype=torch.int64, device=dev)
+    o["infl_buf"] = ob[1:]
+    got, err, _ = table.change(op, ccs, [9] * G, out=o)
+    assert np.array_equal(err, err_ref)
+    a, b = got.numpy(), ref.numpy()
+    for k in b:
+        assert np.array_equal(a[k], b[k]), k
+    _check_rings(got, rings, K)
+
+
+def test_wide_wave_owner_lookup():
+    """a wave of 64 groups whose slots exceed k_cc_move's owner
+    table (64 x QB_MAX_SLOTS): groups of 20 slots (5 voters, 15 learners) kept
+    as they are (no operation) and refused (a learner more breaks the engine's
+    16-member limit: the old slots stay) — every slot found by the binary
+    search and moved exactly, rings included."""
+    K = 3
+    G = 256
+
+    def tracker(g):
+        prs = {i: CC.Pr(match=0, next=10 + g, inflight_size=K) for i in range(1, 6)}
+        prs.update({i: CC.Pr(match=0, next=20 + g, is_learner=True, inflight_size=K)
+                    for i in range(100, 115)})
+        return CC.Tracker(set(range(1, 6)), None, set(range(100, 115)), None, False, prs, K)
+    orc = [tracker(g) for g in range(G)]
+    table, rings = _ring_marks(_table(orc, K=K), K)
+    before = table.numpy()
+    for op, ccs in ((0, []), (1, [(CC.ADD_LEARNER, 200)])):
+        got, err, _ = table.change([op] * G, [ccs] * G, [50] * G)
+        a = got.numpy()
+        assert int(a["off"][-1]) == 20 * G
+        assert (err == (15 if op else 0)).all()
+        for k in ("off", "ids", "cfg", "match", "next", "pstate"):
+            assert np.array_equal(a[k], before[k]), (op, k)
+        _check_rings(got, rings, K)
+
+
+def test_out_validation_refuses_bad_buffers():
+    """change(out=...) refuses, before any device write, an output
+    set with a short per-slot array or ring, a missing key, a host tensor, a
+    wrong element size, a non-contiguous view, or a buffer aliasing the
+    input table."""
+    import torch
+    from etcd_amd import _lib
+    r = random.Random(5)
+    G, K = 300, 4
+    orc = [CC.Tracker.empty(K) for _ in range(G)]
+    table = _table(orc, K=K)
+    op = [CP.random_op(r, t) for t in orc]
+    ccs = [CP.random_ccs(r) for _ in orc]
+    dev = table.t["off"].device
+    cap = 4 * G
+
+    def good():
+        o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
+             "cfg": torch.empty(G, dtype=torch.int32, device=dev),
+             "ext": torch.empty(G, dtype=torch.int32, device=dev),
+             "err": torch.empty(G, dtype=torch.uint8, device=dev),
+             "err_id": torch.empty(G, dtype=torch.int64, device=dev),
+             "pstate": torch.empty(cap, dtype=torch.uint8, device=dev),
+             "infl_pos": torch.empty(cap, dtype=torch.int32, device=dev),
+             "infl_buf": torch.empty(cap * K, dtype=torch.int64, device=dev)}
+        for k in ("ids", "match", "next", "pending_snapshot"):
+            o[k] = torch.empty(cap, dtype=torch.int64, device=dev)
+        return o
+    table.change(op, ccs, [3] * G, out=good())          # accepted
+    bad = []
+    o = good(); o["infl_buf"] = o["infl_buf"][: cap * K - 1]; bad.append(o)
+    bad.append(good()); del bad[-1]["err_id"]
+    o = good(); o["cfg"] = o["cfg"].cpu(); bad.append(o)
+    o = good(); o["infl_pos"] = o["infl_pos"].to(torch.int64); bad.append(o)
+    o = good(); o["ids"] = torch.empty(2 * cap, dtype=torch.int64, device=dev)[::2]; bad.append(o)
+    o = good(); o["match"] = table.t["match"]; bad.append(o)
+    o = good(); o["next"] = o["ids"]; bad.append(o)
+    o = good(); o["new_off"] = o["new_off"][:G]; bad.append(o)
+    for o in bad:
+        with pytest.raises(_lib.QuorumBatchError):
+            table.change(op, ccs, [3] * G, out=o)
+    # a shorter per-slot array sets the capacity: nothing past it is written
+    o = good()
+    o["match"] = torch.full((40,), -7, dtype=torch.int64, device=dev)
+    with pytest.raises(_lib.QuorumBatchError, match="capacity 40"):
+        table.change(op, ccs, [3] * G, out=o)
+    assert int(o["new_off"][G].item()) > 40
