@@ -447,8 +447,31 @@ def zipf_table(G: int, gen, dev):
     return cdf, torch.randperm(G, generator=gen, device=dev)
 
 
-def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7, skew="none"):
-    """nb distinct streaming batches (device tensors)."""
+# Group terms of the stream (--terms).  A raft group's term
+# grows by one per election or leader transfer (raft.go:747-748, 785), so a
+# massive multi-raft host holds groups of every age:
+#   wide   (default) log-uniform over [1, 2^20): floor(2^(20 u)), u uniform —
+#          about 45 % of the groups past 2045 (the compact record's term
+#          field, qb_bucket.h), from fresh groups to ones a million elections
+#          old;
+#   small  every group at term 7 (the stream of rounds 1-5);
+#   large  uniform over [20000, 2^20): every term past the field.
+# 1 % of each tick's records carry the group's term - 1 (stale).
+TRACKER_TERMS = ("wide", "small", "large")
+
+
+def tracker_group_terms(G: int, terms: str, gen, dev) -> torch.Tensor:
+    if terms == "small":
+        return torch.full((G,), 7, dtype=torch.int64, device=dev)
+    if terms == "large":
+        return torch.randint(20000, 1 << 20, (G,), generator=gen, device=dev, dtype=torch.int64)
+    u = torch.rand(G, generator=gen, device=dev, dtype=torch.float64)
+    return torch.exp2(20.0 * u).floor_().clamp_(1, (1 << 20) - 1).to(torch.int64)
+
+
+def tracker_batches(G, nb, last, n_slots_fn, gen, dev, gterm, skew="none"):
+    """nb distinct streaming batches (device tensors); ``gterm``: the group
+    terms (int64 [G])."""
     out = []
     zipf = zipf_table(G, gen, dev) if skew.startswith("zipf") else None
     for k in range(nb):
@@ -456,18 +479,20 @@ def tracker_batches(G, nb, last, n_slots_fn, gen, dev, seed_term=7, skew="none")
         slot = n_slots_fn(group, gen)
         lag = torch.randint(0, 96, (G,), generator=gen, device=dev, dtype=torch.int64)
         index = last[group.long()] + (k + 1) * TRACKER_E - lag
-        term = torch.where(torch.rand(G, generator=gen, device=dev) < 0.01, seed_term - 1,
-                           seed_term).to(torch.int64)
+        t = gterm[group.long()]
+        term = torch.where(torch.rand(G, generator=gen, device=dev) < 0.01, t - 1, t)
         out.append(batch.AppRespBatch(group, slot.to(torch.uint8), index, term))
     return out
 
 
-def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool, skew: str = "none"):
+def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool, skew: str = "none",
+                  terms: str = "wide"):
     """The configs[4] stream as the bench runs it: the leader state (after
     the initial maybeCommit, the leader's own match raised to the last of the
     nb * E entries it appended) and the nb device batches (``skew``: the
-    records' group distribution, SKEWS).  Returns (tracker, batches, info).
-    tests/ replays exactly this stream on the oracle."""
+    records' group distribution, SKEWS; ``terms``: the group terms,
+    TRACKER_TERMS).  Returns (tracker, batches, info).  tests/ replays
+    exactly this stream on the oracle."""
     n = 5
     gen = torch.Generator(device=dev)
     gen.manual_seed(TRACKER_SEED + 7919 * rank)
@@ -500,15 +525,18 @@ def tracker_setup(G: int, nb: int, rank: int, dev, csr: bool, skew: str = "none"
         def slots(group, g_):
             return torch.randint(1, n, group.shape, generator=g_, device=dev)
         slots_mean = voters_mean = float(n)
-    tr.term.fill_(7)
+    gterm = tracker_group_terms(G, terms, gen, dev)
+    tr.term.copy_(gterm)
     tr.commit_advance()
-    batches = tracker_batches(G, nb, last, slots, gen, dev, skew=skew)
+    batches = tracker_batches(G, nb, last, slots, gen, dev, gterm, skew=skew)
+    big = float((gterm >= 2046).double().mean().item())
     if csr:
         tr.match[first] = last + nb * TRACKER_E   # the leader appended nb*E entries
     else:
         tr.match[0].copy_(last + nb * TRACKER_E)
     torch.cuda.synchronize(dev)
-    return tr, batches, {"slots_mean": slots_mean, "voters_mean": voters_mean, "gen": gen}
+    return tr, batches, {"slots_mean": slots_mean, "voters_mean": voters_mean, "gen": gen,
+                         "terms_past_field": big}
 
 
 def tracker_host_state(tr, csr: bool, Gs: int, g0: int = 0):
@@ -561,7 +589,7 @@ def parity_windows(G: int, Gs: int):
     return [(0, w), ((G - w) // 2, w), (G - w, w)]
 
 
-def tracker_cpu_baseline(seconds: float, csr: bool):
+def tracker_cpu_baseline(seconds: float, csr: bool, terms: str = "wide"):
     """The oracle's sequential stepLeader restatement (one record at a time in
     batch order: term filter, MaybeUpdate, maybeCommit when updated;
     oracle/quorum_oracle.c appresp_range) on a bounded sample of the same
@@ -581,6 +609,12 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
     else:
         m0, _, _, ts0 = oc.gen_fixed(TRACKER_SEED, n, Gs)
         last = m0[0].copy()
+    if terms == "small":
+        gterm = np.full(Gs, 7, np.uint64)
+    elif terms == "large":
+        gterm = rng.integers(20000, 1 << 20, size=Gs).astype(np.uint64)
+    else:
+        gterm = np.clip(np.floor(np.exp2(20.0 * rng.random(Gs))), 1, (1 << 20) - 1).astype(np.uint64)
     batches = []
     for k in range(R):
         grp = rng.integers(0, Gs, size=Gs).astype(np.uint32)
@@ -590,7 +624,7 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
             slot = rng.integers(1, n, size=Gs).astype(np.uint8)
         lag = rng.integers(0, 96, size=Gs).astype(np.uint64)
         idx = last[grp] + np.uint64((k + 1) * TRACKER_E) - lag
-        trm = np.where(rng.random(Gs) < 0.01, 6, 7).astype(np.uint64)
+        trm = np.where(rng.random(Gs) < 0.01, gterm[grp] - np.uint64(1), gterm[grp]).astype(np.uint64)
         batches.append((grp, slot, idx, trm))
     m_start = m0.copy()
     if csr:
@@ -600,7 +634,7 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
 
     def fresh():
         st = {"match": m_start.copy(), "active": np.zeros(Gs, np.uint16),
-              "term": np.full(Gs, 7, np.uint64), "term_start": ts0.copy(),
+              "term": gterm.copy(), "term_start": ts0.copy(),
               "committed": np.zeros(Gs, np.uint64), "stepped_down": np.zeros(Gs, np.uint8)}
         if csr:
             oc.csr_commit_all(off, cfg, st["match"], ts0, st["committed"])
@@ -632,7 +666,8 @@ def tracker_cpu_baseline(seconds: float, csr: bool):
                        f"threads (every CPU the process may use: affinity {info['affinity_cpus']}, "
                        f"cgroup quota {info['cgroup_cpu_quota']}; GOMAXPROCS-equivalent {N}; "
                        f"groups partitioned, records stably partitioned by owner); 1 thread: "
-                       f"{r1:.4g} group-steps/s over {p1} passes; sequential C restatement of "
+                       f"{r1:.4g} group-steps/s over {p1} passes; group terms {terms} as the "
+                       f"GPU stream; sequential C restatement of "
                        f"stepLeader's MsgAppResp path (oracle/quorum_oracle.c)"),
             "value_1thread": r1}
 
@@ -740,10 +775,11 @@ def tracker_main(args, world, rank, dev, barrier):
     W = args.warmup if args.warmup is not None else 4
     nb = W + K
     skew = getattr(args, "skew", "none") or "none"
+    terms = getattr(args, "terms", "wide") or "wide"
     if nb > TRACKER_MAX_BATCHES:
         raise SystemExit(f"--workload {args.workload} keeps one distinct batch per step resident: "
                          f"--steps + --warmup must be <= {TRACKER_MAX_BATCHES}")
-    tr, batches, info = tracker_setup(G, nb, rank, dev, csr, skew)
+    tr, batches, info = tracker_setup(G, nb, rank, dev, csr, skew, terms)
     gen = info["gen"]
     snap = {k: getattr(tr, k).clone() for k in TRACKER_STATE}
     # the whole shard at N = 1; with N ranks sharing the node's CPUs, each
@@ -846,7 +882,7 @@ def tracker_main(args, world, rank, dev, barrier):
         # match 8 each (learners ack but do not count), term_start 8,
         # committed 8 read + 8 written
         bpg = 21 + 16 + 4 + 4 + 8 * info["voters_mean"] + 8 + 8 + 8
-    key = f"tracker{'_csr' if csr else ''}_n5_G{G}"
+    key = f"tracker{'_csr' if csr else ''}_n5_G{G}" + ("" if terms == "small" else f"_{terms}")
     achieved = bpg * G / step_s / 1e9
     kern = ("memset, k_bk_scatter<true> (reserved regions), k_bk_split_compact, "
             + ("k_csr_apply<WMAX,8,false>, k_csr_apply_deferred, k_bk_slow<CsrLay<WMAX>>" if csr
@@ -863,7 +899,12 @@ def tracker_main(args, world, rank, dev, barrier):
         "config": {"workload": ("BASELINE configs[4]: streaming ProgressTracker, batched MsgAppResp "
                                 "scatter-max + commit advance, 16M groups per GPU (128M over 8)"
                                 + (" — ragged CSR groups (3-9 voters + 0-2 learners)" if csr
-                                   else ", 5 voters")),
+                                   else ", 5 voters")
+                                + {"wide": "; group terms log-uniform over [1, 2^20) (raft terms "
+                                           "of groups of every age, ~45 % past 2045)",
+                                   "small": "; every group term 7",
+                                   "large": "; group terms uniform over [20000, 2^20)"}[terms]),
+                   "group_terms": terms, "terms_past_record_field": info["terms_past_field"],
                    "groups_per_gpu": G, "records_per_step": G, "new_entries_per_step": TRACKER_E,
                    "stale_term_fraction": 0.01, "mean_slots": info["slots_mean"],
                    "mean_voters": info["voters_mean"],
@@ -891,7 +932,7 @@ def tracker_main(args, world, rank, dev, barrier):
         "value_per_rank": per_rank,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr)
+        out["cpu_baseline"] = tracker_cpu_baseline(args.cpu_seconds, csr, terms)
     return parity, out
 
 
@@ -1530,6 +1571,9 @@ def parse_args(argv=None):
     ap.add_argument("--lab-lib", default=None,
                     help="A/B lab runs: bind this build of libquorumbatch.so instead of the "
                          "in-tree one (etcd_amd._lib.use_lab_library)")
+    ap.add_argument("--terms", default="wide", choices=list(TRACKER_TERMS),
+                    help="configs[4] group terms: wide (log-uniform [1, 2^20), default), small "
+                         "(all 7, rounds 1-5), large ([20000, 2^20))")
     ap.add_argument("--skew", default="none", choices=list(SKEWS),
                     help="tracker workloads: the records' group distribution (SKEWS: zipf = "
                          "Zipf(1.1) over groups, zipf-capped = at most 4 x 512 records per group, "

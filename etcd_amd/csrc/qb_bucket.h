@@ -33,16 +33,23 @@ constexpr int kShards = 256;         // stat counter shards (one 64-byte line ea
 //   bit lgb + slb            reject
 //   [lgb + slb + 1, 24)      term (tb = 23 - lgb - slb bits: 10 or 11)
 //   [24, 64)                 index (40 bits)
-// A record whose index >= 2^40 or whose term does not fit tb bits is an
-// escape: its term field is all ones and the index field holds the record's
-// batch position, from which K5 reads the exact index and term in the
-// original batch — or, in a K3 tile most of whose records escape (a stream
-// of terms >= 1023), kEscColumn | its buf1 position, where K3 wrote them in
-// the escape column (whole lines: the tile's runs).  Raft indexes below
-// 2^40 and terms below 1023 keep every record in 8 bytes; an escape costs K5
-// two 8-byte gathers (or one 16-byte read beside its neighbours), never a
-// wrong answer.  (Round 2's packed form moved index + meta|term32, 16 bytes, four
-// times per record: K3 write, K4 read + write, K5 read.)
+// The term field holds the term itself below tside() = 2^tb - 2 (1022 or
+// 2046).  Round 6: a larger term below 2^32 - 1 with an
+// index below 2^40 is a SIDE record — term field tside(), the index in the
+// record, the term as a u32 in the side column at the record's position
+// (Cols::side), carried through K4 beside the record — whenever its K3 tile
+// has at least 1/8 of such records (kSideDen: a stream of realistic, long-
+// lived terms); the side column then moves 4 bytes per record per level,
+// in whole lines.  Anything else that does not fit (an index >= 2^40, a term
+// >= 2^32 - 1, or a large term in a tile where they are rare) is an ESCAPE:
+// term field tesc() = all ones, the index field the record's batch position,
+// from which K5 reads the exact index and term in the original batch (two
+// 8-byte gathers).  Raft indexes below 2^40 and terms below 1022 keep every
+// record in 8 bytes; never a wrong answer.  (Round 5 wrote an escape-dense
+// tile's exact (index, term) pairs to a 16-byte escape column at the buf1
+// position, which K5 gathered across the region: a tick of terms >= 1023 cost
+// 1.43x a small-term tick.  Round 2's packed form moved index + meta|term32,
+// 16 bytes, four times per record: K3 write, K4 read + write, K5 read.)
 struct Cols {
   u64* index;
   u64* term;
@@ -50,8 +57,15 @@ struct Cols {
   u32* term32;
   u8* cl;        // compact: chunk-low of each record (K3 -> K4)
   u32 compact;
+  u32* side;     // compact: the side column (a side record's u32 term at its position)
+  u32* sflag;    // compact: the call's flag word, nonzero once a K3 tile wrote side records
 };
 constexpr u32 kTermEscape = 0xFFFFFFFFu;
+// A K3 tile writes side records (and the side column for all its records)
+// when more than 1/kSideDen of its records escape: then the escapes' gathers
+// cost K5 more than the column costs K3-K5 (at 100 %: ~490 us vs ~50 us per
+// 16M-record tick).
+constexpr u32 kSideDen = 8;
 // chunk_slow values: 1 = slow (k_bk_slow applies the chunk from the batch),
 // 2 = deferred to the CSR step's second launch, 3 = a record of the chunk
 // found no place (K3: the overflow pool was exhausted — never with the
@@ -63,17 +77,41 @@ __host__ __device__ __forceinline__ u32 term_to32(u64 t) {
 }
 constexpr u32 kIndexBits = 40;
 constexpr u32 kRecHdrBits = 24;  // lg | slot | reject | term
+// a side record's term and its index both fit the side form
+__device__ __forceinline__ bool side_fits(u64 index, u64 term) {
+  return (index >> kIndexBits) == 0 && term < u64(kTermEscape);
+}
 struct RecFmt {
   u32 lgb, slb, tb;
   __host__ __device__ u32 rej_shift() const { return lgb + slb; }
   __host__ __device__ u32 term_shift() const { return lgb + slb + 1; }
   __host__ __device__ u32 tesc() const { return (1u << tb) - 1u; }
+  __host__ __device__ u32 tside() const { return (1u << tb) - 2u; }
+  // (a large term is encoded as an escape here; K3 turns it into a side
+  // record in a tile dense with them)
   __device__ __forceinline__ u64 encode(u32 lg, u32 slot, bool rej, u64 index, u64 term,
                                         u32 ridx) const {
-    const bool esc = term >= u64(tesc()) || (index >> kIndexBits) != 0;
+    const bool esc = term >= u64(tside()) || (index >> kIndexBits) != 0;
     const u64 hdr = u64(lg) | (u64(slot) << lgb) | (u64(rej) << rej_shift()) |
                     (u64(esc ? tesc() : u32(term)) << term_shift());
     return hdr | ((esc ? u64(ridx) : index) << kRecHdrBits);
+  }
+  // K3 (round 6): a term past the field with an index and term that fit the
+  // side form is encoded as a side record up front (term field tside(), the
+  // index in the record); a tile that turns out not dense with them turns
+  // them back into escapes (to_escape) — the raw columns die in the first pass
+  __device__ __forceinline__ u64 encode_side(u32 lg, u32 slot, bool rej, u64 index, u64 term,
+                                             u32 ridx) const {
+    const bool iok = (index >> kIndexBits) == 0;
+    const bool inl = iok && term < u64(tside());
+    const bool sf = iok && !inl && term < u64(kTermEscape);
+    const u32 tf = inl ? u32(term) : sf ? tside() : tesc();
+    const u64 hdr = u64(lg) | (u64(slot) << lgb) | (u64(rej) << rej_shift()) | (u64(tf) << term_shift());
+    return hdr | ((inl || sf ? index : u64(ridx)) << kRecHdrBits);
+  }
+  __device__ __forceinline__ u64 to_escape(u64 r, u32 ridx) const {
+    return (r & ((1ull << term_shift()) - 1ull)) | (u64(tesc()) << term_shift()) |
+           (u64(ridx) << kRecHdrBits);
   }
   __device__ __forceinline__ u32 lg(u64 r) const { return u32(r) & ((1u << lgb) - 1u); }
   __device__ __forceinline__ u32 slot(u64 r) const { return (u32(r) >> lgb) & ((1u << slb) - 1u); }
@@ -301,7 +339,7 @@ inline Geometry geometry(u32 n, u64 G, u64 M, u32 ch = 0, bool il = false) {
 // zeroed by one memset per call (bucket_records).
 struct Carve {
   size_t shards, flags, counts, chunk_flags, ptab, sbflag, ext, user, zero_end, owner, heavy,
-      side_idx, side_tc, chunk_start, buf1, buf2, cl, esc, total;
+      side_idx, side_tc, chunk_start, buf1, buf2, cl, side1, side2, total;
   u64 nside;   // dedup side-table entries (compact form: kDedupSlots per chunk-start row)
   u64 nrec;    // records of the region grid (pool part 0 starts here)
   u64 nrec_all;  // records per column of buf1 / buf2: the region grid + the pool
@@ -314,6 +352,7 @@ inline size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 // region grid followed by the overflow pool (Pool).
 constexpr u32 kFlagPoolCtr = 2;  // flag word: pool parts drawn
 constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions overflowed
+constexpr u32 kFlagSide = 4;      // flag word: a K3 tile wrote side records (Cols::sflag)
 // K4 dedup (compact form, round 5): a chunk's run of at least kHeavyRun
 // records in one part (a hot group: an even batch puts ~32 records of a chunk
 // in a part; a batch capped at raft's 4 x 512 in-flight acks per group per
@@ -327,15 +366,16 @@ constexpr u32 kFlagHeavyCtr = 3;  // flag word: super-buckets whose regions over
 // K5 applies it as `count` records of that class (MaybeUpdate is a max, the
 // RecentActive bit an or; batch order only matters in a chunk with a
 // higher-term record, which still goes to the slow path, which re-reads the
-// original batch).  Escape payloads (batch positions, or kEscColumn | a buf1
-// position) stay below 2^39.
+// original batch).  Escape payloads (batch positions) stay below 2^32.
+// Side records fold too (round 6): K4 reads the side term and the group term
+// and folds a side record equal to its group's term under term code
+// kTermIsGroup (K5 reads the group term back for it), a stale one as term 0
+// (stale against any group term it is below); a higher one is not folded.
 constexpr u32 kHeavyRun = 2048;
 constexpr u32 kDedupSlots = 256;
 constexpr u64 kDedupFlag = 1ull << 39;
-// An escape of an escape-dense K3 tile: payload = kEscColumn | its buf1
-// position, its exact index and term in the escape column there.
-constexpr u64 kEscColumn = 1ull << 38;
 constexpr u32 kDedupCountShift = 12;
+constexpr u32 kTermIsGroup = (1u << kDedupCountShift) - 1u;  // side_tc term code
 constexpr u32 kExtClasses = 4;  // stale, applied, rejected, non-member
 inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   Carve c{};
@@ -369,9 +409,9 @@ inline Carve carve(const Geometry& g, int ncols = 3, size_t user = 0) {
   c.buf1 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.buf2 = o;  o += ncols * up256(sizeof(u64) * nrec);
   c.cl = o;  o += ncols == 1 ? up256(nrec) : 0;
-  // compact form: the escape column — an escape's exact (index, term) at its
-  // buf1 position, written by K3 for escape-dense tiles only
-  c.esc = o;  o += ncols == 1 ? up256(2 * sizeof(u64) * nrec) : 0;
+  // compact form: the side columns beside buf1 (K3 -> K4) and buf2 (K4 -> K5)
+  c.side1 = o;  o += ncols == 1 ? up256(sizeof(u32) * nrec) : 0;
+  c.side2 = o;  o += ncols == 1 ? up256(sizeof(u32) * nrec) : 0;
   c.total = o;
   return c;
 }
@@ -408,16 +448,19 @@ inline Side side_at(char* ws, const Carve& c, const u64* group_term = nullptr,
 
 inline Cols cols_at(char* base, u64 M, int ncols = 3) {
   const size_t col = up256(sizeof(u64) * (M ? M : 1));
-  if (ncols == 1) return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, nullptr, 0};
+  if (ncols == 1)
+    return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, nullptr, 0, nullptr, nullptr};
   return Cols{reinterpret_cast<u64*>(base), reinterpret_cast<u64*>(base + col),
-              reinterpret_cast<u64*>(base + 2 * col), nullptr, nullptr, 0};
+              reinterpret_cast<u64*>(base + 2 * col), nullptr, nullptr, 0, nullptr, nullptr};
 }
 // The compact form's columns: the u64 records at `base`, the chunk-low bytes
-// at `cl` and the escape column at `esc` (K3's output only; K4's output needs
-// neither).
-inline Cols compact_at(char* base, char* cl, char* esc = nullptr) {
-  return Cols{reinterpret_cast<u64*>(esc), nullptr, reinterpret_cast<u64*>(base), nullptr,
-              reinterpret_cast<u8*>(cl), 1};
+// at `cl` (K3's output only), the side column at `side` and the flag word.
+inline Cols compact_at(char* base, char* cl, char* side, u32* sflag) {
+  return Cols{nullptr, nullptr, reinterpret_cast<u64*>(base), nullptr, reinterpret_cast<u8*>(cl),
+              1, reinterpret_cast<u32*>(side), sflag};
+}
+inline u32* side_flag_at(char* ws, const Carve& c) {
+  return reinterpret_cast<u32*>(ws + c.flags) + kFlagSide;
 }
 
 

@@ -206,6 +206,7 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   u32 bj[kPer], rj[kPer];
   u64 vj[kPer];
   u32 nbad = 0, nnon = 0;  // wave-uniform: invalid records
+  u32 mside = 0;           // compact: side-form records (staged terms at their tile index)
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = rk(j);
@@ -224,10 +225,19 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
       }
     }
     bj[j] |= geo.cl_of_chunk(geo.chunk_of(g[j])) << 16;
-    if constexpr (COMPACT)
-      vj[j] = geo.fmt.encode(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j], vt[j],
-                             u32(t0 + k));
+    if constexpr (COMPACT) {
+      vj[j] = geo.fmt.encode_side(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j],
+                                  vt[j], u32(t0 + k));
+      // a side record's term, staged at its tile index in the (not yet
+      // used) record stage
+      if (ok && geo.fmt.term(vj[j]) == geo.fmt.tside()) {
+        reinterpret_cast<u32*>(L.stage)[k] = u32(vt[j]);
+        ++mside;
+      }
+    }
   }
+  if constexpr (COMPACT)
+    if (mside) atomicAdd(&s_nesc, mside);
   __syncthreads();
   for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
     const u32 nbin = start[b];
@@ -252,54 +262,44 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   }
   const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
   if constexpr (COMPACT) {
+    // A tile where side records are not rare (more than 1/kSideDen of its
+    // records: a stream of terms past the record's term field) keeps them —
+    // the index in the record, the term in the side column at the record's
+    // position — and writes the side column for every record of the tile, so
+    // the column's lines are whole (the tile's runs); K4 carries it beside
+    // the records and K5 reads it with them (round 5 gathered such records'
+    // index and term from the batch: 1.43x the tick of small terms).  A tile
+    // where they are rare turns them into escapes (no column writes: partial
+    // lines cost more than a few records' gathers).
+    const bool side = s_nesc * kSideDen > nvalid;  // (block-uniform)
+    u32* t32 = reinterpret_cast<u32*>(L.rank);     // (rank + perm: unused by this form)
+    u32 tj[kPer];
+    if (side) {  // the staged terms, read before the stage is overwritten below
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        tj[j] = (bj[j] & 0xFFFFu) != u32(kNoBin) && geo.fmt.term(vj[j]) == geo.fmt.tside()
+                    ? reinterpret_cast<const u32*>(L.stage)[rk(j)]
+                    : 0u;
+      __syncthreads();
+    }
     // after the scan each record is stored at its sorted LDS slot with its
-    // bin and chunk-low, and the output pass reads the slots in order
-    u32 mesc = 0;
+    // bin and chunk-low (and, side, its term), and the output pass reads the
+    // slots in order
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const u32 b = bj[j] & 0xFFFFu;
       if (b == u32(kNoBin)) continue;
       const u32 e = start[b] + rj[j];
-      L.stage[e] = vj[j];
+      u64 v = vj[j];
+      if (!side && geo.fmt.term(v) == geo.fmt.tside()) v = geo.fmt.to_escape(v, u32(t0 + rk(j)));
+      L.stage[e] = v;
       L.bin[e] = u16(b);
       L.cl[e] = u8(bj[j] >> 16);
-      mesc += geo.fmt.term(vj[j]) == geo.fmt.tesc();
+      if (side) t32[e] = tj[j];
     }
-    if (mesc) atomicAdd(&s_nesc, mesc);
     __syncthreads();
+    if (side && threadIdx.x == 0) *out.sflag = 1u;
     const u32 x = blockIdx.x % kRegionShards;
-    if (2 * s_nesc > nvalid) {  // (block-uniform)
-      // A tile most of whose records escape (terms past the record's term
-      // field, indexes >= 2^40): each escape's exact index and term go to
-      // the escape column at the record's own position — lines the tile's
-      // runs fill — read back from this tile's batch lines (L2 hits), and
-      // the record's payload becomes that position with kEscColumn.  K5
-      // then reads the pair beside the region's other records instead of
-      // two random gathers from the batch (a stream whose every term is
-      // >= 1023: 1053 -> ~810 us per 16M-record tick).  A tile of rare
-      // escapes keeps the batch position: scattered 16-byte column stores
-      // (partial lines) cost K3 and K5 ~20 us each at 1 % escapes.
-      for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
-        const u32 b = L.bin[e];
-        const u32 gs = gstart[b];
-        const u32 rel = gs + (e - start[b]);
-        const u64 d = rel < geo.cap ? u64(b * kRegionShards + x) * geo.cap + rel
-                                    : region_dst(geo, pool, b, x, rel, gs, pid0[b], pid1[b]);
-        if (d == ~0ull) {
-          chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
-          continue;
-        }
-        u64 v = L.stage[e];
-        if (geo.fmt.term(v) == geo.fmt.tesc()) {
-          const u32 bp = u32(v >> kRecHdrBits);
-          *reinterpret_cast<ulonglong2*>(out.index + 2 * d) = ulonglong2{ri[bp], rt[bp]};
-          v = (v & ((1ull << kRecHdrBits) - 1ull)) | ((d | kEscColumn) << kRecHdrBits);
-        }
-        out.mr[d] = v;
-        out.cl[d] = L.cl[e];
-      }
-      return;
-    }
     for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
       const u32 b = L.bin[e];
       const u32 gs = gstart[b];
@@ -309,6 +309,7 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
       if (d != ~0ull) {
         out.mr[d] = L.stage[e];
         out.cl[d] = L.cl[e];
+        if (side) out.side[d] = t32[e];
       } else {  // no pool part (never with the carve's sizing): the exact slow path
         chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
       }
@@ -532,7 +533,7 @@ __device__ __forceinline__ u32 bin_of(const u32* start, u32 e) {
 __device__ __forceinline__ void dedup_compact_part(const Geometry& geo, Cols out,
                                                    u32* __restrict__ cs, u32 lo, u32 nrec, u64 row,
                                                    u32 sb, Side side, const u64* stage, u32* start,
-                                                   u32* wsum) {
+                                                   u32* wsum, bool sided) {
   const RecFmt fmt = geo.fmt;
   __shared__ u32 hkey[kDedupSlots];
   __shared__ u64 hmax[kDedupSlots];
@@ -546,16 +547,34 @@ __device__ __forceinline__ void dedup_compact_part(const Geometry& geo, Cols out
   }
   if (threadIdx.x <= kChunksPerSb) cnt2[threadIdx.x] = 0;
   __syncthreads();
+  const u32 hmask = (1u << kRecHdrBits) - 1u;
+  const u32 ts = fmt.term_shift();
   u32 keep = 0;  // bit j: position threadIdx.x + j * kSplitThreads stays a record of its own
+  u32 ksv[kSplitPer];  // the side word of each position (sided calls), moved with a kept record
   for (u32 j = 0; j < u32(kSplitPer); ++j) {
     const u32 e = threadIdx.x + j * kSplitThreads;
+    ksv[j] = 0;
     if (e >= nrec) break;
     const u32 b = bin_of(start, e);
     const u32 nb = (b + 1 < kChunksPerSb ? start[b + 1] : nrec) - start[b];
     const u64 v = stage[e];
+    // (the placement above wrote this workgroup's side words before its
+    // barrier; no wave read these lines earlier in this launch)
+    if (sided) ksv[j] = out.side[lo + e];
     bool merged = false;
-    if (nb >= kHeavyRun && fmt.term(v) != fmt.tesc()) {
-      const u32 key = (b << kRecHdrBits) | (u32(v) & ((1u << kRecHdrBits) - 1u));
+    u32 hdr = u32(v) & hmask;
+    bool foldable = nb >= kHeavyRun && fmt.term(v) != fmt.tesc();
+    if (foldable && fmt.term(v) == fmt.tside()) {
+      // a side record: folded under the term code kTermIsGroup when its term
+      // is the group's, as a term-0 record (stale either way) when below it;
+      // a higher one stays (its chunk goes to the slow path)
+      const u64 g = u64(geo.chunk_of_sb_cl(sb, b)) * geo.CH + fmt.lg(v);
+      const u64 gt = side.group_term[g];
+      if (u64(ksv[j]) < gt) hdr &= (1u << ts) - 1u;
+      else foldable = u64(ksv[j]) == gt;
+    }
+    if (foldable) {
+      const u32 key = (b << kRecHdrBits) | hdr;
       const u32 h = (key * 2654435761u) >> 24;
       for (u32 q = 0; q < 8 && !merged; ++q) {
         const u32 sl = (h + q) & (kDedupSlots - 1u);
@@ -580,40 +599,45 @@ __device__ __forceinline__ void dedup_compact_part(const Geometry& geo, Cols out
   if (threadIdx.x <= kChunksPerSb)
     cs[row * (kChunksPerSb + 1) + threadIdx.x] =
         lo + (threadIdx.x < kChunksPerSb ? cnt2[threadIdx.x] : total);
-  __syncthreads();  // (cnt2 is a placement cursor from here on)
+  __syncthreads();  // (cnt2 is a placement cursor from here on; every side word is read)
   for (u32 j = 0; j < u32(kSplitPer); ++j) {
     const u32 e = threadIdx.x + j * kSplitThreads;
     if (e >= nrec) break;
     if (!((keep >> j) & 1u)) continue;
-    out.mr[lo + atomicAdd(&cnt2[bin_of(start, e)], 1u)] = stage[e];
+    const u32 p = lo + atomicAdd(&cnt2[bin_of(start, e)], 1u);
+    out.mr[p] = stage[e];
+    if (sided) out.side[p] = ksv[j];
   }
   if (hk != kEmpty) {
     const u32 n = hcnt[threadIdx.x];
-    const u64 mx = hmax[threadIdx.x], hdr = hk & ((1u << kRecHdrBits) - 1u);
-    u64 rec = hdr | (mx << kRecHdrBits);  // a single record: itself
+    const u64 mx = hmax[threadIdx.x], hdr = hk & hmask;
+    const u32 t = fmt.term(hdr);
+    const u32 c = geo.chunk_of_sb_cl(sb, hk >> kRecHdrBits);
+    const u64 g = u64(c) * geo.CH + fmt.lg(hdr);
+    const u64 gt = side.group_term[g];
+    u64 rec = hdr | (mx << kRecHdrBits);  // a single record: itself (a side one: term gt)
     if (n > 1) {
       const u64 si = row * kDedupSlots + threadIdx.x;
-      const u32 t = fmt.term(hdr);
       side.idx[si] = mx;
-      side.tc[si] = t | (n << kDedupCountShift);
-      const u64 tmask = u64(fmt.tesc()) << fmt.term_shift();
+      side.tc[si] = (t == fmt.tside() ? kTermIsGroup : t) | (n << kDedupCountShift);
+      const u64 tmask = u64(fmt.tesc()) << ts;
       rec = (hdr & ~tmask) | tmask | ((si | kDedupFlag) << kRecHdrBits);
       // the n - 1 records folded away, in the class K5 gives the record that
       // stands for them (a higher term sends the chunk to the slow path,
       // which counts every record itself: nothing to add)
-      const u32 c = geo.chunk_of_sb_cl(sb, hk >> kRecHdrBits);
-      const u64 g = u64(c) * geo.CH + fmt.lg(hdr);
       const u32 s = fmt.slot(hdr);
       u32 cls = 4;  // none
       if (side.off && s >= side.off[g + 1] - side.off[g]) {
         cls = 3;  // non-member (CSR: raft.go:1100-1104)
       } else {
-        const u64 gt = side.group_term[g];
-        cls = u64(t) < gt ? 0u : u64(t) > gt ? 4u : fmt.rej(hdr) ? 2u : 1u;
+        const u64 tt = t == fmt.tside() ? gt : u64(t);
+        cls = tt < gt ? 0u : tt > gt ? 4u : fmt.rej(hdr) ? 2u : 1u;
       }
       if (cls < kExtClasses) atomicAdd(&side.ext[u64(c) * kExtClasses + cls], n - 1u);
     }
-    out.mr[lo + atomicAdd(&cnt2[hk >> kRecHdrBits], 1u)] = rec;
+    const u32 p = lo + atomicAdd(&cnt2[hk >> kRecHdrBits], 1u);
+    out.mr[p] = rec;
+    if (sided) out.side[p] = u32(gt);  // (read only for a single side record: its term)
   }
 }
 
@@ -623,6 +647,9 @@ __device__ __forceinline__ void split_compact_part(const Geometry& geo, Cols in,
   __shared__ u64 stage[kTile];
   __shared__ u32 start[kChunksPerSb];
   __shared__ u32 wsum[kSplitThreads / 64];
+  // side records anywhere in this call (K3's flag word): the side column
+  // moves with the records, every position of the part written (whole lines)
+  const bool sided = *in.sflag != 0u;
   u64 vm[kSplitPer];  // loaded together: one round trip
   u32 vc[kSplitPer];
 #pragma unroll
@@ -633,11 +660,12 @@ __device__ __forceinline__ void split_compact_part(const Geometry& geo, Cols in,
   }
   if (threadIdx.x < kChunksPerSb) start[threadIdx.x] = 0;
   __syncthreads();
-  u32 rk[kSplitPer];
+  // (each record's rank rides in its chunk-low word: vc = chunk-low | rank << 8,
+  // so the side words cost no registers past the kernel's 64)
 #pragma unroll
   for (int j = 0; j < kSplitPer; ++j) {
     const u32 k = threadIdx.x + j * kSplitThreads;
-    rk[j] = k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u;
+    vc[j] |= (k < nrec ? atomicAdd(&start[vc[j]], 1u) : 0u) << 8;
   }
   // a chunk with >= kHeavyRun records in this part (a hot group): the dedup
   // pass below (rare; block-uniform)
@@ -652,14 +680,45 @@ __device__ __forceinline__ void split_compact_part(const Geometry& geo, Cols in,
 #pragma unroll
   for (int j = 0; j < kSplitPer; ++j) {
     const u32 k = threadIdx.x + j * kSplitThreads;
-    if (k < nrec) stage[start[vc[j]] + rk[j]] = vm[j];
+    if (k < nrec) stage[start[vc[j] & 0xFFu] + (vc[j] >> 8)] = vm[j];
   }
-  __syncthreads();
-  if (heavy) {
-    dedup_compact_part(geo, out, cs, lo, nrec, row, sb, side, stage, start, wsum);
+  if (heavy) {  // (rare) the side words go to their sorted positions directly
+    if (sided) {
+#pragma unroll
+      for (int j = 0; j < kSplitPer; ++j) {
+        const u32 k = threadIdx.x + j * kSplitThreads;
+        if (k < nrec) out.side[lo + start[vc[j] & 0xFFu] + (vc[j] >> 8)] = in.side[lo + k];
+      }
+    }
+    __syncthreads();
+    dedup_compact_part(geo, out, cs, lo, nrec, row, sb, side, stage, start, wsum, sided);
     return;
   }
+  // the side words (block-uniform), loaded once the records' registers are
+  // free; their latency runs under the record stores below
+  u32 sv[kSplitPer];
+  if (sided) {
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j) {
+      const u32 k = threadIdx.x + j * kSplitThreads;
+      sv[j] = k < nrec ? in.side[lo + k] : 0u;
+    }
+  }
+  __syncthreads();
   for (u32 e = threadIdx.x; e < nrec; e += kSplitThreads) out.mr[lo + e] = stage[e];
+  if (sided) {
+    // sorted through the records' LDS (now read): scattered LDS stores, then
+    // coalesced global ones (scattered 4-byte global stores cost K4 ~2x)
+    u32* s32 = reinterpret_cast<u32*>(stage);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j) {
+      const u32 k = threadIdx.x + j * kSplitThreads;
+      if (k < nrec) s32[start[vc[j] & 0xFFu] + (vc[j] >> 8)] = sv[j];
+    }
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < nrec; e += kSplitThreads) out.side[lo + e] = s32[e];
+  }
 }
 
 // (the dedup path's registers would otherwise cost the common path its
@@ -678,9 +737,9 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_split_
 
 // ---------------------------------------------------------------- K5 ----
 // Records arrive compact (one u64 each, RecFmt: lg, slot, reject, term,
-// index; an escape record carries its batch position and K5 reads its exact
-// index and term from the original batch — or, from an escape-dense K3 tile,
-// its buf1 position with kEscColumn and K5 reads them from the escape column).  A chunk none of whose records is
+// index; a side record's term is the u32 at its position in the side column,
+// read with the record; an escape record carries its batch position and K5
+// reads its exact index and term from the original batch).  A chunk none of whose records is
 // above its group's term (the steady state) is applied here.  A chunk with a
 // higher-term record (the sequential leader steps down there and ignores what
 // follows, raft.go:875-879: batch order matters) is "slow": K5 leaves its
@@ -736,6 +795,9 @@ __device__ __forceinline__ void apply_chunk(
   // with the run table's loads, tested once the table is built)
   const u32 hf = skip_heavy ? hv.sbflag[sb] : 0u;
   const bool heavy_sb = hf != 0u && hf - 1u < hv.blocks / kChunksPerSb;
+  // side records in this call (K3's flag word): their side words are read
+  // with the records
+  const bool sided = *recs.sflag != 0u;
   // the records K4's dedup folded away (stale, applied, rejected)
   const u32 extv = esc.side.ext[u64(c) * kExtClasses + (threadIdx.x & 3u)];
   u64 gtr[GPT];
@@ -779,6 +841,7 @@ __device__ __forceinline__ void apply_chunk(
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
+  u32 srec[kRecPer];  // side words (a call with side records: K3's flag)
   // branch-free (clamped; an empty chunk reads record 0, which exists)
   auto fetch = [&](u32 f0, u32 tot) {
     u32 ix[kRecPer];
@@ -789,6 +852,8 @@ __device__ __forceinline__ void apply_chunk(
     }
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
+#pragma unroll
+    for (int r = 0; r < kRecPer; ++r) srec[r] = sided ? recs.side[ix[r]] : 0u;
   };
   auto apply = [&](u32 f0, u32 tot) {
 #pragma unroll
@@ -799,10 +864,11 @@ __device__ __forceinline__ void apply_chunk(
         const u64 x = rec[r];
         const u32 lg = fmt.lg(x), s = fmt.slot(x);
         u64 t = fmt.term(x), idx = fmt.payload(x);
-        // escape: the exact values from the batch, or a folded record's from
-        // the side table
-        if (t == fmt.tesc()) unescape(esc, t, idx);
         const u64 gt = gterm[lg];
+        // a side record: its term from the side column; an escape: the exact
+        // values from the batch, or a folded record's from the side table
+        if (t == fmt.tside()) t = srec[r];
+        else if (t == fmt.tesc()) unescape(esc, t, idx, gt);
         if (t > gt) {
           slow = 1;  // higher term: step-down order (raft.go:875-879)
         } else if (t < gt) {
@@ -829,7 +895,7 @@ __device__ __forceinline__ void apply_chunk(
   fetch(0, total);
   // pinned: the records are loaded here, not sunk into apply's branches
 #pragma unroll
-  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]), "+v"(srec[r]));
   apply(0, total);
   // The rest of the region table, then the chunk's records in the overflow
   // pool (a skewed batch; none otherwise) in windows of 64 pool rows
@@ -851,7 +917,7 @@ __device__ __forceinline__ void apply_chunk(
       }
       fetch(f0, tot);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]), "+v"(srec[r]));
       apply(f0, tot);
       f0 += B * kRecPer;
     }
@@ -940,7 +1006,6 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
 
 struct ApplyArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
-  const u64* esc;      // the escape column (escapes of escape-dense K3 tiles)
   Side side;           // K4's folded records
   const u64 *gt, *ts;
   u64 *match, *next;
@@ -958,7 +1023,7 @@ struct ApplyArgs {
 template <int N, bool MANY>
 void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
                        const ApplyArgs& a, hipStream_t st) {
-  const EscArgs esc{a.ri, a.rt, a.esc, a.side};
+  const EscArgs esc{a.ri, a.rt, a.side};
   const dim3 grid(a.hv.blocks + geo.NC);
   if (a.next)
     hipLaunchKernelGGL((k_bk_apply<N, true, MANY>), grid, dim3(k5_block(N)), 0, st, geo, recs, counts,
@@ -1031,8 +1096,9 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   const unsigned pblocks = geo.npool;
   const Pool pool = pool_at(ws, cv, geo);
   if (compact) {
-    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.esc),
-               buf2 = compact_at(ws + cv.buf2, nullptr);
+    u32* sflag = side_flag_at(ws, cv);
+    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, sflag),
+               buf2 = compact_at(ws + cv.buf2, nullptr, ws + cv.side2, sflag);
     hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads),
                        4 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
                        buf1, counts, shards, chunk_flags, pool);
@@ -1143,7 +1209,7 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-  const bk::Cols recs = bk::compact_at(ws + cv.buf2, nullptr);
+  const bk::Cols recs = bk::compact_at(ws + cv.buf2, nullptr, ws + cv.side2, bk::side_flag_at(ws, cv));
   u64* stt = reinterpret_cast<u64*>(stats);
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
@@ -1152,7 +1218,6 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::ApplyArgs a{reinterpret_cast<const u64*>(rec_index),
                         reinterpret_cast<const u64*>(rec_term),
-                        reinterpret_cast<const u64*>(ws + cv.esc),
                         bk::side_at(ws, cv),
                         reinterpret_cast<const u64*>(group_term),
                         reinterpret_cast<const u64*>(term_start),

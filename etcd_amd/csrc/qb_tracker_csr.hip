@@ -91,6 +91,9 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
   // see k_bk_apply; read with the first loads, tested once the table is built)
   const u32 hf = skip_heavy ? hv.sbflag[sb] : 0u;
   const bool heavy_sb = hf != 0u && hf - 1u < hv.blocks / kChunksPerSb;
+  // side records in this call (K3's flag word): their side words are read
+  // with the records
+  const bool sided = *recs.sflag != 0u;
   // the records K4's dedup folded away (stale, applied, rejected, non-member)
   const u32 extv = esc.side.ext[u64(c) * kExtClasses + (threadIdx.x & 3u)];
   // Load order: (1) slot offsets, group terms and the run table's rows (the
@@ -180,6 +183,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
   constexpr int kRecPer = int(kK5Inflight / B);  // records in flight per workgroup
   const RecFmt fmt = geo.fmt;
   u64 rec[kRecPer];
+  u32 srec[kRecPer];  // side words (a call with side records)
   auto load = [&](u32 f0, u32 n) {
     u32 ix[kRecPer];
 #pragma unroll
@@ -189,6 +193,8 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
     }
 #pragma unroll
     for (int r = 0; r < kRecPer; ++r) rec[r] = recs.mr[ix[r]];
+#pragma unroll
+    for (int r = 0; r < kRecPer; ++r) srec[r] = sided ? recs.side[ix[r]] : 0u;
   };
   auto apply = [&](u32 f0, u32 n) {
 #pragma unroll
@@ -203,11 +209,13 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
           non = true;                                     // no Progress: raft.go:1100-1104
         } else {
           u64 t = fmt.term(x), idx = fmt.payload(x);
-          // escape: the exact values from the batch, or a folded record's
-          // from the side table
-          if (t == fmt.tesc()) unescape(esc, t, idx);
           u64 gt = gterm[lg];
           if (gt == 0xFFFFFFFFull) gt = group_term[g0 + lg];  // (terms past 32 bits)
+          // a side record: its term from the side column; an escape: the
+          // exact values from the batch, or a folded record's from the side
+          // table
+          if (t == fmt.tside()) t = srec[r];
+          else if (t == fmt.tesc()) unescape(esc, t, idx, gt);
           if (t > gt) {
             slow = 1;  // higher term: step-down order (raft.go:875-879)
           } else if (t < gt) {
@@ -232,12 +240,12 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
   };
   load(0, total);
 #pragma unroll
-  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+  for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]), "+v"(srec[r]));
   apply(0, total);
   for (u32 f0 = B * kRecPer; f0 < total; f0 += B * kRecPer) {  // (all rows in one table)
     load(f0, total);
 #pragma unroll
-    for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+    for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]), "+v"(srec[r]));
     apply(f0, total);
   }
   // The chunk's records in the overflow pool (a skewed batch; none
@@ -250,7 +258,7 @@ __device__ __forceinline__ void csr_apply_chunk(const u32 c, const bool skip_hea
     for (u32 f0 = 0; f0 < tot; f0 += B * kRecPer) {
       load(f0, tot);
 #pragma unroll
-      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]));
+      for (int r = 0; r < kRecPer; ++r) asm volatile("" : "+v"(rec[r]), "+v"(srec[r]));
       apply(f0, tot);
     }
   }
@@ -359,7 +367,6 @@ __global__ __launch_bounds__(csr_block()) void k_csr_apply_deferred(QB_CSR_APPLY
 
 struct CsrStepArgs {
   const u64 *ri, *rt;  // the original batch (escape records)
-  const u64* esc;      // the escape column (escapes of escape-dense K3 tiles)
   Side side;           // K4's folded records
   const u32 *off, *cfg;
   const u64 *gt, *ts;
@@ -380,7 +387,7 @@ void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const 
                        const CsrStepArgs& a, hipStream_t st) {
   constexpr int CAPW = SECOND ? WMAX : (WMAX < kCsrCapW ? WMAX : kCsrCapW);
   const dim3 grid(SECOND ? (geo.NC + kDeferSpan - 1) / kDeferSpan : a.hv.blocks + geo.NC);
-  const EscArgs esc{a.ri, a.rt, a.esc, a.side};
+  const EscArgs esc{a.ri, a.rt, a.side};
 #define QB_CSR_LAUNCH(NX)                                                                       \
   hipLaunchKernelGGL((SECOND ? k_csr_apply_deferred<WMAX, CAPW, NX, MANY>                        \
                              : k_csr_apply<WMAX, CAPW, NX, MANY>),                                 \
@@ -464,7 +471,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   char* ws = static_cast<char*>(workspace);
   u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
   u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-  const bk::Cols buf2 = bk::compact_at(ws + cv.buf2, nullptr);
+  const bk::Cols buf2 = bk::compact_at(ws + cv.buf2, nullptr, ws + cv.side2, bk::side_flag_at(ws, cv));
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
@@ -477,7 +484,6 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   const bk::Pool pool = bk::pool_at(ws, cv, geo);
   const bk::CsrStepArgs a{ri,
                           rtm,
-                          reinterpret_cast<const u64*>(ws + cv.esc),
                           bk::side_at(ws, cv),
                           off,
                           cfg,

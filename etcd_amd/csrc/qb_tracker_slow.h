@@ -31,24 +31,22 @@ struct HeavyArgs {
   u32 blocks;  // leading workgroups of the grid that take the heavy chunks
 };
 // K4's folded records (kDedupFlag) and the escapes: the exact index and term
-// — the side table, the escape column (kEscColumn: an escape-dense K3 tile)
-// or the original batch.
+// — the side table or the original batch.  (Side records carry their term
+// in the side column, read with the record: RecFmt::tside.)
 struct EscArgs {
   const u64 *ri, *rt;  // the original batch
-  const u64* esc;      // the escape column: (index, term) at a record's buf1 position
   Side side;
 };
 // (A folded record counts once here; K4 added the records it folded away to
 // the chunk's ext counters by class, which K5 adds unless the chunk is slow.)
-__device__ __forceinline__ void unescape(const EscArgs& e, u64& t, u64& idx) {
+// gt: the record's group term (a folded side record equal to it carries
+// kTermIsGroup instead of the term).
+__device__ __forceinline__ void unescape(const EscArgs& e, u64& t, u64& idx, u64 gt) {
   if (idx & kDedupFlag) {
     const u64 si = idx & (kDedupFlag - 1ull);
     idx = e.side.idx[si];
-    t = e.side.tc[si] & ((1u << kDedupCountShift) - 1u);
-  } else if (idx & kEscColumn) {
-    const u64 r = 2ull * (idx & (kEscColumn - 1ull));
-    idx = e.esc[r];
-    t = e.esc[r + 1];
+    t = e.side.tc[si] & kTermIsGroup;
+    if (t == kTermIsGroup) t = gt;
   } else {
     const u32 ridx = u32(idx);
     idx = e.ri[ridx];

@@ -382,11 +382,24 @@ def test_wide_wave_owner_lookup():
         prs.update({i: CC.Pr(match=0, next=20 + g, is_learner=True, inflight_size=K)
                     for i in range(100, 115)})
         return CC.Tracker(set(range(1, 6)), None, set(range(100, 115)), None, False, prs, K)
+    import torch
     orc = [tracker(g) for g in range(G)]
     table, rings = _ring_marks(_table(orc, K=K), K)
     before = table.numpy()
+    dev = table.t["off"].device
+    cap = 20 * G + 8   # (the default capacity assumes <= 16 slots per group)
     for op, ccs in ((0, []), (1, [(CC.ADD_LEARNER, 200)])):
-        got, err, _ = table.change([op] * G, [ccs] * G, [50] * G)
+        o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
+             "cfg": torch.empty(G, dtype=torch.int32, device=dev),
+             "ext": torch.empty(G, dtype=torch.int32, device=dev),
+             "err": torch.empty(G, dtype=torch.uint8, device=dev),
+             "err_id": torch.empty(G, dtype=torch.int64, device=dev),
+             "pstate": torch.empty(cap, dtype=torch.uint8, device=dev),
+             "infl_pos": torch.empty(cap, dtype=torch.int32, device=dev),
+             "infl_buf": torch.empty(cap * K, dtype=torch.int64, device=dev)}
+        for k in ("ids", "match", "next", "pending_snapshot"):
+            o[k] = torch.empty(cap, dtype=torch.int64, device=dev)
+        got, err, _ = table.change([op] * G, [ccs] * G, [50] * G, out=o)
         a = got.numpy()
         assert int(a["off"][-1]) == 20 * G
         assert (err == (15 if op else 0)).all()

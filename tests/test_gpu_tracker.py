@@ -151,11 +151,11 @@ def test_appresp_then_commit_vs_sequential(mode, n, G, M, kw):
 
 @pytest.mark.parametrize("term_base", [20000, 0xFFFFFFFF - 5, 1 << 40, (1 << 64) - 16])
 def test_step_wide_terms_vs_sequential(term_base):
-    """Terms past the compact record's term field (>= 1023: every record an
-    escape, so every K3 tile is escape-dense and writes the escape column),
-    around and past 2^32 (qb_bucket.h: term_to32); group terms straddle the
-    escape value so equal / stale / higher records land on both sides of
-    it."""
+    """Terms past the compact record's term field (>= 2046: every K3 tile is
+    dense with them, so every record is a side record whose term travels in
+    the side column), around and past 2^32 - 1 (where the side form ends:
+    batch-position escapes; term_to32); group terms straddle 2^32 - 1 so
+    equal / stale / higher records land on both sides of it."""
     n, G, M = 5, 70001, 70001
     rng = np.random.default_rng(term_base % 1000003)
     st = _random_state(rng, n, G, term_base)
@@ -174,12 +174,13 @@ def test_step_wide_terms_vs_sequential(term_base):
         seq["stepped_down"][:] = 0
 
 
-@pytest.mark.parametrize("frac", [0.3, 0.5, 0.7])
+@pytest.mark.parametrize("frac", [0.05, 0.125, 0.5])
 def test_step_mixed_escape_density(frac):
-    """A fraction of the groups at terms >= 1023 (their records escape): K3
-    tiles on both sides of the escape-dense threshold in one batch, so
-    escapes read from the batch and from the escape column meet in the same
-    chunks (qb_bucket.h kEscColumn)."""
+    """A fraction of the groups at terms past the record's term field: K3
+    tiles on both sides of the side threshold (1/8 of a tile, qb_bucket.h
+    kSideDen) in one batch at 0.125, so side records and batch-position
+    escapes of the same terms meet in the same chunks (and K4 / K5 read side
+    words of tiles that wrote none for their other records)."""
     n, G, M = 5, 70001, 140002
     rng = np.random.default_rng(int(frac * 1000))
     st = _random_state(rng, n, G)
@@ -504,23 +505,26 @@ def test_step_dense_batch_many_parts_per_region():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("higher", [0.0, 0.0005])
-def test_step_hot_groups_fold_in_k4(higher):
+@pytest.mark.parametrize("higher,big", [(0.0, 0.5), (0.0005, 0.5), (0.0005, 1.0)])
+def test_step_hot_groups_fold_in_k4(higher, big):
     """Hot groups: 35 % of 2M records on one group and 15 % on eight more,
     the rest uniform over 1M groups — their chunks' runs in a K4 part pass
     kHeavyRun, so K4 folds records with equal lg | slot | reject | term into
     one (side table, counts classed into the chunk's ext counters by the
     group term) and their super-buckets' regions overflow into the pool
     (heavy chunks applied by the leading workgroups).  Hot records include
-    stale terms, rejects, terms past the compact field (escapes, never
-    folded; the state's 1 % of groups above 2^63 escape by index); with
-    `higher`, some chunks go to the slow
-    path and must not count their folded records twice.  State and every
-    stat counter equal the sequential oracle's."""
+    stale terms, rejects, terms past the compact field (side records: K4
+    folds those equal to the group term under kTermIsGroup and the stale ones
+    as term 0, never a higher one; the state's 1 % of groups above 2^63
+    escape by index, never folded); `big` of the groups (all hot ones at
+    1.0) have such terms; with `higher`, some chunks go to the slow path and
+    must not count their folded records twice.  State and every stat counter
+    equal the sequential oracle's."""
     n, G, M = 5, 1 << 20, 1 << 21
-    rng = np.random.default_rng(81)
+    rng = np.random.default_rng(81 + int(big * 10))
     st = _random_state(rng, n, G)
-    st["term"][:] = np.where(rng.random(G) < 0.5, 9, 5000).astype(np.uint64)  # > 2047: escapes
+    st["term"][:] = np.where(rng.random(G) < big, 5000 + rng.integers(0, 1 << 20, size=G),
+                             9).astype(np.uint64)
     tr = _tracker_from(n, st, track_next=False)
     st.pop("next")
     group, slot, index, term, rej, flags = _random_batch(rng, n, G, M, st, higher=higher,

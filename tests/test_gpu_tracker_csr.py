@@ -114,7 +114,8 @@ def test_csr_step_vs_sequential(kind, G, M, kw):
 
 @pytest.mark.parametrize("term_base", [20000, 0xFFFFFFFF - 5, (1 << 64) - 16])
 def test_csr_step_wide_terms(term_base):
-    """Group terms straddling the u32 escape (qb_bucket.h term_to32)."""
+    """Group terms past the record's term field (side records) and
+    straddling 2^32 - 1, where the side form ends (batch-position escapes)."""
     G = M = 20000
     rng = np.random.default_rng(term_base % 99991)
     off, cfg, sizes, st = _state(rng, "joint", G, term_base)
@@ -463,14 +464,20 @@ def test_csr_step_dense_batch_many_parts_per_region():
 
 
 @pytest.mark.timeout(300)
-def test_csr_step_hot_groups_fold_in_k4():
+@pytest.mark.parametrize("big", [0.0, 1.0])
+def test_csr_step_hot_groups_fold_in_k4(big):
     """The CSR step with hot groups (40 % of 2M records on one group, 15 % on
     eight more): K4 folds their repeated records, classing what it folds by
     the group term and, for a slot past the group's count, as non-member —
-    state and every stat counter equal the sequential oracle's."""
+    state and every stat counter equal the sequential oracle's.  big = 1:
+    every group term past the record's term field (side records, folded
+    under kTermIsGroup / as term 0 by K4)."""
     G, M = 1 << 20, 1 << 21
-    rng = np.random.default_rng(79)
+    rng = np.random.default_rng(79 + int(big))
     off, cfg, sizes, st = _state(rng, "ragged", G)
+    if big:
+        st["term"] = (st["term"] + np.uint64(3000) +
+                      rng.integers(0, 1 << 24, size=G).astype(np.uint64)).astype(np.uint64)
     st.pop("next")
     tr = _tracker(off, cfg, st, track_next=False)
     group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, higher=0.0002)
@@ -486,6 +493,8 @@ def test_csr_step_hot_groups_fold_in_k4():
     index = np.where(lag < last, last - lag, np.uint64(0)).astype(np.uint64)
     v = rng.random(M)
     term = st["term"][group] - (v < 0.05).astype(np.uint64)
+    if big:   # a few higher terms too: their chunks take the slow path
+        term = term + (v > 0.9997).astype(np.uint64)
     rej = rng.random(M) < 0.05
     flags = (slot | (rej.astype(np.uint8) << 7)).astype(np.uint8)
     stats = oc.csr_appresp_sequential(off, cfg, (group, flags, index, term), st, threads=16)
