@@ -89,6 +89,9 @@ SIGNATURES = {
     "qb_dev_wire_group_rows": (_i32, [_u64, _p, _p, _p, _p]),
     "qb_dev_ingest_messages_rows": (_i32, [_u64, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p,
                                            _p, _p, _p, _p, _p, _p, _p]),
+    "qb_wire_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
+    "qb_dev_ingest_fixed_tracker_step": (_i32, [_u32, _u64, _u64, _p, _u64] + [_p] * 17 +
+                                         [C.c_size_t, _p]),
     "qb_conf_change_workspace_bytes": (C.c_size_t, [_u64]),
     "qb_dev_conf_change": (_i32, [_p, _p, _p, C.c_size_t, _p]),
     "qb_shard_range": (_i32, [_u64, _i32, _i32, _p, _p]),
@@ -103,7 +106,7 @@ SIGNATURES = {
     "qb_allgather_changed_workspace_bytes": (C.c_size_t, [_u64, _i32]),
     "qb_dev_allgather_changed": (_i32, [_p, _u64, _p, _p, _p, _p, _p, C.c_size_t, _p]),
     "qb_route_partition_workspace_bytes": (C.c_size_t, [_i32, _u64]),
-    "qb_dev_route_partition": (_i32, [_u64, _i32, _u64] + [_p] * 13 + [C.c_size_t, _p]),
+    "qb_dev_route_partition": (_i32, [_u64, _i32, _u64] + [_p] * 14 + [C.c_size_t, _p]),
     "qb_route_workspace_bytes": (C.c_size_t, [_i32, _u64]),
     "qb_dev_route_records": (_i32, [_p, _u64, _u64] + [_p] * 12 + [_u64, _p, _p, C.c_size_t, _p]),
     "qb_dev_synth_fixed": (_i32, [_u64, _u32, _u64, _u64, _p, _p, _p, _p, _p]),

@@ -25,102 +25,13 @@
 //                    batch index), MaybeUpdate as LDS atomic max, RecentActive
 //                    as LDS atomic or, then maybeCommit for the chunk's groups
 //                    and a coalesced write-back of match/next/active/committed.
-#include "qb_bucket.h"
+#include "qb_bucket_tile.h"
 #include "qb_tracker_slow.h"
 
 
 namespace qb {
 namespace bk {
 
-// ------------------------------------------------ LDS tile partition ----
-// Counting sort of one tile (<= kTile records) by a small key, in LDS.  The
-// caller provides each record's bin (or kNoBin); afterwards perm[e] is the
-// tile index of the e-th record in bin order and start[b] the first e of
-// bin b.  Payload columns are then moved with tile_move: coalesced global
-// load into LDS, permuted LDS read, coalesced global store.
-constexpr u16 kNoBin = 0xFFFF;
-constexpr int kPartThreads = 1024;
-
-struct alignas(16) TileLds {
-  u16 bin[kTile];
-  u16 rank[kTile];
-  u16 perm[kTile];
-  u64 stage[kTile];
-  u8 cl[kTile];  // compact records: chunk-low, the next level's key
-  u32 wsum[kPartThreads / 64];
-};
-
-// Exclusive scan of cnt[0..nb) in place (per-thread serial runs + wave
-// shuffles + one LDS pass); returns the number of binned records.
-__device__ __forceinline__ u32 tile_scan_bins(u32* cnt, u32 nb, u32* wsum) {
-  const u32 T = blockDim.x;
-  const u32 per = (nb + T - 1) / T;
-  u32 run = 0;
-  for (u32 j = 0; j < per; ++j) {
-    const u32 b = threadIdx.x * per + j;
-    if (b < nb) run += cnt[b];
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = int(T >> 6);
-  u32 x = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u32 y = u32(__shfl_up(int(x), o, 64));
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  u32 before = 0, total = 0;
-  for (int q = 0; q < nw; ++q) {
-    total += wsum[q];
-    if (q < w) before += wsum[q];
-  }
-  u32 acc = before + x - run;
-  for (u32 j = 0; j < per; ++j) {
-    const u32 b = threadIdx.x * per + j;
-    if (b < nb) {
-      const u32 c = cnt[b];
-      cnt[b] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-  return total;
-}
-
-template <class Lds>
-__device__ __forceinline__ void tile_perm(Lds& L, const u32* start, u32 nrec) {
-  for (u32 k = threadIdx.x; k < nrec; k += blockDim.x) {
-    const u16 b = L.bin[k];
-    if (b != kNoBin) L.perm[start[b] + L.rank[k]] = u16(k);
-  }
-  __syncthreads();
-}
-
-// ---------------------------------------------------------------- K3 ----
-// Level 1: one block per tile of the original records; bins = super-buckets.
-// Every global load of the tile (group, flags and both payload columns) is
-// issued before the first LDS step, so the loads overlap each other and the
-// ranking.  Each super-bucket's run of the tile reserves its place in region
-// b * 8 + x (x = the XCD slot, blockIdx % 8) with one returning atomic on the
-// region's fill counter; what lies past the region's cap (a skewed batch)
-// continues in the region's overflow pool parts (Pool, qb_bucket.h: at most
-// two per run, drawn here).  Invalid records go to the stat shards.
-constexpr int kPer = kTile / kPartThreads;  // records per thread
-static_assert((kTile & (kTile - 1)) == 0, "pool offsets by shift and mask");
-constexpr u32 kTileShift = 12;
-static_assert((1u << kTileShift) == u32(kTile), "kTile = 2^kTileShift");
-// Record index of region-relative position rel of super-bucket b's region x
-// (the region grid, then the pool parts p0 / p1 drawn for the run that
-// starts at gs), or ~0 when the run's pool part could not be drawn.
-__device__ __forceinline__ u64 region_dst(const Geometry& geo, const Pool& pool, u32 b, u32 x,
-                                          u32 rel, u32 gs, u32 p0, u32 p1) {
-  if (rel < geo.cap) return u64(b * kRegionShards + x) * geo.cap + rel;
-  const u32 q = rel - geo.cap, k = q >> kTileShift;
-  const u32 k0 = ((gs > geo.cap ? gs : geo.cap) - geo.cap) >> kTileShift;
-  const u32 pid = k == k0 ? p0 : p1;
-  if (pid == kNoPart) return ~0ull;
-  return pool.base + u64(pid) * kTile + (q & (u32(kTile) - 1u));
-}
 // (two 1024-thread blocks per CU need <= 64 VGPRs and <= 80 SGPRs)
 // COMPACT: the 8-byte records (the tracker steps) go from registers straight
 // to their sorted LDS slot (round 3: K3 115 -> 112 us against the
@@ -1004,21 +915,6 @@ __global__ __launch_bounds__(k5_block(N)) __attribute__((amdgpu_num_sgpr(80))) v
                              shards, ptab, hv);
 }
 
-struct ApplyArgs {
-  const u64 *ri, *rt;  // the original batch (escape records)
-  Side side;           // K4's folded records
-  const u64 *gt, *ts;
-  u64 *match, *next;
-  u16* active;
-  u64* committed;
-  u32* stepdown;
-  u8* adv;
-  u8* chunk_slow;
-  u32* any_slow;
-  u64* stats;
-  const u32* ptab;  // the overflow pool's part table
-  HeavyArgs hv;
-};
 
 template <int N, bool MANY>
 void launch_apply_rows(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
@@ -1044,9 +940,8 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* 
 template <int N>
 void launch_slow(const Geometry& geo, const ApplyArgs& a, const SlowArgs& s, u64* stats,
                  hipStream_t st) {
-  hipLaunchKernelGGL((k_bk_slow<FixedLay<N>>), dim3(s.grid), dim3(kBlock), 0, st, geo,
-                     FixedLay<N>{geo.G}, s.rg, s.rf, s.ri,
-                     s.rt, a.gt, a.ts, a.chunk_slow, a.any_slow, s.bar, a.stepdown, a.match, a.next,
+  hipLaunchKernelGGL((k_bk_slow<FixedLay<N>, ColSrc>), dim3(s.grid), dim3(kBlock), 0, st, geo,
+                     FixedLay<N>{geo.G}, ColSrc{s.rg, s.rf, s.ri, s.rt}, a.gt, a.ts, a.chunk_slow, a.any_slow, s.bar, a.stepdown, a.match, a.next,
                      a.active, a.committed, a.adv, a.stats, stats);
 }
 
@@ -1071,6 +966,42 @@ using namespace qb;
 
 namespace qb {
 namespace bk {
+
+// K4 of the compact form: each part of the region grid and of the pool
+// sorted by chunk-low (bucket_records' second launch; the composed wire ->
+// tracker step runs it after its own level 1, qb_wire_tracker.hip).
+void launch_split_compact(const Geometry& geo, const Carve& cv, char* ws, const u64* group_term,
+                          const u32* csr_off, hipStream_t st) {
+  const unsigned kparts = geo.NSB * kRegionShards * geo.ppx;
+  u32* sflag = side_flag_at(ws, cv);
+  const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, sflag),
+             buf2 = compact_at(ws + cv.buf2, nullptr, ws + cv.side2, sflag);
+  hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts + geo.npool), dim3(kSplitThreads), 0, st, geo,
+                     reinterpret_cast<u32*>(ws + cv.counts), buf1, buf2,
+                     reinterpret_cast<u32*>(ws + cv.chunk_start), pool_at(ws, cv, geo), kparts,
+                     side_at(ws, cv, group_term, csr_off));
+}
+
+ApplyArgs fixed_apply_args(const Geometry& geo, const Carve& cv, char* ws, const u64* ri,
+                           const u64* rt, const u64* group_term, const u64* term_start, u64* match,
+                           u64* next, u16* active, u64* committed, u32* stepdown_at, u8* advanced) {
+  const Pool pool = pool_at(ws, cv, geo);
+  return ApplyArgs{ri, rt, side_at(ws, cv), group_term, term_start, match, next, active, committed,
+                   stepdown_at, advanced, reinterpret_cast<u8*>(ws + cv.chunk_flags),
+                   reinterpret_cast<u32*>(ws + cv.flags), reinterpret_cast<u64*>(ws + cv.shards),
+                   reinterpret_cast<const u32*>(ws + cv.ptab),
+                   HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
+                             geo.NC < kHeavyBlocks ? geo.NC : kHeavyBlocks}};
+}
+
+// K5 of the FIXED step (k_bk_apply<n>) over buf2.
+void launch_fixed_apply(u32 n, const Geometry& geo, const Carve& cv, char* ws, const ApplyArgs& a,
+                        hipStream_t st) {
+  const Cols recs = compact_at(ws + cv.buf2, nullptr, ws + cv.side2, side_flag_at(ws, cv));
+  dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs,
+                 reinterpret_cast<const u32*>(ws + cv.counts),
+                 reinterpret_cast<const u32*>(ws + cv.chunk_start), a, st);
+}
 
 int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* rec_group,
                    const u8* rec_flags, const u64* rec_index, const u64* rec_term, u64* shards,
@@ -1097,14 +1028,12 @@ int bucket_records(const Geometry& geo, const Carve& cv, char* ws, const u32* re
   const Pool pool = pool_at(ws, cv, geo);
   if (compact) {
     u32* sflag = side_flag_at(ws, cv);
-    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, sflag),
-               buf2 = compact_at(ws + cv.buf2, nullptr, ws + cv.side2, sflag);
+    const Cols buf1 = compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, sflag);
     hipLaunchKernelGGL(k_bk_scatter<true>, dim3(geo.tile_grid()), dim3(kPartThreads),
                        4 * sizeof(u32) * geo.NSB, st, geo, rec_group, rec_flags, rec_index, rec_term,
                        buf1, counts, shards, chunk_flags, pool);
     QB_CHECK_LAUNCH("k_bk_scatter");
-    hipLaunchKernelGGL(k_bk_split_compact, dim3(kparts + pblocks), dim3(kSplitThreads), 0, st, geo,
-                       counts, buf1, buf2, cs, pool, kparts, side_at(ws, cv, group_term, csr_off));
+    launch_split_compact(geo, cv, ws, group_term, csr_off, st);
     QB_CHECK_LAUNCH("k_bk_split_compact");
     return QB_OK;
   }
@@ -1207,34 +1136,16 @@ extern "C" int qb_dev_fixed_tracker_apply(uint32_t n, uint64_t G, uint64_t M,
   if (rc != QB_OK) return rc;
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
-  u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
-  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-  const bk::Cols recs = bk::compact_at(ws + cv.buf2, nullptr, ws + cv.side2, bk::side_flag_at(ws, cv));
   u64* stt = reinterpret_cast<u64*>(stats);
-  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* rg = reinterpret_cast<const u32*>(rec_group);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
-  const bk::Pool pool = bk::pool_at(ws, cv, geo);
-  const bk::ApplyArgs a{reinterpret_cast<const u64*>(rec_index),
-                        reinterpret_cast<const u64*>(rec_term),
-                        bk::side_at(ws, cv),
-                        reinterpret_cast<const u64*>(group_term),
-                        reinterpret_cast<const u64*>(term_start),
-                        reinterpret_cast<u64*>(match),
-                        reinterpret_cast<u64*>(next),
-                        active,
-                        reinterpret_cast<u64*>(committed),
-                        stepdown_at,
-                        advanced_out,
-                        reinterpret_cast<u8*>(ws + cv.chunk_flags),
-                        reinterpret_cast<u32*>(ws + cv.flags),
-                        shards,
-                        reinterpret_cast<const u32*>(ws + cv.ptab),
-                        bk::HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
-                                      geo.NC < bk::kHeavyBlocks ? geo.NC : bk::kHeavyBlocks}};
-  bk::dispatch_apply(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, recs, counts, cs, a,
-                     st);
+  const bk::ApplyArgs a = bk::fixed_apply_args(
+      geo, cv, ws, ri, rtm, reinterpret_cast<const u64*>(group_term),
+      reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
+      reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed), stepdown_at,
+      advanced_out);
+  bk::launch_fixed_apply(n, geo, cv, ws, a, st);
   QB_CHECK_LAUNCH("k_bk_apply");
   // chunks flagged slow by K5 (none in the steady state: the launch folds
   // the stat shards and returns) + the stat fold

@@ -411,8 +411,8 @@ void launch_csr_step(const Geometry& geo, Cols recs, const u32* counts, const u3
                      const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
   launch_apply<WMAX, false>(geo, recs, counts, cs, a, st);
   if constexpr (WMAX > kCsrCapW) launch_apply<WMAX, true>(geo, recs, counts, cs, a, st);
-  hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
-                     CsrLay<WMAX>{a.off, a.cfg}, sa.rg, sa.rf, sa.ri, sa.rt, a.gt, a.ts,
+  hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>, ColSrc>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
+                     CsrLay<WMAX>{a.off, a.cfg}, ColSrc{sa.rg, sa.rf, sa.ri, sa.rt}, a.gt, a.ts,
                      a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,
                      a.committed, a.adv, a.shards, stats);
 }

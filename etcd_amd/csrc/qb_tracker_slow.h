@@ -97,10 +97,25 @@ __device__ __forceinline__ void stats_fold_block(const u64* __restrict__ shards,
 // each even as no-ops.
 constexpr unsigned kSlowBlockMax = 256;
 
-__device__ __forceinline__ bool in_slow_chunk(const Geometry& geo, u32 g, u32 f,
-                                              const u8* __restrict__ chunk_slow) {
-  return g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[geo.chunk_of(g)] == 1;
-}
+// Record sources of the slow path.  get(i, ...) is true when record i of the
+// batch is a valid record (group < G, slot < n) of a flagged chunk, with its
+// group, flags, index and term.  ColSrc: the batch's columns (the tracker
+// steps); the composed wire -> tracker step decodes the message instead
+// (qb_wire_tracker.hip).
+struct ColSrc {
+  const u32* rg;
+  const u8* rf;
+  const u64 *ri, *rt;
+  __device__ __forceinline__ bool get(const Geometry& geo, const u8* __restrict__ chunk_slow,
+                                      u64 i, u32& g, u32& f, u64& idx, u64& t) const {
+    g = rg[i];
+    f = rf[i];
+    if (!(g < geo.G && (f & 0x0Fu) < geo.n && chunk_slow[geo.chunk_of(g)] == 1)) return false;
+    t = rt[i];
+    idx = ri[i];
+    return true;
+  }
+};
 
 // Tracker state layouts.  FIXED: n voters, slot-major rows of G (every slot
 // below geo.n is a member).  CSR: group-major slots off[g] .. off[g+1]-1,
@@ -150,10 +165,9 @@ __device__ __forceinline__ void grid_barrier(u32* ctr, u32 target) {
   __syncthreads();
 }
 
-template <class Lay>
+template <class Lay, class Src>
 __global__ __launch_bounds__(kBlock) void k_bk_slow(
-    Geometry geo, Lay lay, const u32* __restrict__ rg, const u8* __restrict__ rf,
-    const u64* __restrict__ ri, const u64* __restrict__ rt, const u64* __restrict__ group_term,
+    Geometry geo, Lay lay, Src src, const u64* __restrict__ group_term,
     const u64* __restrict__ term_start, const u8* __restrict__ chunk_slow,
     const u32* __restrict__ any_slow, u32* __restrict__ bar, u32* __restrict__ stepdown_at,
     u64* __restrict__ match, u64* __restrict__ next, u16* __restrict__ active,
@@ -170,10 +184,11 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
   // Phase 1: the first higher-term record per group in batch order
   // (raft.go:875-879); K5 reset stepdown_at of every flagged chunk's groups.
   for (u64 i = tid0; i < geo.M; i += stride) {
-    const u32 g = rg[i], f = rf[i];
+    u32 g, f;
+    u64 idx, t;
     bool higher = false;
-    if (in_slow_chunk(geo, g, f, chunk_slow) && lay.member(g, f & 0x0Fu) &&
-        rt[i] > group_term[g]) {
+    if (src.get(geo, chunk_slow, i, g, f, idx, t) && lay.member(g, f & 0x0Fu) &&
+        t > group_term[g]) {
       atomicMin(stepdown_at + g, u32(i));
       higher = true;
     }
@@ -182,12 +197,14 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
   grid_barrier(bar, gridDim.x);
   // Phase 2: MaybeUpdate / RecentActive for records before the step-down.
   for (u64 i = tid0; i < geo.M; i += stride) {
-    const u32 g = rg[i], f = rf[i];
+    u32 g, f;
+    u64 idx, t;
     bool stale = false, applied = false, rejected = false, after = false, non = false;
-    if (in_slow_chunk(geo, g, f, chunk_slow) && !lay.member(g, f & 0x0Fu)) {
-      non = true;  // raft.go:1100-1104 (slots >= geo.n were counted by K1)
-    } else if (in_slow_chunk(geo, g, f, chunk_slow)) {
-      const u64 t = rt[i], gt = group_term[g];
+    const bool in = src.get(geo, chunk_slow, i, g, f, idx, t);
+    if (in && !lay.member(g, f & 0x0Fu)) {
+      non = true;  // raft.go:1100-1104 (slots >= geo.n were counted by K3)
+    } else if (in) {
+      const u64 gt = group_term[g];
       stale = t < gt;  // raft.go:883-921
       if (t == gt) {
         if (stepdown_at[g] < u32(i)) {
@@ -202,7 +219,6 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
             rejected = true;
           } else {
             applied = true;
-            const u64 idx = ri[i];
             const u64 at = lay.at(g, s);
             atomicMax(match + at, idx);                  // progress.go:146-150
             if (next) atomicMax(next + at, idx + 1ull);  // progress.go:151
@@ -236,6 +252,32 @@ __global__ __launch_bounds__(kBlock) void k_bk_slow(
     if (advanced) advanced[g] = adv ? 1 : 0;
   }
 }
+
+struct ApplyArgs {
+  const u64 *ri, *rt;  // the original batch (escape records)
+  Side side;           // K4's folded records
+  const u64 *gt, *ts;
+  u64 *match, *next;
+  u16* active;
+  u64* committed;
+  u32* stepdown;
+  u8* adv;
+  u8* chunk_slow;
+  u32* any_slow;
+  u64* stats;
+  const u32* ptab;  // the overflow pool's part table
+  HeavyArgs hv;
+};
+
+// Host launchers of qb_tracker_bucket.hip shared with the composed wire ->
+// tracker step (qb_wire_tracker.hip).
+void launch_split_compact(const Geometry& geo, const Carve& cv, char* ws, const u64* group_term,
+                          const u32* csr_off, hipStream_t st);
+ApplyArgs fixed_apply_args(const Geometry& geo, const Carve& cv, char* ws, const u64* ri,
+                           const u64* rt, const u64* group_term, const u64* term_start, u64* match,
+                           u64* next, u16* active, u64* committed, u32* stepdown_at, u8* advanced);
+void launch_fixed_apply(u32 n, const Geometry& geo, const Carve& cv, char* ws, const ApplyArgs& a,
+                        hipStream_t st);
 
 struct SlowArgs {
   const u32* rg;

@@ -1,0 +1,558 @@
+// qb_wire_tracker.hip — the composed per-tick path in one pipeline: raw
+// raftpb.Message bytes of a tick's responses -> the leader's ProgressTracker
+// (FIXED layout) stepped and the commit advanced, without the decoded record
+// columns between the two (VERDICT r5 "next" item 2).
+//
+// Reference path (paths relative to the reference's root):
+//   server/etcdserver/api/rafthttp/stream.go:466   messages off the transport
+//   raft/raftpb/raft.pb.go:1739-2061               Message.Unmarshal
+//   raft/raft.go:847-921                           Step's term filter
+//   raft/raft.go:1100-1109, 1237-1259              stepLeader MsgAppResp (quorum part)
+//   raft/tracker/progress.go:144-153               Progress.MaybeUpdate
+//   raft/raft.go:585-588, raft/log.go:328-334      maybeCommit
+//
+// Pipeline (one call of qb_dev_ingest_fixed_tracker_step):
+//   memset           stat shards, flag words, region fills, chunk flags
+//   K3w k_wire_scatter  per tile of 4096 messages (1024 threads, 4 per
+//                    thread): each wave stages its 64 messages' bytes into
+//                    its own LDS slice (LDS-DMA, no block barrier), decodes
+//                    them with the ingest's fast prefix, looks From up in the
+//                    group row, writes the status byte, and the tile's
+//                    records go straight into the reserved regions as K3 of
+//                    the tracker step writes them (compact 8-byte records,
+//                    chunk-low bytes, side column) — the ingest's record
+//                    columns (39 B per message written, 21 B read back by K3)
+//                    never exist
+//   K3d k_wire_deferred  messages the fast prefix left (non-canonical
+//                    encodings, spans past the wave's slice): the generic
+//                    decoder from global memory, each record appended to its
+//                    region (one atomic each; rare)
+//   K4  k_bk_split_compact, K5 k_bk_apply<n>  as the tracker step
+//   slow k_bk_slow<FixedLay<n>, WireSrc>  a chunk with a higher-term record
+//                    re-decodes its messages from the bytes, in batch order
+// Semantics: exactly qb_dev_ingest_messages_rows followed by
+// qb_dev_fixed_tracker_step on its records, with the records that are not a
+// MsgAppResp stepping nothing (a non-OK status or another message type
+// counts as QB_STAT_BAD_GROUP, as the ingest's group ~0 does) and a From with
+// no Progress (QB_REC_NO_PROGRESS) counted as QB_STAT_NON_MEMBER.  Escapes
+// (an index >= 2^40, a term >= 2^32 - 1, a large term in a tile where they
+// are rare) keep their exact index and term in two batch-order columns of
+// the workspace, written only at their own positions.
+#include "qb_wire_decode.h"
+#include "qb_bucket_tile.h"
+#include "qb_tracker_slow.h"
+
+namespace qb {
+namespace wt {
+
+using namespace bk;
+using wire::Decoded;
+using wire::GroupRow;
+using wire::LdsSrc;
+using wire::GlobalSrc;
+using wire::RowArgs;
+
+// Workgroup: kWtThreads threads, 4 messages each (one per sub-round): a
+// tile of kWtTile messages.  Its LDS: the sorted records, their side terms,
+// bins and chunk-lows — and, while the tile is decoded, each wave's byte
+// slice in the same bytes (3584 B per wave: 64 messages of up to ~54 B on
+// average; a wave whose span is longer is deferred).
+#ifndef QB_WT_THREADS
+#define QB_WT_THREADS 1024
+#endif
+constexpr u32 kWtThreads = QB_WT_THREADS;
+constexpr u32 kWtTile = kWtThreads * kPer;
+constexpr u32 kWaves = kWtThreads / 64;
+constexpr u32 kSlice = 3584;
+constexpr u32 kSliceSpan = kSlice - 48;  // window over-reads (<= 24 B) + 16-byte alignment
+struct alignas(16) WtLds {
+  u64 stage[kWtTile];  // sorted records
+  u32 t32[kWtTile];    // their side terms
+  u16 bin[kWtTile];
+  u8 cl[kWtTile];
+  u32 wsum[kWaves];
+};
+static_assert(kWaves * kSlice <= offsetof(WtLds, cl), "the slices fit stage..bin");
+static_assert(kWtTile <= u32(kTile), "a tile's run spans at most two pool parts");
+
+struct WireArgs {
+  u64 nbytes;
+  const u8* bytes;
+  RowArgs R;        // G, msg_off, msg_group, off, ids, rows
+  u8* status;       // per message (QB_WIRE_*)
+  u64 *ri, *rt;     // escapes: the exact index / term at the message's position
+  u64* wstats;      // nullable: QB_WIRE_* counts
+};
+
+// The leader-inbox record of a decoded message as the tracker takes it:
+// valid (a MsgAppResp of a group < G from a member slot < n), or counted
+// bad (not a record of a group) / non-member.
+struct RecClass {
+  bool ok, bad, non;
+};
+__device__ __forceinline__ RecClass classify(const Geometry& geo, const Decoded& d) {
+  const bool rec = d.st == QB_WIRE_OK && ((d.flags >> 4) & 3u) == QB_IN_APP_RESP && d.group < geo.G;
+  const bool member = (d.flags & QB_REC_NO_PROGRESS) == 0 && (d.flags & 0x0Fu) < geo.n;
+  return RecClass{rec && member, !rec, rec && !member};
+}
+
+// The XCD slot (region shard) of tile t: the blockIdx % 8 of the K3w
+// workgroup that took it (Geometry::tile's mapping inverted), so a deferred
+// record lands in the region its tile's records went to and every region
+// keeps the bound geometry() sized it for.
+__device__ __forceinline__ u32 region_slot_of_tile(const Geometry& geo, u32 tile, u32 grid) {
+  return geo.xcd ? tile / (grid / kXcds) : tile % kXcds;
+}
+// Tiles of kWtTile messages and their grid (XCD-major as Geometry::tile when
+// the geometry's runs are short).
+inline u32 wt_tiles(const Geometry& geo) { return u32((geo.M + kWtTile - 1) / kWtTile); }
+inline u32 wt_grid(const Geometry& geo) {
+  const u32 nt = wt_tiles(geo);
+  return geo.xcd ? (nt + kXcds - 1) / kXcds * kXcds : nt;
+}
+
+// Stage a wave's span of sub-round r — its messages' bytes [q0 of its first
+// lane, q1 of its last) — into its slice by LDS-DMA (plain loads for an
+// unaligned buffer or the buffer's last partial piece), without waiting for
+// it; [lb, le) = the staged span, empty when the span does not fit (the
+// wave's messages are then deferred).  The caller waits (vmcnt) before
+// decoding; the compiler barriers keep every later load after the DMA in
+// issue order, which that wait's count relies on.
+__device__ __forceinline__ void stage_span(u8* slice, const WireArgs& W, u32 nrec, int r, u32 w,
+                                           u32 lane, u64 p0, u64 p1, u64& lb, u64& le) {
+  const u32 wk0 = u32(r) * kWtThreads + w * 64u;
+  const u32 nw = wk0 < nrec ? (nrec - wk0 < 64u ? nrec - wk0 : 64u) : 0u;
+  const u64 b0 = __shfl(p0, 0, 64), b1 = __shfl(p1, nw ? int(nw) - 1 : 0, 64);
+  lb = le = 0;
+  if (!(nw && b1 > b0 && b1 - b0 <= kSliceSpan)) return;  // (wave-uniform)
+  const u64 a0 = b0 & ~u64(15);
+  const u64 a1 = (b1 + 15) & ~u64(15);
+  const u32 n16 = u32((a1 - a0) / 16);
+  const u64 whole = (W.nbytes - a0) / 16;
+  const u32 nfull = u32(n16 < whole ? n16 : whole);
+  if ((reinterpret_cast<uintptr_t>(W.bytes) & 15u) == 0) {
+#pragma unroll
+    for (u32 q = 0; q < (kSlice / 16 + 63) / 64; ++q) {
+      const u32 i = q * 64u + lane;
+      if (i < nfull)
+        __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)(W.bytes + a0 + 16ull * i),
+                                         (lds_void_t*)(slice + 16u * 64u * q), 16, 0, 2);
+    }
+  } else {
+    for (u32 i = lane; i < nfull; i += 64)
+      reinterpret_cast<uint4*>(slice)[i] = reinterpret_cast<const uint4*>(W.bytes + a0)[i];
+  }
+  for (u32 i = nfull + lane; i < n16; i += 64)
+    for (u32 t = 0; t < 16; ++t) {
+      const u64 p = a0 + 16ull * i + t;
+      slice[16 * i + t] = p < W.nbytes ? W.bytes[p] : u8(0);
+    }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  lb = a0;
+  le = a1 < W.nbytes ? a1 : W.nbytes;
+}
+
+// ------------------------------------------------------------------ K3w ----
+__global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
+    Geometry geo, WireArgs W, Cols out, u32* __restrict__ counts, u64* __restrict__ shards,
+    u8* __restrict__ chunk_slow, Pool pool, u32 ntiles) {
+  extern __shared__ __attribute__((aligned(16))) u32 dyn[];
+  u32* start = dyn;               // NSB: count, then local exclusive start
+  u32* gstart = dyn + geo.NSB;    // NSB: the run's offset in its region
+  u32* pid0 = dyn + 2 * geo.NSB;  // NSB: pool parts of the run past the cap
+  u32* pid1 = dyn + 3 * geo.NSB;
+  __shared__ WtLds L;
+  __shared__ __attribute__((aligned(16))) u8 s_slice2[kWaves * kSlice];  // the second slice of each wave
+  __shared__ u32 s_nside;
+  __shared__ u32 wtl[4];
+  const u32 tile = geo.xcd ? xcd_major() : blockIdx.x;
+  if (tile >= ntiles) return;
+  if (threadIdx.x == 0) s_nside = 0;
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) start[b] = 0;
+  __syncthreads();
+  const u64 t0 = u64(tile) * kWtTile;
+  const u32 nrec = u32(geo.M - t0 < u64(kWtTile) ? geo.M - t0 : u64(kWtTile));
+  const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  u8* slice = reinterpret_cast<u8*>(&L) + w * kSlice;
+  BlockTally<4> wtally;  // OK, UNMARSHAL, TYPE, CTX
+  u32 nbad = 0, nnon = 0, nside = 0;
+  // per record (message t0 + r * 1024 + threadIdx.x): bin | chunk-low << 16
+  // (kNoBin: none), its rank in the bin, the encoded record, a side term
+  u32 bj[kPer], rj[kPer], tj[kPer];
+  u64 vj[kPer];
+  // Sub-round pipeline.  Every sub-round's message offsets and envelope
+  // groups are requested up front; sub-round r + 1's group row and byte span
+  // (into the wave's other slice) are requested before sub-round r is
+  // decoded, so the decode overlaps the next sub-round's round trips instead
+  // of waiting for them.
+  u64 q0[kPer], q1[kPer];
+  u32 qg[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const u32 k = u32(r) * kWtThreads + threadIdx.x;
+    const u64 mc = k < nrec ? t0 + k : geo.M - 1;
+    q0[r] = __builtin_nontemporal_load(W.R.moff + mc);
+    q1[r] = __builtin_nontemporal_load(W.R.moff + mc + 1);
+    qg[r] = __builtin_nontemporal_load(W.R.mgroup + mc);
+  }
+  u8* slices[2] = {slice, s_slice2 + w * kSlice};
+  u64 sb[2], se[2];  // the staged span of each slice
+  GroupRow nrow;
+  wire::load_row_of(W.R, qg[0], nrow);
+  stage_span(slices[0], W, nrec, 0, w, lane, q0[0], q1[0], sb[0], se[0]);
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const u32 k = u32(r) * kWtThreads + threadIdx.x;  // tile index
+    const bool in = k < nrec;
+    const u64 m = t0 + k;
+    const u64 p0 = q0[r], p1 = q1[r];
+    GroupRow row = nrow;
+    const u64 lbase = sb[r & 1], lend = se[r & 1];
+    if (r + 1 < kPer) {
+      wire::load_row_of(W.R, qg[r + 1], nrow);
+      // sub-round r's LDS-DMA is done once at most the loads just issued (the
+      // next group row: 4 loads, or 2 without the row table) are outstanding
+      // (vmcnt counts in issue order; the DMA was issued before them, pinned
+      // by the compiler barriers in stage_span)
+      if (W.R.rows) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      stage_span(slices[(r + 1) & 1], W, nrec, r + 1, w, lane, q0[r + 1], q1[r + 1], sb[(r + 1) & 1],
+                 se[(r + 1) & 1]);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    u8* const slice_r = slices[r & 1];
+    wire::load_ids(W.R, row);
+    Decoded d{wire::kDeferred, 0xFFFFFFFFu, 0, 0, 0, 0, 0, 0};
+    if (in && p0 >= lbase && p1 <= lend && p0 <= p1)
+      d = wire::decode_one<LdsSrc, false>(W.R, W.nbytes, LdsSrc{slice_r, lbase}, p0, p1, row);
+    const bool dec = in && d.st != wire::kDeferred;  // decoded here (else K3d's)
+    if (in) __builtin_nontemporal_store(u8(d.st), W.status + m);
+    wtally.add(0, dec && d.st == QB_WIRE_OK);
+    wtally.add(1, dec && d.st == QB_WIRE_UNMARSHAL);
+    wtally.add(2, dec && d.st == QB_WIRE_TYPE);
+    wtally.add(3, dec && d.st == QB_WIRE_CTX);
+    const RecClass c = classify(geo, d);
+    const bool ok = dec && c.ok;
+    nbad += wave_popc(dec && c.bad);
+    nnon += wave_popc(dec && c.non);
+    const u32 g = ok ? d.group : 0u;
+    bj[r] = ok ? geo.sb_of(g) : u32(kNoBin);
+    rj[r] = ok ? atomicAdd(&start[bj[r]], 1u) : 0u;
+    bj[r] |= geo.cl_of_chunk(geo.chunk_of(g)) << 16;
+    vj[r] = geo.fmt.encode_side(g & (geo.CH - 1u), d.flags & 0x0Fu, (d.flags & QB_REC_REJECT) != 0,
+                                d.index, d.term, u32(m));
+    const u32 tf = geo.fmt.term(vj[r]);
+    tj[r] = ok && tf == geo.fmt.tside() ? u32(d.term) : 0u;
+    nside += ok && tf == geo.fmt.tside() ? 1u : 0u;
+    if (ok && tf == geo.fmt.tesc()) {  // exact values for K5 (rare: no partial-line worry)
+      W.ri[m] = d.index;
+      W.rt[m] = d.term;
+    }
+  }
+  if (nside) atomicAdd(&s_nside, nside);
+  if (W.wstats) {
+    const int slot[4] = {QB_WIRE_OK, QB_WIRE_UNMARSHAL, QB_WIRE_TYPE, QB_WIRE_CTX};
+    wtally.flush(wtl, W.wstats, slot);  // (synchronises: every wave is done with its slice)
+  } else {
+    __syncthreads();
+  }
+  // ---- level 1, as k_bk_scatter<true>: each super-bucket's run reserves its
+  // place in the region of this workgroup's XCD slot with one atomic
+  for (u32 b = threadIdx.x; b < geo.NSB; b += blockDim.x) {
+    const u32 nbin = start[b];
+    if (!nbin) continue;
+    const u32 rr = b * kRegionShards + blockIdx.x % kRegionShards;
+    const u32 gs = atomicAdd(&counts[rr], nbin);
+    gstart[b] = gs;
+    if (gs + nbin > geo.cap) {
+      if (gs <= geo.cap) mark_heavy(pool, b);
+      const u32 lo = gs > geo.cap ? gs : geo.cap;
+      const u32 k0 = (lo - geo.cap) >> kTileShift, k1 = (gs + nbin - 1u - geo.cap) >> kTileShift;
+      const u32 a = pool_acquire(pool, rr, k0);
+      pid0[b] = a;
+      pid1[b] = k1 != k0 ? pool_acquire(pool, rr, k1) : a;
+    }
+  }
+  if (lane == 0 && (nbad | nnon)) {
+    u64* sh = shards + u64(tile % kShards) * QB_STAT_COUNT;
+    if (nbad) atomicAdd(sh + QB_STAT_BAD_GROUP, u64(nbad));
+    if (nnon) atomicAdd(sh + QB_STAT_NON_MEMBER, u64(nnon));
+  }
+  const u32 nvalid = tile_scan_bins(start, geo.NSB, L.wsum);
+  // side records kept when not rare in the tile (qb_bucket.h kSideDen); else
+  // escapes, their exact values written at their message positions
+  const bool side = s_nside * kSideDen > nvalid;  // (block-uniform)
+  u32* t32 = L.t32;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const u32 b = bj[r] & 0xFFFFu;
+    if (b == u32(kNoBin)) continue;
+    const u32 e = start[b] + rj[r];
+    u64 v = vj[r];
+    if (!side && geo.fmt.term(v) == geo.fmt.tside()) {
+      const u64 m = t0 + u32(r) * kWtThreads + threadIdx.x;
+      W.ri[m] = geo.fmt.payload(v);
+      W.rt[m] = tj[r];
+      v = geo.fmt.to_escape(v, u32(m));
+    }
+    L.stage[e] = v;
+    L.bin[e] = u16(b);
+    L.cl[e] = u8(bj[r] >> 16);
+    if (side) t32[e] = tj[r];
+  }
+  __syncthreads();
+  if (side && threadIdx.x == 0) *out.sflag = 1u;
+  const u32 x = blockIdx.x % kRegionShards;
+  for (u32 e = threadIdx.x; e < nvalid; e += blockDim.x) {
+    const u32 b = L.bin[e];
+    const u32 gs = gstart[b];
+    const u32 rel = gs + (e - start[b]);
+    const u64 dd = rel < geo.cap ? u64(b * kRegionShards + x) * geo.cap + rel
+                                 : region_dst(geo, pool, b, x, rel, gs, pid0[b], pid1[b]);
+    if (dd != ~0ull) {
+      out.mr[dd] = L.stage[e];
+      out.cl[dd] = L.cl[e];
+      if (side) out.side[dd] = t32[e];
+    } else {  // no pool part (never with the carve's sizing): the exact slow path
+      chunk_slow[geo.chunk_of_sb_cl(b, L.cl[e])] = kChunkOverflow;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ K3d ----
+// The deferred messages: a thread scans kScan consecutive statuses (16-byte
+// words); with nothing deferred the launch reads the status column once.
+// Each deferred message is decoded by the generic loop from global memory,
+// its status and wire stats written, and its record (an escape when its term
+// does not fit the field: no side column here) appended to the region of its
+// tile's XCD slot with one atomic on the fill (a pool part past the cap, as
+// K3 draws them).
+constexpr u32 kScan = 32;
+__device__ __forceinline__ bool has_ff_byte(u32 v) {  // SWAR: a byte of v is 0xFF
+  const u32 y = ~v;
+  return ((y - 0x01010101u) & ~y & 0x80808080u) != 0;
+}
+__global__ __launch_bounds__(kBlock) void k_wire_deferred(Geometry geo, u32 k3grid, WireArgs W,
+                                                          Cols out, u32* __restrict__ counts,
+                                                          u64* __restrict__ shards,
+                                                          u8* __restrict__ chunk_slow, Pool pool) {
+  __shared__ u32 lds[4];
+  const u64 m0 = (u64(blockIdx.x) * kBlock + threadIdx.x) * kScan;
+  u32 sw[kScan / 4];
+  if (m0 + kScan <= geo.M && (reinterpret_cast<uintptr_t>(W.status + m0) & 15u) == 0) {
+#pragma unroll
+    for (u32 q = 0; q < kScan / 16; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(W.status + m0)[q];
+      sw[4 * q] = v.x;
+      sw[4 * q + 1] = v.y;
+      sw[4 * q + 2] = v.z;
+      sw[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (u32 q = 0; q < kScan / 4; ++q) {
+      u32 v = 0;
+#pragma unroll
+      for (u32 b = 0; b < 4; ++b) {
+        const u64 m = m0 + 4 * q + b;
+        v |= u32(m < geo.M ? W.status[m] : u8(0)) << (8 * b);
+      }
+      sw[q] = v;
+    }
+  }
+  bool any = false;
+#pragma unroll
+  for (u32 q = 0; q < kScan / 4; ++q) any |= has_ff_byte(sw[q]);
+  u32 cnt[4] = {0, 0, 0, 0};
+  u32 nbad = 0, nnon = 0;
+  for (u32 k = 0; any && k < kScan; ++k) {
+    if (u8(sw[k / 4] >> (8 * (k % 4))) != wire::kDeferred) continue;
+    const u64 m = m0 + k;
+    GroupRow row;
+    wire::load_row(W.R, m, row);
+    wire::load_ids(W.R, row);
+    const Decoded d = wire::decode_one<GlobalSrc, true>(W.R, W.nbytes, GlobalSrc{W.bytes},
+                                                         W.R.moff[m], W.R.moff[m + 1], row);
+    W.status[m] = u8(d.st);
+    ++cnt[d.st];
+    const RecClass c = classify(geo, d);
+    nbad += c.bad ? 1u : 0u;
+    nnon += c.non ? 1u : 0u;
+    if (!c.ok) continue;
+    const u32 g = d.group;
+    const u64 v = geo.fmt.encode(g & (geo.CH - 1u), d.flags & 0x0Fu,
+                                 (d.flags & QB_REC_REJECT) != 0, d.index, d.term, u32(m));
+    if (geo.fmt.term(v) == geo.fmt.tesc()) {
+      W.ri[m] = d.index;
+      W.rt[m] = d.term;
+    }
+    const u32 b = geo.sb_of(g);
+    const u32 x = region_slot_of_tile(geo, u32(m / kWtTile), k3grid);
+    const u32 rr = b * kRegionShards + x;
+    const u32 rel = atomicAdd(&counts[rr], 1u);
+    u64 dd;
+    if (rel < geo.cap) {
+      dd = u64(rr) * geo.cap + rel;
+    } else {
+      if (rel == geo.cap) mark_heavy(pool, b);
+      const u32 pid = pool_acquire(pool, rr, (rel - geo.cap) >> kTileShift);
+      dd = pid == kNoPart ? ~0ull : pool.base + u64(pid) * kTile + ((rel - geo.cap) & (u32(kTile) - 1u));
+    }
+    if (dd != ~0ull) {
+      out.mr[dd] = v;
+      out.cl[dd] = u8(geo.cl_of_chunk(geo.chunk_of(g)));
+    } else {
+      chunk_slow[geo.chunk_of(g)] = kChunkOverflow;
+    }
+  }
+  if (nbad | nnon) {
+    u64* sh = shards + u64(blockIdx.x % kShards) * QB_STAT_COUNT;
+    if (nbad) atomicAdd(sh + QB_STAT_BAD_GROUP, u64(nbad));
+    if (nnon) atomicAdd(sh + QB_STAT_NON_MEMBER, u64(nnon));
+  }
+  if (!W.wstats) return;
+  if (threadIdx.x < 4) lds[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const u32 v = wave_sum(cnt[q]);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&lds[q], v);
+  }
+  __syncthreads();
+  // statuses 0..3 are the stat slots QB_WIRE_OK .. QB_WIRE_CTX
+  if (threadIdx.x < 4 && lds[threadIdx.x]) atomicAdd(W.wstats + threadIdx.x, u64(lds[threadIdx.x]));
+}
+
+// ----------------------------------------------------------------- slow ----
+// The slow path's records re-decoded from the bytes: message i is a record of
+// a flagged chunk when its envelope group's chunk is flagged, its status is
+// OK and it decodes to a MsgAppResp from a member slot (what the records the
+// ingest would have written hold).  Only those messages are decoded.
+struct WireSrc {
+  WireArgs W;
+  __device__ __forceinline__ bool get(const Geometry& geo, const u8* __restrict__ chunk_slow,
+                                      u64 i, u32& g, u32& f, u64& idx, u64& t) const {
+    g = W.R.mgroup[i];
+    if (!(g < geo.G && chunk_slow[geo.chunk_of(g)] == 1 && W.status[i] == QB_WIRE_OK)) return false;
+    GroupRow row;
+    wire::load_row(W.R, i, row);
+    wire::load_ids(W.R, row);
+    const Decoded d = wire::decode_one<GlobalSrc, true>(W.R, W.nbytes, GlobalSrc{W.bytes},
+                                                         W.R.moff[i], W.R.moff[i + 1], row);
+    if (!classify(geo, d).ok) return false;
+    f = d.flags;
+    idx = d.index;
+    t = d.term;
+    return true;
+  }
+};
+
+template <int N>
+void launch_slow_wire(const Geometry& geo, const ApplyArgs& a, const WireArgs& W, u32* bar,
+                      unsigned grid, u64* stats, hipStream_t st) {
+  hipLaunchKernelGGL((k_bk_slow<FixedLay<N>, WireSrc>), dim3(grid), dim3(kBlock), 0, st, geo,
+                     FixedLay<N>{geo.G}, WireSrc{W}, a.gt, a.ts, a.chunk_slow, a.any_slow, bar,
+                     a.stepdown, a.match, a.next, a.active, a.committed, a.adv, a.stats, stats);
+}
+template <int... Ns>
+void dispatch_slow_wire(std::integer_sequence<int, Ns...>, int n, const Geometry& geo,
+                        const ApplyArgs& a, const WireArgs& W, u32* bar, unsigned grid, u64* stats,
+                        hipStream_t st) {
+  ((n == Ns + 1 ? launch_slow_wire<Ns + 1>(geo, a, W, bar, grid, stats, st) : void()), ...);
+}
+
+// Workspace: the tracker step's carve, then the escapes' index / term
+// columns (M u64 each, written only at escape positions).
+struct WtCarve {
+  Carve cv;
+  size_t ri, rt, total;
+};
+inline WtCarve wt_carve(const Geometry& geo) {
+  WtCarve w{};
+  w.cv = carve(geo, 1);
+  const size_t col = up256(sizeof(u64) * (geo.M ? geo.M : 1));
+  w.ri = w.cv.total;
+  w.rt = w.ri + col;
+  w.total = w.rt + col;
+  return w;
+}
+
+}  // namespace wt
+}  // namespace qb
+
+using namespace qb;
+
+extern "C" size_t qb_wire_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M) {
+  if (n < 1 || n > QB_MAX_SLOTS) return 0;
+  const wt::WtCarve w = wt::wt_carve(bk::geometry(n, G, M, 0, bk::kSbIl));
+  return w.cv.nrec_all <= 0xFFFFFFFFull ? w.total : 0;
+}
+
+extern "C" int qb_dev_ingest_fixed_tracker_step(
+    uint32_t n, uint64_t G, uint64_t M, const uint8_t* bytes, uint64_t nbytes,
+    const uint64_t* msg_off, const uint32_t* msg_group, const uint64_t* rows, const uint32_t* off,
+    const uint64_t* ids, const uint64_t* group_term, const uint64_t* term_start, uint64_t* match,
+    uint64_t* next, uint16_t* active, uint64_t* committed, uint32_t* stepdown_at,
+    uint8_t* advanced_out, uint8_t* status, uint64_t* wire_stats, uint64_t* stats,
+    void* workspace, size_t workspace_bytes, void* stream) {
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
+  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
+  QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
+  QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
+             "required state pointer is NULL");
+  QB_REQUIRE(M == 0 || (msg_off && msg_group && status), "msg_off, msg_group and status are required");
+  QB_REQUIRE(nbytes == 0 || bytes, "bytes is NULL");
+  QB_REQUIRE(rows || (off && ids), "rows, or off and ids, are required");
+  QB_REQUIRE(!rows || (reinterpret_cast<uintptr_t>(rows) & 15u) == 0, "rows must be 16-byte aligned");
+  const bk::Geometry geo = bk::geometry(n, G, M, 0, bk::kSbIl);
+  const wt::WtCarve wc = wt::wt_carve(geo);
+  const bk::Carve& cv = wc.cv;
+  QB_REQUIRE(cv.nrec_all <= 0xFFFFFFFFull,
+             "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
+             (unsigned long long)M, (unsigned long long)cv.nrec_all);
+  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)", (unsigned long long)G);
+  QB_REQUIRE(workspace && workspace_bytes >= wc.total,
+             "workspace too small: need %zu bytes (qb_wire_fixed_tracker_workspace_bytes)", wc.total);
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.zero_end - cv.shards, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
+  u64* ri = reinterpret_cast<u64*>(ws + wc.ri);
+  u64* rt = reinterpret_cast<u64*>(ws + wc.rt);
+  const wt::WireArgs W{nbytes, bytes,
+                       wire::RowArgs{G, reinterpret_cast<const u64*>(msg_off), msg_group, off,
+                                     reinterpret_cast<const u64*>(ids),
+                                     reinterpret_cast<const u64*>(rows)},
+                       status, ri, rt, reinterpret_cast<u64*>(wire_stats)};
+  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
+  u8* chunk_flags = reinterpret_cast<u8*>(ws + cv.chunk_flags);
+  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
+  const bk::Pool pool = bk::pool_at(ws, cv, geo);
+  if (M) {
+    const bk::Cols buf1 = bk::compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, bk::side_flag_at(ws, cv));
+    const unsigned grid = wt::wt_grid(geo);
+    hipLaunchKernelGGL(wt::k_wire_scatter, dim3(grid), dim3(wt::kWtThreads), 4 * sizeof(u32) * geo.NSB,
+                       st, geo, W, buf1, counts, shards, chunk_flags, pool, wt::wt_tiles(geo));
+    QB_CHECK_LAUNCH("k_wire_scatter");
+    hipLaunchKernelGGL(wt::k_wire_deferred, dim3(grid_for((M + wt::kScan - 1) / wt::kScan)), dim3(kBlock),
+                       0, st, geo, grid, W, buf1, counts, shards, chunk_flags, pool);
+    QB_CHECK_LAUNCH("k_wire_deferred");
+    bk::launch_split_compact(geo, cv, ws, reinterpret_cast<const u64*>(group_term), nullptr, st);
+    QB_CHECK_LAUNCH("k_bk_split_compact");
+  }
+  const bk::ApplyArgs a = bk::fixed_apply_args(
+      geo, cv, ws, ri, rt, reinterpret_cast<const u64*>(group_term),
+      reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
+      reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed), stepdown_at,
+      advanced_out);
+  bk::launch_fixed_apply(n, geo, cv, ws, a, st);
+  QB_CHECK_LAUNCH("k_bk_apply");
+  wt::dispatch_slow_wire(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, W,
+                         reinterpret_cast<u32*>(ws + cv.flags) + 16, bk::slow_blocks(),
+                         reinterpret_cast<u64*>(stats), st);
+  QB_CHECK_LAUNCH("k_bk_slow");
+  return QB_OK;
+}

@@ -75,6 +75,48 @@ def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: tor
     return ib, status[:M], mtype[:M]
 
 
+def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor,
+                        msg_group: torch.Tensor, rows: torch.Tensor = None,
+                        off: torch.Tensor = None, ids: torch.Tensor = None,
+                        advanced_out: torch.Tensor = None, wire_stats: torch.Tensor = None,
+                        reset_stats: bool = True, rearm: bool = True) -> torch.Tensor:
+    """The composed tick in one call (qb_dev_ingest_fixed_tracker_step): M
+    encoded responses decoded and stepped into ``tracker`` (a
+    ``batch.FixedTracker``), the commit advanced — ``ingest`` followed by
+    ``tracker.step`` on its records, without the record columns between them
+    (a message that is not a MsgAppResp steps nothing).  ``rows``
+    (``group_rows``) or ``off`` + ``ids`` give the groups' slot IDs.
+    ``reset_stats`` / ``rearm`` as ``FixedTracker.step``; ``wire_stats`` (int64
+    [4], nullable) accumulates the QB_WIRE_* counts.  Returns the per-message
+    status (u8 [M])."""
+    for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
+        if not t.is_cuda:
+            raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
+    if rows is None and (off is None or ids is None):
+        raise _lib.QuorumBatchError("rows, or off and ids, are required")
+    dev = buf.device
+    M = msg_group.numel()
+    if reset_stats:
+        tracker.stats.zero_()
+    if rearm:
+        tracker.stepdown_at.fill_(-1)
+    need = _lib.load().qb_wire_fixed_tracker_workspace_bytes(tracker.n, tracker.G, M)
+    if need == 0:
+        raise _lib.QuorumBatchError(f"batch of {M} messages too large for one call")
+    ws = getattr(tracker, "_wire_ws", None)
+    if ws is None or ws.numel() < need:
+        ws = tracker._wire_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    status = torch.empty(max(M, 1), dtype=torch.uint8, device=dev)
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    _lib.call("qb_dev_ingest_fixed_tracker_step", tracker.n, tracker.G, M, buf.data_ptr(), nbytes,
+              msg_off.data_ptr(), msg_group.data_ptr(), p(rows), p(off), p(ids), p(tracker.term),
+              p(tracker.term_start), p(tracker.match), p(tracker.next), p(tracker.active),
+              p(tracker.committed), p(tracker.stepdown_at), p(advanced_out), status.data_ptr(),
+              p(wire_stats), p(tracker.stats), ws.data_ptr(), ws.numel(),
+              torch.cuda.current_stream(dev).cuda_stream)
+    return status[:M]
+
+
 # ------------------------------------------------------- workload synth ---
 
 def _vfix(v: np.ndarray, n: int) -> np.ndarray:

@@ -672,6 +672,42 @@ int qb_dev_ingest_messages_rows(uint64_t M, const uint8_t* bytes, uint64_t nbyte
                                 uint8_t* status, uint8_t* msg_type, uint64_t* stats,
                                 void* stream);
 
+/* The composed per-tick path in one call (round 6): a tick's M encoded
+ * responses decoded and stepped into the FIXED ProgressTracker of G groups
+ * with n voters, the commit advanced — what a multi-raft host runs per tick
+ * between the transport (server/etcdserver/api/rafthttp/stream.go:466:
+ * Message.Unmarshal, raft.pb.go:1739-2061) and Ready (node.go:564-568:
+ * raft.Step -> stepLeader MsgAppResp -> maybeCommit, raft.go:847-921,
+ * 1100-1109, 1237-1259, 585-588).  Replaces qb_dev_ingest_messages[_rows]
+ * followed by qb_dev_fixed_tracker_step on its records, with the same
+ * result, minus the decoded record columns between them: the decoder writes
+ * the tracker step's level-1 buckets directly.
+ *   bytes, nbytes, msg_off [M+1], msg_group [M]: as qb_dev_ingest_messages;
+ *   rows (qb_dev_wire_group_rows, 16-byte aligned) or off [G+1] + ids: the
+ *     groups' slot IDs (rows preferred; ids are also read for members past
+ *     the row's 7);
+ *   group_term .. advanced_out, stats: as qb_dev_fixed_tracker_step
+ *     (stepdown_at[g] = the message index of the first higher-term response;
+ *     entry rule as there);
+ *   status [M] (required): QB_WIRE_* per message, as the ingest;
+ *   wire_stats [4] (nullable): QB_WIRE_* counts added, as the ingest's stats.
+ * A message that is not a decoded MsgAppResp steps nothing and counts as
+ * QB_STAT_BAD_GROUP (the ingest gives it group ~0); a From that is not a
+ * member of the group (QB_REC_NO_PROGRESS) counts as QB_STAT_NON_MEMBER.
+ * Workspace: qb_wire_fixed_tracker_workspace_bytes(n, G, M) bytes (0: the
+ * batch is too large for one call). */
+size_t qb_wire_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, uint64_t M);
+int qb_dev_ingest_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M, const uint8_t* bytes,
+                                     uint64_t nbytes, const uint64_t* msg_off,
+                                     const uint32_t* msg_group, const uint64_t* rows,
+                                     const uint32_t* off, const uint64_t* ids,
+                                     const uint64_t* group_term, const uint64_t* term_start,
+                                     uint64_t* match, uint64_t* next, uint16_t* active,
+                                     uint64_t* committed, uint32_t* stepdown_at,
+                                     uint8_t* advanced_out, uint8_t* status,
+                                     uint64_t* wire_stats, uint64_t* stats, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+
 /* ----------------------------------------------------------------------- */
 /* Configuration changes                             */
 /* ----------------------------------------------------------------------- */

@@ -24,6 +24,26 @@ def test_header_declares_what_binding_types():
     assert header_functions() == sorted(_lib.SIGNATURES)
 
 
+def header_arity():
+    """name -> number of parameters of each declaration in the header."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(qb_\w+)\s*\(([^;{)]*)\)\s*;", text):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_arity_matches_header():
+    """Every ctypes binding takes exactly the header's parameter count (an
+    argument past the argtypes would be passed as a C int: a truncated
+    stream or pointer)."""
+    ar = header_arity()
+    assert sorted(ar) == header_functions()
+    bad = {k: (ar[k], len(v[1])) for k, v in _lib.SIGNATURES.items() if ar[k] != len(v[1])}
+    assert not bad, bad
+
+
 def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in header_functions():

@@ -1,0 +1,226 @@
+"""The composed per-tick path in one call (qb_dev_ingest_fixed_tracker_step,
+etcd_amd/csrc/qb_wire_tracker.hip) against the chain of C oracles: the
+restated Message.Unmarshal (oracle/wire_oracle.c, raft.pb.go:1739-2061) and
+the sequential stepLeader MsgAppResp case (oracle/quorum_oracle.c,
+raft.go:847-921, 1100-1109, 1237-1259; progress.go:144-153; log.go:328-334)
+on the decoded records, with the fused entry's contract applied to them: a
+message that is not a decoded MsgAppResp steps nothing (counted as a bad
+group) and a From without Progress counts as a non-member."""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import raftpb_ref as W
+from tests import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _chain_oracle(n, G, buf, moff, grp, off, ids, st):
+    """C decode, the fused contract on its records, the sequential tracker."""
+    want = oc.ingest(buf, moff, grp, off, ids, threads=8)
+    g = want["group"].copy()
+    f = want["flags"].copy()
+    notrec = (want["status"] != 0) | (((f >> 4) & 3) != 0)
+    g[notrec] = 0xFFFFFFFF
+    nonm = ~notrec & ((f & 0x40) != 0)
+    f[nonm] = (f[nonm] & 0xF0) | 0x0F  # slot 15 >= n: a non-member
+    stats = oc.appresp_sequential(n, G, (g, f, want["index"], want["term"]), st, threads=8)
+    return want["status"], stats
+
+
+def _host_state(tr, G):
+    return {"match": _u64(tr.match).copy(),
+            "active": tr.active.cpu().numpy().view(np.uint16)[:G].copy(),
+            "term": _u64(tr.term).copy(), "term_start": _u64(tr.term_start).copy(),
+            "committed": _u64(tr.committed).copy(), "stepped_down": np.zeros(G, np.uint8)}
+
+
+def _check(tr, G, st, stats_dev, stats_want):
+    assert np.array_equal(_u64(tr.match), st["match"])
+    assert np.array_equal(_u64(tr.committed), st["committed"])
+    assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"])
+    sd = tr.stepdown_at.cpu().numpy().view(np.uint32)
+    assert np.array_equal(sd != 0xFFFFFFFF, st["stepped_down"] != 0)
+    assert np.array_equal(stats_dev[:7], stats_want[:7].astype(np.int64)), (stats_dev, stats_want)
+
+
+def test_fused_tick_vs_chain_of_c_oracles():
+    """The bench row's workload (tools/bench_configs.py wire_tracker_tick:
+    canonical MsgAppResp, leader terms 20006-20007: side records) at 64K
+    groups over three ticks, against the C chain; and the same ticks through
+    the device chain (ingest + tracker step) reach the same state."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs as bc
+    G, n = 1 << 16, 5
+    tr, snap, ticks, rows, off, ids = bc.wire_tracker_tick(G, 3, dev_=torch.device("cuda"))
+    st = _host_state(tr, G)
+    h_off, h_ids = off.cpu().numpy().view(np.uint32), _u64(ids)
+    wst = torch.zeros(4, dtype=torch.int64, device="cuda")
+    for buf, nbytes, moff, grp, _direct in ticks:
+        status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows, wire_stats=wst)
+        want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], _u64(moff),
+                                                grp.cpu().numpy().view(np.uint32), h_off, h_ids, st)
+        assert np.array_equal(status.cpu().numpy(), want_status)
+        _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+    assert int(wst[0].item()) == 3 * G and int(wst[1:].sum().item()) == 0
+    fused = {k: getattr(tr, k).clone() for k in snap}
+    for k, v in snap.items():
+        getattr(tr, k).copy_(v)
+    for buf, nbytes, moff, grp, _direct in ticks:
+        ib, status, _ = wire.ingest(buf, nbytes, moff, grp, off, ids, rows=rows)
+        tr.step(batch.AppRespBatch(ib.group, ib.flags, ib.index, ib.term))
+    for k in snap:
+        assert torch.equal(getattr(tr, k), fused[k]), k
+    assert int((st["committed"] > 0).sum()) > G // 2
+
+
+def _mixed_tick(r, G, n, gterm, ids_of, k, hot=None, big_waves=0):
+    """One tick of M = 4G messages of every kind the fused path must tell
+    apart, host-encoded (oracle/raftpb_ref.py marshal_message)."""
+    M = 4 * G
+    msgs, grps = [], []
+    for i in range(M):
+        g = hot if hot is not None and r.random() < 0.3 else r.randrange(G)
+        ids = ids_of(g)
+        s = r.randrange(n)
+        t = int(gterm[g])
+        x = r.random()
+        term = t - 1 if x < 0.04 and t > 0 else t + 1 if x < 0.045 else t
+        idx = (1 << 30) + g * 97 + k * 64 + r.randrange(200)
+        if r.random() < 0.02:
+            idx = (1 << 41) + g  # past the record's 40-bit index: an escape
+        rej = r.random() < 0.1
+        y = r.random()
+        if y < 0.05:     # heartbeat response: decoded, not stepped
+            b = W.marshal_message(9, ids[0], ids[s], term, 0, 0, (), 0, W.EMPTY_SNAPSHOT, False, 0,
+                                  r.getrandbits(63).to_bytes(8, "big") if r.random() < 0.5 else None)
+        elif y < 0.10:   # From without Progress
+            b = W.marshal_message(4, ids[0], 999_999_999 + i, term, 0, idx, (), 0, W.EMPTY_SNAPSHOT,
+                                  rej, 0, None)
+        elif y < 0.14:   # non-canonical (a field moved to the front): the generic decoder
+            b = W._key(6, 0) + W.varint(idx) + W.marshal_message(4, ids[0], ids[s], term, 0, idx,
+                                                                (), 0, W.EMPTY_SNAPSHOT, rej, 0)
+        elif y < 0.16:   # truncated: an unmarshal error
+            full = W.marshal_message(4, ids[0], ids[s], term, 0, idx, (), 0, W.EMPTY_SNAPSHOT, rej, 0)
+            b = full[: r.randrange(1, len(full))]
+        elif y < 0.17:   # another message type
+            b = W.marshal_message(3, ids[0], ids[s], term, 0, idx)
+        else:
+            b = W.marshal_message(4, ids[0], ids[s], term, 0, idx, (), 0, W.EMPTY_SNAPSHOT, rej, 0)
+        if r.random() < 0.01:
+            g = G + r.randrange(5)  # envelope group past the shard
+        msgs.append(b)
+        grps.append(g)
+    # whole waves of large messages (entries): past a wave's LDS slice
+    for w in range(big_waves):
+        base = r.randrange(M // 64) * 64
+        for j in range(64):
+            g = grps[base + j] % G
+            ids = ids_of(g)
+            ent = W.marshal_entry(1, 2, 0, bytes(120))
+            msgs[base + j] = W.marshal_message(4, ids[0], ids[1 + j % (n - 1)], int(gterm[g]), 0,
+                                               (1 << 30) + g * 97 + k * 64 + 300, (ent,))
+            grps[base + j] = g
+    return msgs, grps
+
+
+@pytest.mark.parametrize("large_frac,hot,big_waves", [(0.05, False, 0), (0.6, False, 3),
+                                                      (0.6, True, 0), (0.0, False, 2)])
+def test_fused_mixed_stream_vs_chain_of_c_oracles(large_frac, hot, big_waves):
+    """Every kind of message in one stream — stale / higher-term (the slow
+    path re-decodes its chunk) / rejects, heartbeat responses and another
+    type, non-members, groups past the shard, non-canonical encodings and
+    whole waves of large messages (the deferred launch), truncations,
+    indexes past 2^40 and terms past 2^32 (escapes) — with group terms small,
+    past the record's term field (side records when dense in a tile, escapes
+    when rare: large_frac) and past 2^32; hot: 30 % of a tick on one group
+    (K4 folds it).  Four ticks against the C chain, state and every stat."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(int(large_frac * 100) + 7 * hot + big_waves)
+    G, n = 1 << 12, 5
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (1000 + np.arange(n * G, dtype=np.uint64) * 3)  # ascending per group
+    ids_of = lambda g: [int(v) for v in ids[n * g: n * g + n]]  # noqa: E731
+    gterm = np.where(np.array([r.random() < large_frac for _ in range(G)]),
+                     np.array([r.randrange(2048, 1 << 20) for _ in range(G)], np.uint64),
+                     np.uint64(7)).astype(np.uint64)
+    gterm[: G // 64] = (1 << 33) + np.arange(G // 64, dtype=np.uint64)  # past 2^32: escapes
+    dev = torch.device("cuda")
+    tr = batch.FixedTracker(n, G, dev)
+    tr.term.copy_(torch.from_numpy(gterm.view(np.int64)))
+    tr.term_start.fill_(1 << 30)
+    tr.match[0].fill_((1 << 31))
+    for s in range(1, n):
+        tr.match[s].copy_(torch.from_numpy(((1 << 30) + np.arange(G, dtype=np.int64) * 97)))
+    tr.commit_advance()
+    st = _host_state(tr, G)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    rows = wire.group_rows(d_off, d_ids)
+    wst = torch.zeros(4, dtype=torch.int64, device=dev)
+    want_w = np.zeros(4, np.int64)
+    for k in range(4):
+        msgs, grps = _mixed_tick(r, G, n, gterm, ids_of, k, hot=r.randrange(G) if hot else None,
+                                 big_waves=big_waves)
+        buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+        status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows, wire_stats=wst)
+        want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], _u64(moff),
+                                                grp.cpu().numpy().view(np.uint32), off, ids, st)
+        assert np.array_equal(status.cpu().numpy(), want_status)
+        want_w += np.bincount(want_status, minlength=4)[:4]
+        _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+        # the higher-term records stepped some groups down: re-arm them
+        tr.stepdown_at.fill_(-1)
+        st["stepped_down"][:] = 0
+    assert np.array_equal(wst.cpu().numpy(), want_w)
+
+
+def test_fused_off_ids_and_empty():
+    """off + ids instead of the row table (a member past the row's 7 read from
+    ids), and M = 0 (the tracker still runs maybeCommit, as the step)."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(5)
+    G, n = 1 << 10, 9
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (50 + np.arange(n * G, dtype=np.uint64) * 2)
+    dev = torch.device("cuda")
+    tr = batch.FixedTracker(n, G, dev)
+    tr.term.fill_(3)
+    tr.term_start.fill_(10)
+    st = _host_state(tr, G)
+    msgs, grps = [], []
+    for i in range(3 * G):
+        g = r.randrange(G)
+        s = r.randrange(n)
+        msgs.append(W.marshal_message(4, int(ids[n * g]), int(ids[n * g + s]), 3, 0,
+                                      20 + r.randrange(100), (), 0, W.EMPTY_SNAPSHOT,
+                                      r.random() < 0.1, 0))
+        grps.append(g)
+    buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, off=d_off, ids=d_ids)
+    want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], _u64(moff),
+                                            grp.cpu().numpy().view(np.uint32), off, ids, st)
+    assert np.array_equal(status.cpu().numpy(), want_status)
+    _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+    assert int((st["match"][8] > 0).sum()) > 0  # slot 8: past the 7 IDs a row holds
+    empty = torch.zeros(1, dtype=torch.uint8, device=dev)
+    mo = torch.zeros(1, dtype=torch.int64, device=dev)
+    eg = torch.zeros(0, dtype=torch.int32, device=dev)
+    wire.ingest_tracker_step(tr, empty, 0, mo, eg, off=d_off, ids=d_ids)
+    assert np.array_equal(_u64(tr.committed), st["committed"])

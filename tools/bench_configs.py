@@ -293,15 +293,20 @@ def wire_tracker_tick(G, nb, E=64, seed=77, dev_=None):
     return tr, snap, ticks, rows, off, ids
 
 
-def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=None):
-    """Composed row: wire bytes -> qb_dev_ingest_messages_rows -> records ->
-    qb_dev_fixed_tracker_step, per tick (rafthttp/stream.go:466 decode ->
-    raft.go:1106-1259 stepLeader MsgAppResp -> maybeCommit), G groups and G
-    messages per tick.  Parity in the row (size-independent): every decoded
-    column equals the columns the bytes were encoded from, every status OK,
-    and the tracker state after the ticks equals the state the direct step
-    (same columns, no wire) reaches — bit-exact.  The GPU suite checks the
-    chain against the C oracles (tests/test_gpu_wire.py)."""
+def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=None,
+                        fused_only=False):
+    """Composed row: wire bytes -> tracker tick, per tick (rafthttp/stream.go:466
+    decode -> raft.go:1106-1259 stepLeader MsgAppResp -> maybeCommit), G
+    groups and G messages per tick, in one call (round 6:
+    qb_dev_ingest_fixed_tracker_step — the decoder writes the tracker step's
+    level-1 buckets, no record columns between them); beside it the chain of
+    round 5 (qb_dev_ingest_messages_rows -> records -> qb_dev_fixed_tracker_step)
+    and its two halves.  Parity in the row (size-independent): every status
+    OK and the tracker state after the ticks through the one call equals the
+    state the direct step (same columns, no wire) reaches, and so does the
+    chain's (its decoded columns equal the encoded ones) — bit-exact.  The GPU
+    suite checks both against the C oracles (tests/test_gpu_wire.py,
+    tests/test_gpu_wire_tracker.py)."""
     reporter = reporter or report
     from etcd_amd.quorum import wire
     nb = warm + reps
@@ -312,9 +317,12 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
         for k_, v_ in snap.items():
             getattr(tr, k_).copy_(v_)
 
-    def composed(tk):
+    def chain(tk):
         ib, _, _ = wire.ingest(tk[0], tk[1], tk[2], tk[3], off, ids, rows=rows)
         tr.step(batch.AppRespBatch(ib.group, ib.flags, ib.index, ib.term))
+
+    def fused(tk):
+        wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows)
 
     def timed(fn):
         ev = HipEvents(2)
@@ -333,12 +341,21 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
                 ts.append(ev.elapsed_ms(0, 1) / 1e3 / reps)
         ev.close()
         return float(np.median(ts))
-    t = timed(composed)
-    t_ingest = timed(lambda tk: wire.ingest(tk[0], tk[1], tk[2], tk[3], off, ids, rows=rows))
-    t_step = timed(lambda tk: tr.step(tk[4]))
-    # parity: the composed chain against the direct step over every tick
-    restore()
+    t = timed(fused)
+    if fused_only:  # development A/B: the one call alone
+        t_chain = t_ingest = t_step = float("nan")
+    else:
+        t_chain = timed(chain)
+        t_ingest = timed(lambda tk: wire.ingest(tk[0], tk[1], tk[2], tk[3], off, ids, rows=rows))
+        t_step = timed(lambda tk: tr.step(tk[4]))
+    # parity: the one call and the chain against the direct step over every tick
     bad = 0
+    restore()
+    for tk in ticks:
+        status = wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows)
+        bad += int((status != 0).sum())
+    via_fused = {k_: getattr(tr, k_).clone() for k_ in snap}
+    restore()
     for tk in ticks:
         ib, status, _ = wire.ingest(tk[0], tk[1], tk[2], tk[3], off, ids, rows=rows)
         d = tk[4]
@@ -352,20 +369,24 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
         tr.step(tk[4])
     for k_ in snap:
         bad += int((getattr(tr, k_) != via_wire[k_]).sum())
+        bad += int((getattr(tr, k_) != via_fused[k_]).sum())
     nbytes = ticks[0][1]
     del ticks
     # algorithmic bytes per message: its wire bytes, msg_off 8, envelope group
-    # 4, the group's slot IDs 40 (wire row); the tracker's match RMW 16 and
-    # the commit advance 64 per group (configs[4] row) — the decoded records
-    # between the two are intermediate, not algorithmic
-    algo = nbytes + G * (8 + 4 + 40) + G * (16 + 64)
+    # 4, the group's slot IDs 40 (wire row), its status byte 1; the tracker's
+    # match RMW 16 and the commit advance 64 per group (configs[4] row) — the
+    # decoded records are intermediate, not algorithmic
+    algo = nbytes + G * (8 + 4 + 40 + 1) + G * (16 + 64)
     reporter("wire -> tracker tick (composed)", G, t, algo,
-             {"unit": "group-steps/s", "ingest_us": t_ingest * 1e6, "tracker_step_us": t_step * 1e6,
+             {"unit": "group-steps/s", "form": "one call (qb_dev_ingest_fixed_tracker_step)",
+              "chain_us": t_chain * 1e6, "chain_ingest_us": t_ingest * 1e6,
+              "chain_tracker_step_us": t_step * 1e6,
               "bytes_per_message": nbytes / G,
               "parity": "bit-exact" if bad == 0 else f"MISMATCH {bad}",
-              "parity_check": f"{nb} ticks of {G} messages: decoded columns == encoded columns, "
-                              "every status OK, tracker state (match, committed, active, "
-                              "stepdown_at) == the direct step's"})
+              "parity_check": f"{nb} ticks of {G} messages: every status OK; tracker state "
+                              "(match, committed, active, stepdown_at) through the one call == "
+                              "through the chain == the direct step's; the chain's decoded "
+                              "columns == the encoded columns"})
     if bad:
         raise AssertionError(f"wire -> tracker tick: {bad} mismatches")
 
@@ -819,6 +840,8 @@ def main():
         confchange_config(1 << 23, a.reps)
     if "wire-tracker" in which:
         wire_tracker_config(1 << 24, a.reps)
+    if "wire-tracker-fused" in which:  # development A/B: the one call alone
+        wire_tracker_config(1 << 24, a.reps, fused_only=True)
 
 
 if __name__ == "__main__":
