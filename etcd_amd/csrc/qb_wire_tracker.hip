@@ -58,7 +58,7 @@ using wire::RowArgs;
 // slice in the same bytes (3584 B per wave: 64 messages of up to ~54 B on
 // average; a wave whose span is longer is deferred).
 #ifndef QB_WT_THREADS
-#define QB_WT_THREADS 1024
+#define QB_WT_THREADS 512
 #endif
 constexpr u32 kWtThreads = QB_WT_THREADS;
 constexpr u32 kWtTile = kWtThreads * kPer;
@@ -181,6 +181,7 @@ __global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
   // (kNoBin: none), its rank in the bin, the encoded record, a side term
   u32 bj[kPer], rj[kPer], tj[kPer];
   u64 vj[kPer];
+  u32 stw = 0;  // the status byte of each sub-round's message (byte r: sub-round r)
   // Sub-round pipeline.  Every sub-round's message offsets and envelope
   // groups are requested up front; sub-round r + 1's group row and byte span
   // (into the wave's other slice) are requested before sub-round r is
@@ -228,7 +229,9 @@ __global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
     if (in && p0 >= lbase && p1 <= lend && p0 <= p1)
       d = wire::decode_one<LdsSrc, false>(W.R, W.nbytes, LdsSrc{slice_r, lbase}, p0, p1, row);
     const bool dec = in && d.st != wire::kDeferred;  // decoded here (else K3d's)
-    if (in) __builtin_nontemporal_store(u8(d.st), W.status + m);
+    // the status bytes are stored after the last sub-round: a store issued
+    // here would be one more access the next sub-round's vmcnt wait covers
+    stw |= u32(u8(d.st)) << (8 * r);
     wtally.add(0, dec && d.st == QB_WIRE_OK);
     wtally.add(1, dec && d.st == QB_WIRE_UNMARSHAL);
     wtally.add(2, dec && d.st == QB_WIRE_TYPE);
@@ -250,6 +253,11 @@ __global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
       W.ri[m] = d.index;
       W.rt[m] = d.term;
     }
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const u32 k = u32(r) * kWtThreads + threadIdx.x;
+    if (k < nrec) __builtin_nontemporal_store(u8(stw >> (8 * r)), W.status + t0 + k);
   }
   if (nside) atomicAdd(&s_nside, nside);
   if (W.wstats) {

@@ -118,6 +118,42 @@ def check_tracker_stream(dev, csr: bool, G: int, ticks: int, parity_groups: int 
             f"{ticks} ticks (match, committed, active, stepdown{', stats' if stats else ''})")
 
 
+def check_wire_tracker(dev, G: int = 1 << 18, ticks: int = 2) -> str:
+    """The composed tick in one call (qb_dev_ingest_fixed_tracker_step) on the
+    bench row's workload (tools/bench_configs.py wire_tracker_tick: encoded
+    MsgAppResp, leader terms past the record's term field) against the C
+    chain: the restated Message.Unmarshal (oracle/wire_oracle.c), then the
+    sequential tracker oracle on its records; statuses, state and every stat
+    after each tick."""
+    from etcd_amd.quorum import wire
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs as bc
+    d = torch.device(dev)
+    n = 5
+    tr, _snap, tks, rows, off, ids = bc.wire_tracker_tick(G, ticks, dev_=d)
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+    st = {"match": u64(tr.match).copy(), "active": tr.active.cpu().numpy().view(np.uint16)[:G].copy(),
+          "term": u64(tr.term).copy(), "term_start": u64(tr.term_start).copy(),
+          "committed": u64(tr.committed).copy(), "stepped_down": np.zeros(G, np.uint8)}
+    h_off, h_ids = off.cpu().numpy().view(np.uint32), u64(ids)
+    threads = host_threads()
+    for k, (buf, nbytes, moff, grp, _direct) in enumerate(tks):
+        status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows)
+        want = oc.ingest(buf.cpu().numpy()[:nbytes], u64(moff), grp.cpu().numpy().view(np.uint32),
+                         h_off, h_ids, threads=threads)
+        assert np.array_equal(status.cpu().numpy(), want["status"]), f"wire-tracker tick {k}: status"
+        stats = oc.appresp_sequential(n, G, (want["group"], want["flags"], want["index"],
+                                             want["term"]), st, threads=threads)
+        assert np.array_equal(u64(tr.match), st["match"]), f"wire-tracker tick {k}: match"
+        assert np.array_equal(u64(tr.committed), st["committed"]), f"wire-tracker tick {k}: committed"
+        assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"]), \
+            f"wire-tracker tick {k}: active"
+        assert tr.stats.cpu().numpy()[:7].tolist() == [int(x) for x in stats[:7]], \
+            f"wire-tracker tick {k}: stats"
+    return (f"qb_dev_ingest_fixed_tracker_step {G} messages x {ticks} ticks (status, match, "
+            f"committed, active, stats)")
+
+
 NONE = 0xFFFFFFFF
 
 
