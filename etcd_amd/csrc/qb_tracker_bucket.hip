@@ -117,7 +117,8 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
   u32 bj[kPer], rj[kPer];
   u64 vj[kPer];
   u32 nbad = 0, nnon = 0;  // wave-uniform: invalid records
-  u32 mside = 0;           // compact: side-form records (staged terms at their tile index)
+  u32 mside = 0;           // compact: side-form records
+  u32 tj[kPer];            // compact: a side record's term (0 otherwise)
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const u32 k = rk(j);
@@ -139,12 +140,9 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     if constexpr (COMPACT) {
       vj[j] = geo.fmt.encode_side(g[j] & (geo.CH - 1u), f[j] & 0x0Fu, (f[j] & 0x80u) != 0, vi[j],
                                   vt[j], u32(t0 + k));
-      // a side record's term, staged at its tile index in the (not yet
-      // used) record stage
-      if (ok && geo.fmt.term(vj[j]) == geo.fmt.tside()) {
-        reinterpret_cast<u32*>(L.stage)[k] = u32(vt[j]);
-        ++mside;
-      }
+      const bool sr = ok && geo.fmt.term(vj[j]) == geo.fmt.tside();
+      tj[j] = sr ? u32(vt[j]) : 0u;
+      mside += sr ? 1u : 0u;
     }
   }
   if constexpr (COMPACT)
@@ -184,15 +182,6 @@ __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_bk_scatte
     // lines cost more than a few records' gathers).
     const bool side = s_nesc * kSideDen > nvalid;  // (block-uniform)
     u32* t32 = reinterpret_cast<u32*>(L.rank);     // (rank + perm: unused by this form)
-    u32 tj[kPer];
-    if (side) {  // the staged terms, read before the stage is overwritten below
-#pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        tj[j] = (bj[j] & 0xFFFFu) != u32(kNoBin) && geo.fmt.term(vj[j]) == geo.fmt.tside()
-                    ? reinterpret_cast<const u32*>(L.stage)[rk(j)]
-                    : 0u;
-      __syncthreads();
-    }
     // after the scan each record is stored at its sorted LDS slot with its
     // bin and chunk-low (and, side, its term), and the output pass reads the
     // slots in order
