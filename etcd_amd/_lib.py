@@ -92,6 +92,9 @@ SIGNATURES = {
     "qb_wire_fixed_tracker_workspace_bytes": (C.c_size_t, [_u32, _u64, _u64]),
     "qb_dev_ingest_fixed_tracker_step": (_i32, [_u32, _u64, _u64, _p, _u64] + [_p] * 17 +
                                          [C.c_size_t, _p]),
+    "qb_wire_csr_tracker_workspace_bytes": (C.c_size_t, [_u64, _u32, _u64]),
+    "qb_dev_ingest_csr_tracker_step": (_i32, [_u64, _u32, _p, _p, _u64, _p, _u64] + [_p] * 16 +
+                                       [C.c_size_t, _p]),
     "qb_conf_change_workspace_bytes": (C.c_size_t, [_u64]),
     "qb_dev_conf_change": (_i32, [_p, _p, _p, C.c_size_t, _p]),
     "qb_shard_range": (_i32, [_u64, _i32, _i32, _p, _p]),

@@ -34,6 +34,7 @@
 // matters) go to the slow path (qb_tracker_slow.h) exactly as in the FIXED
 // step.
 #include "qb_tracker_slow.h"
+#include "qb_wire_src.h"
 
 namespace qb {
 namespace bk {
@@ -406,15 +407,48 @@ void launch_apply(const Geometry& geo, Cols recs, const u32* counts, const u32* 
   else launch_apply_rows<WMAX, SECOND, false>(geo, recs, counts, cs, a, st);
 }
 
-template <int WMAX>
+// The apply launches and the slow path over a record source (ColSrc: the
+// batch's columns; wt::WireSrc: the composed step re-decodes the bytes).
+template <int WMAX, class Src>
 void launch_csr_step(const Geometry& geo, Cols recs, const u32* counts, const u32* cs,
-                     const CsrStepArgs& a, const SlowArgs& sa, u64* stats, hipStream_t st) {
+                     const CsrStepArgs& a, const Src& src, u32* bar, unsigned grid, u64* stats,
+                     hipStream_t st) {
   launch_apply<WMAX, false>(geo, recs, counts, cs, a, st);
   if constexpr (WMAX > kCsrCapW) launch_apply<WMAX, true>(geo, recs, counts, cs, a, st);
-  hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>, ColSrc>), dim3(sa.grid), dim3(kBlock), 0, st, geo,
-                     CsrLay<WMAX>{a.off, a.cfg}, ColSrc{sa.rg, sa.rf, sa.ri, sa.rt}, a.gt, a.ts,
-                     a.chunk_slow, a.any_slow, sa.bar, a.stepdown, a.match, a.next, a.active,
-                     a.committed, a.adv, a.shards, stats);
+  hipLaunchKernelGGL((k_bk_slow<CsrLay<WMAX>, Src>), dim3(grid), dim3(kBlock), 0, st, geo,
+                     CsrLay<WMAX>{a.off, a.cfg}, src, a.gt, a.ts, a.chunk_slow, a.any_slow, bar,
+                     a.stepdown, a.match, a.next, a.active, a.committed, a.adv, a.shards, stats);
+}
+
+// The step's arguments over a carved workspace (ri / rt: the escapes' exact
+// index and term by batch position).
+CsrStepArgs csr_step_args(const Geometry& geo, const Carve& cv, char* ws, const u64* ri,
+                          const u64* rt, const u32* off, const u32* cfg, const u64* group_term,
+                          const u64* term_start, u64* match, u64* next, u16* active,
+                          u64* committed, u32* stepdown_at, u8* advanced) {
+  const Pool pool = pool_at(ws, cv, geo);
+  return CsrStepArgs{ri, rt, side_at(ws, cv), off, cfg, group_term, term_start, match, next,
+                     active, committed, stepdown_at, advanced,
+                     reinterpret_cast<u8*>(ws + cv.chunk_flags), reinterpret_cast<u32*>(ws + cv.flags),
+                     reinterpret_cast<u64*>(ws + cv.shards), reinterpret_cast<const u32*>(ws + cv.ptab),
+                     HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
+                               geo.NC < kHeavyBlocks ? geo.NC : kHeavyBlocks}};
+}
+
+template <class Src>
+void dispatch_csr_step(u32 wmax, const Geometry& geo, const Carve& cv, char* ws,
+                       const CsrStepArgs& a, const Src& src, u64* stats, hipStream_t st) {
+  const Cols buf2 = compact_at(ws + cv.buf2, nullptr, ws + cv.side2, side_flag_at(ws, cv));
+  const u32* cs = reinterpret_cast<const u32*>(ws + cv.chunk_start);
+  const u32* counts = reinterpret_cast<const u32*>(ws + cv.counts);
+  u32* bar = reinterpret_cast<u32*>(ws + cv.flags) + 16;
+  const unsigned grid = slow_blocks();
+  switch (wmax) {
+    case 4: launch_csr_step<4>(geo, buf2, counts, cs, a, src, bar, grid, stats, st); break;
+    case 8: launch_csr_step<8>(geo, buf2, counts, cs, a, src, bar, grid, stats, st); break;
+    case 12: launch_csr_step<12>(geo, buf2, counts, cs, a, src, bar, grid, stats, st); break;
+    default: launch_csr_step<16>(geo, buf2, counts, cs, a, src, bar, grid, stats, st); break;
+  }
 }
 
 }  // namespace bk
@@ -422,12 +456,36 @@ void launch_csr_step(const Geometry& geo, Cols recs, const u32* counts, const u3
 
 using namespace qb;
 
-namespace {
+namespace qb {
+namespace bk {
 u32 csr_wmax(uint32_t max_slots) {
   const u32 w = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
   return w <= 4 ? 4u : w <= 8 ? 8u : w <= 12 ? 12u : 16u;
 }
-}  // namespace
+Geometry csr_geometry(uint64_t G, uint32_t max_slots, uint64_t M) {
+  const u32 wmax = csr_wmax(max_slots);
+  // the bucketing filters slot >= the table bound (geo.n) as non-member; the
+  // chunk size follows the LDS run capacity (chunk_groups(wmax))
+  Geometry geo = geometry(wmax, G, M, csr_chunk_groups(wmax), kSbIl);
+  geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
+  return geo;
+}
+}  // namespace bk
+namespace wt {
+// The composed CSR step's apply half (qb_wire_tracker.hip): K5 and the slow
+// path re-decoding a flagged chunk's messages from the bytes.
+void csr_apply_wire(u32 wmax, const bk::Geometry& geo, const bk::Carve& cv, char* ws,
+                    const u32* off, const u32* cfg, const u64* group_term, const u64* term_start,
+                    u64* match, u64* next, u16* active, u64* committed, u32* stepdown_at,
+                    u8* advanced, const WireArgs& W, u64* stats, hipStream_t st) {
+  const bk::CsrStepArgs a = bk::csr_step_args(geo, cv, ws, W.ri, W.rt, off, cfg, group_term,
+                                              term_start, match, next, active, committed,
+                                              stepdown_at, advanced);
+  bk::dispatch_csr_step(wmax, geo, cv, ws, a, WireSrc{W}, stats, st);
+}
+}  // namespace wt
+}  // namespace qb
+using bk::csr_wmax;
 
 extern "C" size_t qb_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
   if (max_slots > QB_MAX_SLOTS) return 0;
@@ -455,10 +513,7 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
   QB_REQUIRE(M == 0 || (rec_group && rec_flags && rec_index && rec_term),
              "record pointer is NULL");
   const u32 wmax = csr_wmax(max_slots);
-  // the bucketing filters slot >= the table bound (geo.n) as non-member; the
-  // chunk size follows the LDS run capacity (chunk_groups(wmax))
-  bk::Geometry geo = bk::geometry(wmax, G, M, bk::csr_chunk_groups(wmax), bk::kSbIl);
-  geo.n = max_slots == 0 ? u32(QB_MAX_SLOTS) : max_slots;
+  const bk::Geometry geo = bk::csr_geometry(G, max_slots, M);
   const bk::Carve cv = bk::carve(geo, 1);
   QB_REQUIRE(cv.nrec_all <= 0xFFFFFFFFull,
              "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
@@ -469,9 +524,6 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
              (unsigned long long)G);
   hipStream_t st = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
-  u32* cs = reinterpret_cast<u32*>(ws + cv.chunk_start);
-  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-  const bk::Cols buf2 = bk::compact_at(ws + cv.buf2, nullptr, ws + cv.side2, bk::side_flag_at(ws, cv));
   u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
   const auto* ri = reinterpret_cast<const u64*>(rec_index);
   const auto* rtm = reinterpret_cast<const u64*>(rec_term);
@@ -481,35 +533,13 @@ extern "C" int qb_dev_csr_tracker_step(uint64_t G, uint32_t max_slots, const uin
                                       off);
     if (rc != QB_OK) return rc;
   }
-  const bk::Pool pool = bk::pool_at(ws, cv, geo);
-  const bk::CsrStepArgs a{ri,
-                          rtm,
-                          bk::side_at(ws, cv),
-                          off,
-                          cfg,
-                          reinterpret_cast<const u64*>(group_term),
-                          reinterpret_cast<const u64*>(term_start),
-                          reinterpret_cast<u64*>(match),
-                          reinterpret_cast<u64*>(next),
-                          active,
-                          reinterpret_cast<u64*>(committed),
-                          stepdown_at,
-                          advanced_out,
-                          reinterpret_cast<u8*>(ws + cv.chunk_flags),
-                          reinterpret_cast<u32*>(ws + cv.flags),
-                          shards,
-                          reinterpret_cast<const u32*>(ws + cv.ptab),
-                          bk::HeavyArgs{pool.sbflag, pool.heavy, pool.nheavy,
-                                        geo.NC < bk::kHeavyBlocks ? geo.NC : bk::kHeavyBlocks}};
-  const bk::SlowArgs sa{rec_group, rec_flags, ri, rtm, reinterpret_cast<u32*>(ws + cv.flags) + 16,
-                        bk::slow_blocks()};
-  u64* stt = reinterpret_cast<u64*>(stats);
-  switch (wmax) {
-    case 4: bk::launch_csr_step<4>(geo, buf2, counts, cs, a, sa, stt, st); break;
-    case 8: bk::launch_csr_step<8>(geo, buf2, counts, cs, a, sa, stt, st); break;
-    case 12: bk::launch_csr_step<12>(geo, buf2, counts, cs, a, sa, stt, st); break;
-    default: bk::launch_csr_step<16>(geo, buf2, counts, cs, a, sa, stt, st); break;
-  }
+  const bk::CsrStepArgs a = bk::csr_step_args(
+      geo, cv, ws, ri, rtm, off, cfg, reinterpret_cast<const u64*>(group_term),
+      reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
+      reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed), stepdown_at,
+      advanced_out);
+  bk::dispatch_csr_step(wmax, geo, cv, ws, a, bk::ColSrc{rec_group, rec_flags, ri, rtm},
+                        reinterpret_cast<u64*>(stats), st);
   QB_CHECK_LAUNCH("k_csr_apply / k_bk_slow");
   return QB_OK;
 }

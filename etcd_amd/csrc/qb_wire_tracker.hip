@@ -38,7 +38,7 @@
 // (an index >= 2^40, a term >= 2^32 - 1, a large term in a tile where they
 // are rare) keep their exact index and term in two batch-order columns of
 // the workspace, written only at their own positions.
-#include "qb_wire_decode.h"
+#include "qb_wire_src.h"
 #include "qb_bucket_tile.h"
 #include "qb_tracker_slow.h"
 
@@ -74,27 +74,6 @@ struct alignas(16) WtLds {
 };
 static_assert(kWaves * kSlice <= offsetof(WtLds, cl), "the slices fit stage..bin");
 static_assert(kWtTile <= u32(kTile), "a tile's run spans at most two pool parts");
-
-struct WireArgs {
-  u64 nbytes;
-  const u8* bytes;
-  RowArgs R;        // G, msg_off, msg_group, off, ids, rows
-  u8* status;       // per message (QB_WIRE_*)
-  u64 *ri, *rt;     // escapes: the exact index / term at the message's position
-  u64* wstats;      // nullable: QB_WIRE_* counts
-};
-
-// The leader-inbox record of a decoded message as the tracker takes it:
-// valid (a MsgAppResp of a group < G from a member slot < n), or counted
-// bad (not a record of a group) / non-member.
-struct RecClass {
-  bool ok, bad, non;
-};
-__device__ __forceinline__ RecClass classify(const Geometry& geo, const Decoded& d) {
-  const bool rec = d.st == QB_WIRE_OK && ((d.flags >> 4) & 3u) == QB_IN_APP_RESP && d.group < geo.G;
-  const bool member = (d.flags & QB_REC_NO_PROGRESS) == 0 && (d.flags & 0x0Fu) < geo.n;
-  return RecClass{rec && member, !rec, rec && !member};
-}
 
 // The XCD slot (region shard) of tile t: the blockIdx % 8 of the K3w
 // workgroup that took it (Geometry::tile's mapping inverted), so a deferred
@@ -433,30 +412,6 @@ __global__ __launch_bounds__(kBlock) void k_wire_deferred(Geometry geo, u32 k3gr
   if (threadIdx.x < 4 && lds[threadIdx.x]) atomicAdd(W.wstats + threadIdx.x, u64(lds[threadIdx.x]));
 }
 
-// ----------------------------------------------------------------- slow ----
-// The slow path's records re-decoded from the bytes: message i is a record of
-// a flagged chunk when its envelope group's chunk is flagged, its status is
-// OK and it decodes to a MsgAppResp from a member slot (what the records the
-// ingest would have written hold).  Only those messages are decoded.
-struct WireSrc {
-  WireArgs W;
-  __device__ __forceinline__ bool get(const Geometry& geo, const u8* __restrict__ chunk_slow,
-                                      u64 i, u32& g, u32& f, u64& idx, u64& t) const {
-    g = W.R.mgroup[i];
-    if (!(g < geo.G && chunk_slow[geo.chunk_of(g)] == 1 && W.status[i] == QB_WIRE_OK)) return false;
-    GroupRow row;
-    wire::load_row(W.R, i, row);
-    wire::load_ids(W.R, row);
-    const Decoded d = wire::decode_one<GlobalSrc, true>(W.R, W.nbytes, GlobalSrc{W.bytes},
-                                                         W.R.moff[i], W.R.moff[i + 1], row);
-    if (!classify(geo, d).ok) return false;
-    f = d.flags;
-    idx = d.index;
-    t = d.term;
-    return true;
-  }
-};
-
 template <int N>
 void launch_slow_wire(const Geometry& geo, const ApplyArgs& a, const WireArgs& W, u32* bar,
                       unsigned grid, u64* stats, hipStream_t st) {
@@ -498,6 +453,57 @@ extern "C" size_t qb_wire_fixed_tracker_workspace_bytes(uint32_t n, uint64_t G, 
   return w.cv.nrec_all <= 0xFFFFFFFFull ? w.total : 0;
 }
 
+namespace {
+// The level-1 half shared by the FIXED and CSR entries: argument checks, the
+// carve, the memset, K3w, K3d and K4; W (the bytes' arguments) for the apply
+// half.
+int wire_bucket(const bk::Geometry& geo, const wt::WtCarve& wc, uint64_t M, const uint8_t* bytes,
+                uint64_t nbytes, const uint64_t* msg_off, const uint32_t* msg_group,
+                const uint64_t* rows, const uint32_t* off, const uint64_t* ids,
+                const uint64_t* group_term, const uint32_t* csr_off, uint8_t* status,
+                uint64_t* wire_stats, void* workspace, size_t workspace_bytes, hipStream_t st,
+                const char* ws_fn, wt::WireArgs* W) {
+  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
+  QB_REQUIRE(M == 0 || (msg_off && msg_group && status), "msg_off, msg_group and status are required");
+  QB_REQUIRE(nbytes == 0 || bytes, "bytes is NULL");
+  QB_REQUIRE(rows || (off && ids), "rows, or off and ids, are required");
+  QB_REQUIRE(!rows || (reinterpret_cast<uintptr_t>(rows) & 15u) == 0, "rows must be 16-byte aligned");
+  const bk::Carve& cv = wc.cv;
+  QB_REQUIRE(cv.nrec_all <= 0xFFFFFFFFull,
+             "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
+             (unsigned long long)M, (unsigned long long)cv.nrec_all);
+  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)",
+             (unsigned long long)geo.G);
+  QB_REQUIRE(workspace && workspace_bytes >= wc.total, "workspace too small: need %zu bytes (%s)",
+             wc.total, ws_fn);
+  char* ws = static_cast<char*>(workspace);
+  hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.zero_end - cv.shards, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
+  *W = wt::WireArgs{nbytes, bytes,
+                    wire::RowArgs{geo.G, reinterpret_cast<const u64*>(msg_off), msg_group, off,
+                                  reinterpret_cast<const u64*>(ids),
+                                  reinterpret_cast<const u64*>(rows)},
+                    status, reinterpret_cast<u64*>(ws + wc.ri), reinterpret_cast<u64*>(ws + wc.rt),
+                    reinterpret_cast<u64*>(wire_stats)};
+  if (M == 0) return QB_OK;
+  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
+  u8* chunk_flags = reinterpret_cast<u8*>(ws + cv.chunk_flags);
+  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
+  const bk::Pool pool = bk::pool_at(ws, cv, geo);
+  const bk::Cols buf1 = bk::compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, bk::side_flag_at(ws, cv));
+  const unsigned grid = wt::wt_grid(geo);
+  hipLaunchKernelGGL(wt::k_wire_scatter, dim3(grid), dim3(wt::kWtThreads), 4 * sizeof(u32) * geo.NSB,
+                     st, geo, *W, buf1, counts, shards, chunk_flags, pool, wt::wt_tiles(geo));
+  QB_CHECK_LAUNCH("k_wire_scatter");
+  hipLaunchKernelGGL(wt::k_wire_deferred, dim3(grid_for((M + wt::kScan - 1) / wt::kScan)), dim3(kBlock),
+                     0, st, geo, grid, *W, buf1, counts, shards, chunk_flags, pool);
+  QB_CHECK_LAUNCH("k_wire_deferred");
+  bk::launch_split_compact(geo, cv, ws, reinterpret_cast<const u64*>(group_term), csr_off, st);
+  QB_CHECK_LAUNCH("k_bk_split_compact");
+  return QB_OK;
+}
+}  // namespace
+
 extern "C" int qb_dev_ingest_fixed_tracker_step(
     uint32_t n, uint64_t G, uint64_t M, const uint8_t* bytes, uint64_t nbytes,
     const uint64_t* msg_off, const uint32_t* msg_group, const uint64_t* rows, const uint32_t* off,
@@ -507,60 +513,64 @@ extern "C" int qb_dev_ingest_fixed_tracker_step(
     void* workspace, size_t workspace_bytes, void* stream) {
   if (G == 0) return QB_OK;
   QB_REQUIRE(n >= 1 && n <= QB_MAX_SLOTS, "n must be 1..%d", QB_MAX_SLOTS);
-  QB_REQUIRE(M <= 0xFFFFFFFFull, "batch too large (M=%llu > 2^32-1)", (unsigned long long)M);
   QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
   QB_REQUIRE(group_term && term_start && match && active && committed && stepdown_at && stats,
              "required state pointer is NULL");
-  QB_REQUIRE(M == 0 || (msg_off && msg_group && status), "msg_off, msg_group and status are required");
-  QB_REQUIRE(nbytes == 0 || bytes, "bytes is NULL");
-  QB_REQUIRE(rows || (off && ids), "rows, or off and ids, are required");
-  QB_REQUIRE(!rows || (reinterpret_cast<uintptr_t>(rows) & 15u) == 0, "rows must be 16-byte aligned");
   const bk::Geometry geo = bk::geometry(n, G, M, 0, bk::kSbIl);
   const wt::WtCarve wc = wt::wt_carve(geo);
-  const bk::Carve& cv = wc.cv;
-  QB_REQUIRE(cv.nrec_all <= 0xFFFFFFFFull,
-             "batch too large for the bucket pass (M=%llu: %llu region records > 2^32-1)",
-             (unsigned long long)M, (unsigned long long)cv.nrec_all);
-  QB_REQUIRE(geo.NSB <= 4096, "shard too large for the bucket pass (G=%llu)", (unsigned long long)G);
-  QB_REQUIRE(workspace && workspace_bytes >= wc.total,
-             "workspace too small: need %zu bytes (qb_wire_fixed_tracker_workspace_bytes)", wc.total);
   hipStream_t st = as_stream(stream);
+  wt::WireArgs W;
+  const int rc = wire_bucket(geo, wc, M, bytes, nbytes, msg_off, msg_group, rows, off, ids,
+                             group_term, nullptr, status, wire_stats, workspace, workspace_bytes,
+                             st, "qb_wire_fixed_tracker_workspace_bytes", &W);
+  if (rc != QB_OK) return rc;
   char* ws = static_cast<char*>(workspace);
-  hipError_t e = hipMemsetAsync(ws + cv.shards, 0, cv.zero_end - cv.shards, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(shards, counters)");
-  u64* ri = reinterpret_cast<u64*>(ws + wc.ri);
-  u64* rt = reinterpret_cast<u64*>(ws + wc.rt);
-  const wt::WireArgs W{nbytes, bytes,
-                       wire::RowArgs{G, reinterpret_cast<const u64*>(msg_off), msg_group, off,
-                                     reinterpret_cast<const u64*>(ids),
-                                     reinterpret_cast<const u64*>(rows)},
-                       status, ri, rt, reinterpret_cast<u64*>(wire_stats)};
-  u64* shards = reinterpret_cast<u64*>(ws + cv.shards);
-  u8* chunk_flags = reinterpret_cast<u8*>(ws + cv.chunk_flags);
-  u32* counts = reinterpret_cast<u32*>(ws + cv.counts);
-  const bk::Pool pool = bk::pool_at(ws, cv, geo);
-  if (M) {
-    const bk::Cols buf1 = bk::compact_at(ws + cv.buf1, ws + cv.cl, ws + cv.side1, bk::side_flag_at(ws, cv));
-    const unsigned grid = wt::wt_grid(geo);
-    hipLaunchKernelGGL(wt::k_wire_scatter, dim3(grid), dim3(wt::kWtThreads), 4 * sizeof(u32) * geo.NSB,
-                       st, geo, W, buf1, counts, shards, chunk_flags, pool, wt::wt_tiles(geo));
-    QB_CHECK_LAUNCH("k_wire_scatter");
-    hipLaunchKernelGGL(wt::k_wire_deferred, dim3(grid_for((M + wt::kScan - 1) / wt::kScan)), dim3(kBlock),
-                       0, st, geo, grid, W, buf1, counts, shards, chunk_flags, pool);
-    QB_CHECK_LAUNCH("k_wire_deferred");
-    bk::launch_split_compact(geo, cv, ws, reinterpret_cast<const u64*>(group_term), nullptr, st);
-    QB_CHECK_LAUNCH("k_bk_split_compact");
-  }
   const bk::ApplyArgs a = bk::fixed_apply_args(
-      geo, cv, ws, ri, rt, reinterpret_cast<const u64*>(group_term),
+      geo, wc.cv, ws, W.ri, W.rt, reinterpret_cast<const u64*>(group_term),
       reinterpret_cast<const u64*>(term_start), reinterpret_cast<u64*>(match),
       reinterpret_cast<u64*>(next), active, reinterpret_cast<u64*>(committed), stepdown_at,
       advanced_out);
-  bk::launch_fixed_apply(n, geo, cv, ws, a, st);
+  bk::launch_fixed_apply(n, geo, wc.cv, ws, a, st);
   QB_CHECK_LAUNCH("k_bk_apply");
   wt::dispatch_slow_wire(std::make_integer_sequence<int, QB_MAX_SLOTS>{}, int(n), geo, a, W,
-                         reinterpret_cast<u32*>(ws + cv.flags) + 16, bk::slow_blocks(),
+                         reinterpret_cast<u32*>(ws + wc.cv.flags) + 16, bk::slow_blocks(),
                          reinterpret_cast<u64*>(stats), st);
   QB_CHECK_LAUNCH("k_bk_slow");
+  return QB_OK;
+}
+
+extern "C" size_t qb_wire_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M) {
+  if (max_slots > QB_MAX_SLOTS) return 0;
+  const wt::WtCarve w = wt::wt_carve(bk::csr_geometry(G, max_slots, M));
+  return w.cv.nrec_all <= 0xFFFFFFFFull ? w.total : 0;
+}
+
+extern "C" int qb_dev_ingest_csr_tracker_step(
+    uint64_t G, uint32_t max_slots, const uint32_t* off, const uint32_t* cfg, uint64_t M,
+    const uint8_t* bytes, uint64_t nbytes, const uint64_t* msg_off, const uint32_t* msg_group,
+    const uint64_t* rows, const uint64_t* ids, const uint64_t* group_term,
+    const uint64_t* term_start, uint64_t* match, uint64_t* next, uint16_t* active,
+    uint64_t* committed, uint32_t* stepdown_at, uint8_t* advanced_out, uint8_t* status,
+    uint64_t* wire_stats, uint64_t* stats, void* workspace, size_t workspace_bytes, void* stream) {
+  QB_REQUIRE(max_slots <= QB_MAX_SLOTS, "max_slots must be 0..%d", QB_MAX_SLOTS);
+  QB_REQUIRE(G <= 0xFFFFFFFFull, "shard too large (G=%llu > 2^32-1)", (unsigned long long)G);
+  if (G == 0) return QB_OK;
+  QB_REQUIRE(off && cfg && ids && group_term && term_start && match && active && committed &&
+                 stepdown_at && stats,
+             "required state pointer is NULL");
+  const bk::Geometry geo = bk::csr_geometry(G, max_slots, M);
+  const wt::WtCarve wc = wt::wt_carve(geo);
+  hipStream_t st = as_stream(stream);
+  wt::WireArgs W;
+  const int rc = wire_bucket(geo, wc, M, bytes, nbytes, msg_off, msg_group, rows, off, ids,
+                             group_term, off, status, wire_stats, workspace, workspace_bytes, st,
+                             "qb_wire_csr_tracker_workspace_bytes", &W);
+  if (rc != QB_OK) return rc;
+  wt::csr_apply_wire(bk::csr_wmax(max_slots), geo, wc.cv, static_cast<char*>(workspace), off, cfg,
+                     reinterpret_cast<const u64*>(group_term), reinterpret_cast<const u64*>(term_start),
+                     reinterpret_cast<u64*>(match), reinterpret_cast<u64*>(next), active,
+                     reinterpret_cast<u64*>(committed), stepdown_at, advanced_out, W,
+                     reinterpret_cast<u64*>(stats), st);
+  QB_CHECK_LAUNCH("k_csr_apply / k_bk_slow");
   return QB_OK;
 }

@@ -80,19 +80,24 @@ def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.
                         off: torch.Tensor = None, ids: torch.Tensor = None,
                         advanced_out: torch.Tensor = None, wire_stats: torch.Tensor = None,
                         reset_stats: bool = True, rearm: bool = True) -> torch.Tensor:
-    """The composed tick in one call (qb_dev_ingest_fixed_tracker_step): M
-    encoded responses decoded and stepped into ``tracker`` (a
-    ``batch.FixedTracker``), the commit advanced — ``ingest`` followed by
+    """The composed tick in one call: M encoded responses decoded and stepped
+    into ``tracker``, the commit advanced — ``ingest`` followed by
     ``tracker.step`` on its records, without the record columns between them
-    (a message that is not a MsgAppResp steps nothing).  ``rows``
-    (``group_rows``) or ``off`` + ``ids`` give the groups' slot IDs.
-    ``reset_stats`` / ``rearm`` as ``FixedTracker.step``; ``wire_stats`` (int64
-    [4], nullable) accumulates the QB_WIRE_* counts.  Returns the per-message
-    status (u8 [M])."""
+    (a message that is not a MsgAppResp steps nothing).  A
+    ``batch.FixedTracker`` (qb_dev_ingest_fixed_tracker_step: ``rows``
+    (``group_rows``) or ``off`` + ``ids`` give the groups' slot IDs) or a
+    ``batch.CsrTracker`` (qb_dev_ingest_csr_tracker_step: ``ids`` over the
+    tracker's own ``off``, ``rows`` optional).  ``reset_stats`` / ``rearm``
+    as the trackers' ``step``; ``wire_stats`` (int64 [4], nullable)
+    accumulates the QB_WIRE_* counts.  Returns the per-message status (u8 [M])."""
+    from .batch import CsrTracker
     for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
         if not t.is_cuda:
             raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
-    if rows is None and (off is None or ids is None):
+    csr = isinstance(tracker, CsrTracker)
+    if csr and ids is None:
+        raise _lib.QuorumBatchError("ids (the groups' slot IDs over the tracker's off) are required")
+    if not csr and rows is None and (off is None or ids is None):
         raise _lib.QuorumBatchError("rows, or off and ids, are required")
     dev = buf.device
     M = msg_group.numel()
@@ -100,7 +105,9 @@ def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.
         tracker.stats.zero_()
     if rearm:
         tracker.stepdown_at.fill_(-1)
-    need = _lib.load().qb_wire_fixed_tracker_workspace_bytes(tracker.n, tracker.G, M)
+    lib = _lib.load()
+    need = (lib.qb_wire_csr_tracker_workspace_bytes(tracker.G, tracker.max_slots, M) if csr
+            else lib.qb_wire_fixed_tracker_workspace_bytes(tracker.n, tracker.G, M))
     if need == 0:
         raise _lib.QuorumBatchError(f"batch of {M} messages too large for one call")
     ws = getattr(tracker, "_wire_ws", None)
@@ -108,12 +115,17 @@ def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.
         ws = tracker._wire_ws = torch.empty(need, dtype=torch.uint8, device=dev)
     status = torch.empty(max(M, 1), dtype=torch.uint8, device=dev)
     p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-    _lib.call("qb_dev_ingest_fixed_tracker_step", tracker.n, tracker.G, M, buf.data_ptr(), nbytes,
-              msg_off.data_ptr(), msg_group.data_ptr(), p(rows), p(off), p(ids), p(tracker.term),
-              p(tracker.term_start), p(tracker.match), p(tracker.next), p(tracker.active),
-              p(tracker.committed), p(tracker.stepdown_at), p(advanced_out), status.data_ptr(),
-              p(wire_stats), p(tracker.stats), ws.data_ptr(), ws.numel(),
-              torch.cuda.current_stream(dev).cuda_stream)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    state = (p(tracker.term), p(tracker.term_start), p(tracker.match), p(tracker.next),
+             p(tracker.active), p(tracker.committed), p(tracker.stepdown_at), p(advanced_out),
+             status.data_ptr(), p(wire_stats), p(tracker.stats), ws.data_ptr(), ws.numel(), stream)
+    if csr:
+        _lib.call("qb_dev_ingest_csr_tracker_step", tracker.G, tracker.max_slots, p(tracker.off),
+                  p(tracker.cfg), M, buf.data_ptr(), nbytes, msg_off.data_ptr(),
+                  msg_group.data_ptr(), p(rows), p(ids), *state)
+    else:
+        _lib.call("qb_dev_ingest_fixed_tracker_step", tracker.n, tracker.G, M, buf.data_ptr(),
+                  nbytes, msg_off.data_ptr(), msg_group.data_ptr(), p(rows), p(off), p(ids), *state)
     return status[:M]
 
 

@@ -707,6 +707,22 @@ int qb_dev_ingest_fixed_tracker_step(uint32_t n, uint64_t G, uint64_t M, const u
                                      uint8_t* advanced_out, uint8_t* status,
                                      uint64_t* wire_stats, uint64_t* stats, void* workspace,
                                      size_t workspace_bytes, void* stream);
+/* The same one-call tick for the CSR tracker (ragged / learner / joint
+ * configs, qb_dev_csr_tracker_step's layout and arguments): off [G+1] are
+ * both the tracker's slot offsets and the groups' slot-ID ranges (ids
+ * ascending per group, required; rows, the 64-byte row table of (off, ids),
+ * nullable).  Workspace: qb_wire_csr_tracker_workspace_bytes(G, max_slots, M). */
+size_t qb_wire_csr_tracker_workspace_bytes(uint64_t G, uint32_t max_slots, uint64_t M);
+int qb_dev_ingest_csr_tracker_step(uint64_t G, uint32_t max_slots, const uint32_t* off,
+                                   const uint32_t* cfg, uint64_t M, const uint8_t* bytes,
+                                   uint64_t nbytes, const uint64_t* msg_off,
+                                   const uint32_t* msg_group, const uint64_t* rows,
+                                   const uint64_t* ids, const uint64_t* group_term,
+                                   const uint64_t* term_start, uint64_t* match, uint64_t* next,
+                                   uint16_t* active, uint64_t* committed, uint32_t* stepdown_at,
+                                   uint8_t* advanced_out, uint8_t* status, uint64_t* wire_stats,
+                                   uint64_t* stats, void* workspace, size_t workspace_bytes,
+                                   void* stream);
 
 /* ----------------------------------------------------------------------- */
 /* Configuration changes                             */

@@ -224,3 +224,73 @@ def test_fused_off_ids_and_empty():
     eg = torch.zeros(0, dtype=torch.int32, device=dev)
     wire.ingest_tracker_step(tr, empty, 0, mo, eg, off=d_off, ids=d_ids)
     assert np.array_equal(_u64(tr.committed), st["committed"])
+
+
+@pytest.mark.parametrize("kind,term_base", [("ragged", 0), ("joint", 20000), ("ragged", 1 << 33)])
+def test_fused_csr_vs_chain_of_c_oracles(kind, term_base):
+    """qb_dev_ingest_csr_tracker_step: ragged voters + learners and joint
+    configs (oracle/quorum_oracle.c gen_csr), the groups' slot IDs over the
+    tracker's own off, stale / higher-term / rejected responses, non-members,
+    envelope groups past the shard, heartbeat responses and non-canonical
+    encodings, group terms small, past the record's field and past 2^32 —
+    three ticks against the C chain (restated Unmarshal, then the sequential
+    CSR tracker oracle), state and every stat."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    from tests.test_gpu_tracker_csr import _batch, _state, _tracker
+    G, M = 3000, 12000
+    rng = np.random.default_rng(G + term_base % 997)
+    r = random.Random(term_base % 991)
+    off, cfg, sizes, st = _state(rng, kind, G, term_base)
+    tr = _tracker(off, cfg, st, track_next=False)
+    st.pop("next")
+    ids = (100 + 3 * np.arange(int(off[-1]), dtype=np.uint64)).astype(np.uint64)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to("cuda")
+    wst = torch.zeros(4, dtype=torch.int64, device="cuda")
+    want_w = np.zeros(4, np.int64)
+    for tick in range(3):
+        group, slot, index, term, rej, flags = _batch(rng, G, M, sizes, st, stale=0.05,
+                                                      higher=0.003, reject=0.1, nonmember=0.02,
+                                                      bad=0.01)
+        msgs, grps = [], []
+        for i in range(M):
+            g = int(group[i])
+            gi = g if g < G else 0
+            s0, n_g = int(off[gi]), int(sizes[gi])
+            frm = int(ids[s0 + int(slot[i])]) if int(slot[i]) < n_g else 999_999_999 + i
+            to = int(ids[s0]) if n_g else 1
+            y = r.random()
+            if y < 0.04:
+                b = W.marshal_message(9, to, frm, int(term[i]), 0, 0, (), 0, W.EMPTY_SNAPSHOT,
+                                      False, 0, None)
+            elif y < 0.08:
+                b = W._key(6, 0) + W.varint(int(index[i])) + W.marshal_message(
+                    4, to, frm, int(term[i]), 0, int(index[i]), (), 0, W.EMPTY_SNAPSHOT,
+                    bool(rej[i]), 0)
+            else:
+                b = W.marshal_message(4, to, frm, int(term[i]), 0, int(index[i]), (), 0,
+                                      W.EMPTY_SNAPSHOT, bool(rej[i]), 0)
+            msgs.append(b)
+            grps.append(g)
+        buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device="cuda")
+        status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, ids=d_ids, wire_stats=wst)
+        want = oc.ingest(buf.cpu().numpy()[:nbytes], _u64(moff), grp.cpu().numpy().view(np.uint32),
+                         off, ids, threads=8)
+        assert np.array_equal(status.cpu().numpy(), want["status"])
+        want_w += np.bincount(want["status"], minlength=4)[:4]
+        g2 = want["group"].copy()
+        f2 = want["flags"].copy()
+        notrec = (want["status"] != 0) | (((f2 >> 4) & 3) != 0)
+        g2[notrec] = 0xFFFFFFFF
+        nonm = ~notrec & ((f2 & 0x40) != 0)
+        f2[nonm] = (f2[nonm] & 0xF0) | 0x0F
+        stats = oc.csr_appresp_sequential(off, cfg, (g2, f2, want["index"], want["term"]), st)
+        S = st["match"].size
+        assert np.array_equal(batch.as_u64(tr.match)[:S], st["match"]), tick
+        assert np.array_equal(tr.active.cpu().numpy().view(np.uint16)[:G], st["active"]), tick
+        assert np.array_equal(batch.as_u64(tr.committed), st["committed"]), tick
+        assert np.array_equal(tr.stepped_down().cpu().numpy(), st["stepped_down"].astype(bool))
+        assert tr.stats.cpu().numpy()[:7].tolist() == [int(x) for x in stats[:7]], tick
+        tr.stepdown_at.fill_(-1)
+        st["stepped_down"][:] = 0
+    assert np.array_equal(wst.cpu().numpy(), want_w)

@@ -293,8 +293,54 @@ def wire_tracker_tick(G, nb, E=64, seed=77, dev_=None):
     return tr, snap, ticks, rows, off, ids
 
 
+def wire_tracker_csr_tick(G, nb, E=64, seed=79, dev_=None):
+    """The composed workload over the CSR tracker (configs[2]'s ragged groups:
+    3-9 voters + 0-2 learners, BASELINE configs[4]'s streaming step): G groups,
+    nb ticks of G device-encoded MsgAppResp from a random non-leader slot of a
+    random group, leader term 20007 (1 % stale 20006), indexes past 2^35 (6-byte
+    varints); slot IDs ascending per group (3-byte varints).  Returns (tracker,
+    snapshot, ticks, rows, off, ids) as wire_tracker_tick."""
+    import bench
+    from etcd_amd.quorum import wire
+    d = dev_ or dev
+    B = 1 << 35
+    grp = batch.CsrGroups.synth(bench.CSR_SEED["ragged"], "ragged", G, device=d)
+    tr = batch.CsrTracker(grp.off, grp.cfg, max_slots=grp.max_slots, device=d)
+    tr.match.copy_(grp.match[: tr.S] + B)
+    del grp
+    gen = torch.Generator(device=d)
+    gen.manual_seed(seed)
+    sizes = (tr.off[1:] - tr.off[:-1]).long()
+    first = tr.off[:-1].long()
+    last = tr.match[first].clone()  # slot 0: the leader's own match
+    tr.term.fill_(20007)
+    tr.term_start.copy_(last - 64)
+    tr.commit_advance()
+    gidx = torch.repeat_interleave(torch.arange(G, device=d), sizes)
+    sl = torch.arange(tr.S, device=d) - first[gidx]
+    ids = 16384 + sl * 100000 + (gidx % 100000)  # ascending per group
+    rows = wire.group_rows(tr.off, ids)
+    ticks = []
+    for k in range(nb):
+        group = torch.randint(0, G, (G,), generator=gen, device=d, dtype=torch.int64)
+        r_ = torch.randint(0, 1 << 30, (G,), generator=gen, device=d, dtype=torch.int64)
+        slot = 1 + r_ % (sizes[group] - 1)
+        lag = torch.randint(0, 96, (G,), generator=gen, device=d, dtype=torch.int64)
+        index = last[group] + (k + 1) * E - lag
+        term = torch.where(torch.rand(G, generator=gen, device=d) < 0.01, 20006, 20007)
+        rej = torch.zeros(G, dtype=torch.bool, device=d)
+        buf, nbytes, moff = wire.encode_appresp(ids[first[group]], ids[first[group] + slot], term,
+                                                index, rej)
+        direct = batch.AppRespBatch(group.to(torch.int32), slot.to(torch.uint8), index,
+                                    term.to(torch.int64))
+        ticks.append((buf, nbytes, moff, group.to(torch.int32), direct))
+    tr.match[first] = last + nb * E  # the leader appended nb * E entries
+    snap = {k_: getattr(tr, k_).clone() for k_ in ("match", "committed", "active", "stepdown_at")}
+    return tr, snap, ticks, rows, tr.off, ids
+
+
 def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=None,
-                        fused_only=False):
+                        fused_only=False, csr=False):
     """Composed row: wire bytes -> tracker tick, per tick (rafthttp/stream.go:466
     decode -> raft.go:1106-1259 stepLeader MsgAppResp -> maybeCommit), G
     groups and G messages per tick, in one call (round 6:
@@ -310,7 +356,7 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
     reporter = reporter or report
     from etcd_amd.quorum import wire
     nb = warm + reps
-    tr, snap, ticks, rows, off, ids = wire_tracker_tick(G, nb)
+    tr, snap, ticks, rows, off, ids = (wire_tracker_csr_tick if csr else wire_tracker_tick)(G, nb)
     sp = torch.cuda.current_stream(dev).cuda_stream
 
     def restore():
@@ -322,7 +368,7 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
         tr.step(batch.AppRespBatch(ib.group, ib.flags, ib.index, ib.term))
 
     def fused(tk):
-        wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows)
+        wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows, ids=ids)
 
     def timed(fn):
         ev = HipEvents(2)
@@ -352,7 +398,7 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
     bad = 0
     restore()
     for tk in ticks:
-        status = wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows)
+        status = wire.ingest_tracker_step(tr, tk[0], tk[1], tk[2], tk[3], rows=rows, ids=ids)
         bad += int((status != 0).sum())
     via_fused = {k_: getattr(tr, k_).clone() for k_ in snap}
     restore()
@@ -376,8 +422,13 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
     # 4, the group's slot IDs 40 (wire row), its status byte 1; the tracker's
     # match RMW 16 and the commit advance 64 per group (configs[4] row) — the
     # decoded records are intermediate, not algorithmic
-    algo = nbytes + G * (8 + 4 + 40 + 1) + G * (16 + 64)
-    reporter("wire -> tracker tick (composed)", G, t, algo,
+    if csr:  # the CSR step's row (configs[4] CSR: 117 B per group-step; slot IDs 8 B each)
+        sl = float((off[-1].item()) / G)
+        algo = nbytes + G * (8 + 4 + 8 * sl + 1) + G * (117 - 21)
+    else:
+        algo = nbytes + G * (8 + 4 + 40 + 1) + G * (16 + 64)
+    reporter("wire -> tracker-csr tick (composed)" if csr else "wire -> tracker tick (composed)",
+             G, t, algo,
              {"unit": "group-steps/s", "form": "one call (qb_dev_ingest_fixed_tracker_step)",
               "chain_us": t_chain * 1e6, "chain_ingest_us": t_ingest * 1e6,
               "chain_tracker_step_us": t_step * 1e6,
@@ -842,6 +893,8 @@ def main():
         wire_tracker_config(1 << 24, a.reps)
     if "wire-tracker-fused" in which:  # development A/B: the one call alone
         wire_tracker_config(1 << 24, a.reps, fused_only=True)
+    if "wire-tracker-csr" in which:  # the composed tick over configs[2]'s ragged CSR groups
+        wire_tracker_config(1 << 24, a.reps, csr=True)
 
 
 if __name__ == "__main__":
