@@ -1363,14 +1363,16 @@ def next_rows():
     step (4M groups), ReadIndex acks (4M leaders; local answers as
     ReadStates, the all-message form beside it), wire ingest (16M messages,
     group-row table), a conf change over 8M groups, the composed wire ->
-    tracker tick (16M groups, 16M encoded MsgAppResp per tick; its own
-    decode + state parity in the row), and the configs[0]
+    tracker tick in one call, FIXED and CSR (16M groups, 16M encoded
+    MsgAppResp per tick; the chain's time beside it; decode + state parity in
+    the row), and the configs[0]
     plumbing (the faithful C restatement's ns/op beside the device's ns per
     group).  Each row carries its own parity (round 5): the leader and
     ReadIndex workloads at 256K groups through every output form vs the C
     oracle, the wire decode of all 16M messages vs the C decoder, the conf
-    change's whole result checked on the device, the composed row's decode
-    and state; the GPU suite covers the rest (tests/test_gpu_leader.py,
+    change's whole result checked on the device, the composed rows' decode
+    and state (the one call against the chain and the direct step, FIXED and
+    CSR trackers); the GPU suite covers the rest (tests/test_gpu_leader.py,
     test_gpu_wire.py, test_gpu_confchange.py)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     import bench_configs as bc
@@ -1387,7 +1389,9 @@ def next_rows():
                      ("readindex", lambda: bc.readindex_config(1 << 22, 20, **kw)),
                      ("wire", lambda: bc.wire_config(1 << 24, 20, rows=True, **kw)),
                      ("confchange", lambda: bc.confchange_config(1 << 23, 20, **kw)),
-                     ("wire-tracker", lambda: bc.wire_tracker_config(1 << 24, 10, **kw))):
+                     ("wire-tracker", lambda: bc.wire_tracker_config(1 << 24, 10, **kw)),
+                     ("wire-tracker-csr", lambda: bc.wire_tracker_config(1 << 24, 10, csr=True,
+                                                                         **kw))):
         try:
             fn()
         except Exception as ex:  # reported; the headline stands

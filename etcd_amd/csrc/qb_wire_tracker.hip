@@ -192,11 +192,13 @@ __global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
     if (r + 1 < kPer) {
       wire::load_row_of(W.R, qg[r + 1], nrow);
       // sub-round r's LDS-DMA is done once at most the loads just issued (the
-      // next group row: 4 loads, or 2 without the row table) are outstanding
-      // (vmcnt counts in issue order; the DMA was issued before them, pinned
-      // by the compiler barriers in stage_span)
+      // next group row: 4 x 16 B with the row table — never fewer
+      // instructions; the slot range without it: 2 u32 loads the compiler
+      // may merge into one, so 1) are outstanding (vmcnt counts in issue
+      // order; the DMA was issued before them, pinned by the compiler
+      // barriers in stage_span)
       if (W.R.rows) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
       stage_span(slices[(r + 1) & 1], W, nrec, r + 1, w, lane, q0[r + 1], q1[r + 1], sb[(r + 1) & 1],
                  se[(r + 1) & 1]);
     } else {

@@ -94,6 +94,18 @@ def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.
     for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
         if not t.is_cuda:
             raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
+    G = tracker.G
+    for t, what, dts, n_min in ((rows, "rows", (torch.int64,), 8 * G),
+                                (off, "off", (torch.int32,), G + 1),
+                                (ids, "ids", (torch.int64,), 0),
+                                (advanced_out, "advanced_out", (torch.uint8, torch.bool), G),
+                                (wire_stats, "wire_stats", (torch.int64,), 4),
+                                (msg_off, "msg_off", (torch.int64,), msg_group.numel() + 1),
+                                (msg_group, "msg_group", (torch.int32,), 0)):
+        if t is not None and (not t.is_cuda or t.dtype not in dts or not t.is_contiguous()
+                              or t.numel() < n_min):
+            raise _lib.QuorumBatchError(f"{what} must be a contiguous {dts[0]} device tensor of "
+                                        f">= {n_min} elements")
     csr = isinstance(tracker, CsrTracker)
     if csr and ids is None:
         raise _lib.QuorumBatchError("ids (the groups' slot IDs over the tracker's off) are required")

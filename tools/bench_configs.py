@@ -306,17 +306,20 @@ def wire_tracker_csr_tick(G, nb, E=64, seed=79, dev_=None):
     B = 1 << 35
     grp = batch.CsrGroups.synth(bench.CSR_SEED["ragged"], "ragged", G, device=d)
     tr = batch.CsrTracker(grp.off, grp.cfg, max_slots=grp.max_slots, device=d)
-    tr.match.copy_(grp.match[: tr.S] + B)
     del grp
     gen = torch.Generator(device=d)
     gen.manual_seed(seed)
     sizes = (tr.off[1:] - tr.off[:-1]).long()
     first = tr.off[:-1].long()
-    last = tr.match[first].clone()  # slot 0: the leader's own match
+    gidx = torch.repeat_interleave(torch.arange(G, device=d), sizes)
+    # the leader (slot 0) at last, followers up to 200 behind (6-byte varints)
+    last = B + 1024 + torch.randint(0, 1 << 20, (G,), generator=gen, device=d, dtype=torch.int64)
+    tr.match.copy_(last[gidx] - torch.randint(0, 200, (tr.S,), generator=gen, device=d,
+                                              dtype=torch.int64))
+    tr.match[first] = last
     tr.term.fill_(20007)
     tr.term_start.copy_(last - 64)
     tr.commit_advance()
-    gidx = torch.repeat_interleave(torch.arange(G, device=d), sizes)
     sl = torch.arange(tr.S, device=d) - first[gidx]
     ids = 16384 + sl * 100000 + (gidx % 100000)  # ascending per group
     rows = wire.group_rows(tr.off, ids)
