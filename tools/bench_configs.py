@@ -432,7 +432,8 @@ def wire_tracker_config(G, reps, warm=4, regions=3, *, reporter=None, gpu_only=N
         algo = nbytes + G * (8 + 4 + 40 + 1) + G * (16 + 64)
     reporter("wire -> tracker-csr tick (composed)" if csr else "wire -> tracker tick (composed)",
              G, t, algo,
-             {"unit": "group-steps/s", "form": "one call (qb_dev_ingest_fixed_tracker_step)",
+             {"unit": "group-steps/s",
+              "form": "one call (qb_dev_ingest_%s_tracker_step)" % ("csr" if csr else "fixed"),
               "chain_us": t_chain * 1e6, "chain_ingest_us": t_ingest * 1e6,
               "chain_tracker_step_us": t_step * 1e6,
               "bytes_per_message": nbytes / G,
