@@ -223,6 +223,47 @@ def test_tracker_region_grid_u32_guard():
     assert b"region records" in lib.qb_last_error()
 
 
+def test_composed_tick_validates_before_the_device():
+    """qb_dev_ingest_{fixed,csr}_tracker_step refuse malformed arguments with
+    QB_EINVAL and the reason before any HIP call (no GPU needed): slot counts
+    out of range, a misaligned row table, no slot IDs at all, a batch past
+    the u32 region grid, a short workspace; their workspace sizes are the
+    tracker step's plus the two escape columns, 0 where no workspace fits."""
+    lib = _lib.load()
+    M = 1 << 24
+    assert (lib.qb_wire_fixed_tracker_workspace_bytes(5, M, M)
+            >= lib.qb_fixed_tracker_workspace_bytes(5, M, M) + 16 * M)
+    assert lib.qb_wire_fixed_tracker_workspace_bytes(0, 16, 16) == 0
+    assert lib.qb_wire_fixed_tracker_workspace_bytes(17, 16, 16) == 0
+    assert lib.qb_wire_fixed_tracker_workspace_bytes(5, 1 << 30, 1 << 31) == 0
+    assert (lib.qb_wire_csr_tracker_workspace_bytes(M, 8, M)
+            >= lib.qb_csr_tracker_workspace_bytes(M, 8, M) + 16 * M)
+    assert lib.qb_wire_csr_tracker_workspace_bytes(16, 17, 16) == 0
+    d = C.c_void_p(0x1000)  # never dereferenced: each check fails first
+
+    def fixed(n, G, M_, rows=d, off=None, ids=None, ws_bytes=1 << 40):
+        return lib.qb_dev_ingest_fixed_tracker_step(
+            n, G, M_, d, 100, d, d, rows, off, ids, d, d, d, None, d, d, d, None, d, None, d, d,
+            C.c_size_t(ws_bytes), None)
+    cases = [(lambda: fixed(0, 16, 16), b"n must be"),
+             (lambda: fixed(5, 16, 16, rows=C.c_void_p(0x1008)), b"16-byte aligned"),
+             (lambda: fixed(5, 16, 16, rows=None), b"rows, or off and ids"),
+             (lambda: fixed(5, 1 << 30, 1 << 31), b"region records"),
+             (lambda: fixed(5, 16, 16, ws_bytes=8), b"workspace too small")]
+    for call, why in cases:
+        rc = call()
+        assert rc == _lib.QB_EINVAL, why
+        assert why in lib.qb_last_error(), (why, lib.qb_last_error())
+    rc = lib.qb_dev_ingest_csr_tracker_step(16, 8, d, d, 16, d, 100, d, d, None, None, d, d, d,
+                                            None, d, d, d, None, d, None, d, d, C.c_size_t(1 << 40),
+                                            None)
+    assert rc == _lib.QB_EINVAL and b"required" in lib.qb_last_error()
+    rc = lib.qb_dev_ingest_csr_tracker_step(16, 17, d, d, 16, d, 100, d, d, None, d, d, d, d,
+                                            None, d, d, d, None, d, None, d, d, C.c_size_t(1 << 40),
+                                            None)
+    assert rc == _lib.QB_EINVAL and b"max_slots" in lib.qb_last_error()
+
+
 def test_leader_outbox_binding_layout_matches_header(tmp_path):
     """The Python binding's qb_leader_outbox / qb_read_state match the
     header's layout (gcc on the header itself): the ReadState area's two
