@@ -36,6 +36,36 @@ def group_rows(off: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return rows
 
 
+def _check_tensors(specs):
+    """(tensor, name, dtypes, min elements) each: a contiguous device tensor of
+    one of dtypes and at least that many elements (None: optional, skipped);
+    all on one device.  The C ABI takes plain pointers, so a short or
+    mistyped tensor here would be read past its end on the device."""
+    dev = None
+    for t, what, dts, n_min in specs:
+        if t is None:
+            continue
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
+        if t.dtype not in dts or not t.is_contiguous() or t.numel() < n_min:
+            raise _lib.QuorumBatchError(f"{what} must be a contiguous {dts[0]} device tensor of "
+                                        f">= {n_min} elements")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise _lib.QuorumBatchError(f"{what} is on {t.device}, the batch on {dev}")
+
+
+def _check_batch(buf, nbytes, msg_off, msg_group):
+    """The message batch: nbytes >= 0 bytes of buf, M + 1 offsets, M groups."""
+    if not isinstance(nbytes, int) or nbytes < 0:
+        raise _lib.QuorumBatchError(f"nbytes must be a non-negative int, got {nbytes!r}")
+    M = msg_group.numel() if isinstance(msg_group, torch.Tensor) else 0
+    _check_tensors(((buf, "buf", (torch.uint8,), nbytes),
+                    (msg_off, "msg_off", (torch.int64,), M + 1),
+                    (msg_group, "msg_group", (torch.int32,), 0)))
+
+
 def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: torch.Tensor,
            off: torch.Tensor, ids: torch.Tensor, stats: torch.Tensor = None,
            rows: torch.Tensor = None):
@@ -44,12 +74,14 @@ def ingest(buf: torch.Tensor, nbytes: int, msg_off: torch.Tensor, msg_group: tor
     ``rows`` (``group_rows(off, ids)``) each message gathers one 64-byte row
     instead (qb_dev_ingest_messages_rows).
     Returns (LeaderInbox, status u8 tensor, msg_type u8 tensor)."""
-    for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
-        if not t.is_cuda:
-            raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
+    _check_batch(buf, nbytes, msg_off, msg_group)
+    _check_tensors(((off, "off", (torch.int32,), 1), (ids, "ids", (torch.int64,), 0),
+                    (stats, "stats", (torch.int64,), 4)))
     dev = buf.device
     M = msg_group.numel()
     G = off.numel() - 1
+    _check_tensors(((rows, "rows", (torch.int64,), 8 * G), (buf, "buf", (torch.uint8,), 0),
+                    (off, "off", (torch.int32,), 0)))
     n = max(M, 1)
     rg = torch.empty(n, dtype=torch.int32, device=dev)
     rf = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -91,21 +123,14 @@ def ingest_tracker_step(tracker, buf: torch.Tensor, nbytes: int, msg_off: torch.
     as the trackers' ``step``; ``wire_stats`` (int64 [4], nullable)
     accumulates the QB_WIRE_* counts.  Returns the per-message status (u8 [M])."""
     from .batch import CsrTracker
-    for t, what in ((buf, "buf"), (msg_off, "msg_off"), (msg_group, "msg_group")):
-        if not t.is_cuda:
-            raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
+    _check_batch(buf, nbytes, msg_off, msg_group)
     G = tracker.G
-    for t, what, dts, n_min in ((rows, "rows", (torch.int64,), 8 * G),
-                                (off, "off", (torch.int32,), G + 1),
-                                (ids, "ids", (torch.int64,), 0),
-                                (advanced_out, "advanced_out", (torch.uint8, torch.bool), G),
-                                (wire_stats, "wire_stats", (torch.int64,), 4),
-                                (msg_off, "msg_off", (torch.int64,), msg_group.numel() + 1),
-                                (msg_group, "msg_group", (torch.int32,), 0)):
-        if t is not None and (not t.is_cuda or t.dtype not in dts or not t.is_contiguous()
-                              or t.numel() < n_min):
-            raise _lib.QuorumBatchError(f"{what} must be a contiguous {dts[0]} device tensor of "
-                                        f">= {n_min} elements")
+    _check_tensors(((buf, "buf", (torch.uint8,), 0), (tracker.committed, "tracker", (torch.int64,), G),
+                    (rows, "rows", (torch.int64,), 8 * G),
+                    (off, "off", (torch.int32,), G + 1),
+                    (ids, "ids", (torch.int64,), 0),
+                    (advanced_out, "advanced_out", (torch.uint8, torch.bool), G),
+                    (wire_stats, "wire_stats", (torch.int64,), 4)))
     csr = isinstance(tracker, CsrTracker)
     if csr and ids is None:
         raise _lib.QuorumBatchError("ids (the groups' slot IDs over the tracker's off) are required")

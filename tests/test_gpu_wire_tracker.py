@@ -294,3 +294,73 @@ def test_fused_csr_vs_chain_of_c_oracles(kind, term_base):
         tr.stepdown_at.fill_(-1)
         st["stepped_down"][:] = 0
     assert np.array_equal(wst.cpu().numpy(), want_w)
+
+
+def test_fused_unaligned_buffer_and_input_checks():
+    """The message bytes at an address that is not 16-byte aligned (a view
+    into a larger buffer: the decoder stages its byte slices with plain loads
+    instead of LDS-DMA) give the same status and state as the aligned copy;
+    short or mistyped inputs raise before any device call."""
+    import torch
+    from etcd_amd import _lib
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(11)
+    G, n = 1 << 11, 5
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (7 + np.arange(n * G, dtype=np.uint64) * 5)
+    dev = torch.device("cuda")
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    rows = wire.group_rows(d_off, d_ids)
+    msgs, grps = [], []
+    for _ in range(5 * G + 37):  # a partial last tile
+        g = r.randrange(G)
+        s = r.randrange(n)
+        msgs.append(W.marshal_message(4, int(ids[n * g]), int(ids[n * g + s]), 9, 0,
+                                      100 + r.randrange(1000), (), 0, W.EMPTY_SNAPSHOT,
+                                      r.random() < 0.1, 0))
+        grps.append(g)
+    buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+    outs = []
+    for shift in (0, 3, 8):
+        tr = batch.FixedTracker(n, G, dev)
+        tr.term.fill_(9)
+        tr.term_start.fill_(50)
+        b = buf
+        if shift:
+            host = torch.zeros(nbytes + 32, dtype=torch.uint8, device=dev)
+            b = host[shift:shift + nbytes]
+            b.copy_(buf[:nbytes])
+            assert b.data_ptr() % 16 != 0
+        wst = torch.zeros(4, dtype=torch.int64, device=dev)
+        status = wire.ingest_tracker_step(tr, b, nbytes, moff, grp, rows=rows, wire_stats=wst)
+        outs.append((status.cpu(), batch.as_u64(tr.match).copy(), batch.as_u64(tr.committed).copy(),
+                     tr.stats.cpu().clone(), wst.cpu()))
+        if shift == 0:
+            st = _host_state(tr, G)
+            st["match"][:] = 0
+            st["committed"][:] = 0
+            st["active"][:] = 0
+            want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], _u64(moff),
+                                                    grp.cpu().numpy().view(np.uint32), off, ids, st)
+            assert np.array_equal(status.cpu().numpy(), want_status)
+            _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0])
+        assert np.array_equal(o[1], outs[0][1]) and np.array_equal(o[2], outs[0][2])
+        assert torch.equal(o[3], outs[0][3]) and torch.equal(o[4], outs[0][4])
+    tr = batch.FixedTracker(n, G, dev)
+    bad = [lambda: wire.ingest_tracker_step(tr, buf[: nbytes - 1], nbytes, moff, grp, rows=rows),
+           lambda: wire.ingest_tracker_step(tr, buf.view(torch.int8), nbytes, moff, grp, rows=rows),
+           lambda: wire.ingest_tracker_step(tr, buf, nbytes, moff[:-1], grp, rows=rows),
+           lambda: wire.ingest_tracker_step(tr, buf, nbytes, moff, grp.to(torch.int64), rows=rows),
+           lambda: wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows[:-8]),
+           lambda: wire.ingest_tracker_step(tr, buf, -1, moff, grp, rows=rows),
+           lambda: wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows,
+                                            wire_stats=torch.zeros(3, dtype=torch.int64, device=dev)),
+           lambda: wire.ingest(buf[:10], nbytes, moff, grp, d_off, d_ids),
+           lambda: wire.ingest(buf, nbytes, moff, grp, d_off.to(torch.int64), d_ids),
+           lambda: wire.ingest(buf, nbytes, moff, grp, d_off, d_ids, rows=rows[:8])]
+    for i, call in enumerate(bad):
+        with pytest.raises(_lib.QuorumBatchError):
+            call()
