@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from .. import _lib
+from ._checks import FLAG, I16, I32, I64, U8, check_tensors
 
 INDEX_INF = (1 << 64) - 1
 
@@ -48,9 +49,8 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def _require_device(t: torch.Tensor, what: str):
-    if not t.is_cuda:
-        raise _lib.QuorumBatchError(f"{what} must be a device (HIP) tensor; there is no CPU path")
+def _check_outs(G: int, commit_out, vote_out) -> None:
+    check_tensors(((commit_out, "commit_out", I64, G), (vote_out, "vote_out", U8, G)))
 
 
 def mask_dtype(n: int):
@@ -76,8 +76,8 @@ class FixedGroups:
         self.voted = voted if voted is not None else torch.zeros(G, dtype=mt, device=self.device)
         self.granted = granted if granted is not None else torch.zeros(G, dtype=mt,
                                                                        device=self.device)
-        for t, w in ((self.match, "match"), (self.voted, "voted"), (self.granted, "granted")):
-            _require_device(t, w)
+        check_tensors(((self.match, "match", I64, n * G), (self.voted, "voted", (mt,), G),
+                       (self.granted, "granted", (mt,), G)))
 
     @classmethod
     def synth(cls, seed: int, n: int, G: int, g_begin: int = 0, device="cuda",
@@ -99,6 +99,7 @@ class FixedGroups:
             commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
         if want_vote and vote_out is None:
             vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _check_outs(self.G, commit_out if want_commit else None, vote_out if want_vote else None)
         _lib.call("qb_dev_fixed_committed_vote", self.n, self.G, _ptr(self.match),
                   _ptr(self.voted), _ptr(self.granted), _ptr(commit_out if want_commit else None),
                   _ptr(vote_out if want_vote else None), _stream(self.device))
@@ -226,8 +227,7 @@ class WideGroups:
 
     def __init__(self, off: torch.Tensor, match: torch.Tensor, flags: torch.Tensor,
                  max_slots: Optional[int] = None):
-        for t, w in ((off, "off"), (match, "match"), (flags, "flags")):
-            _require_device(t, w)
+        check_tensors(((off, "off", I32, 1), (match, "match", I64, 1), (flags, "flags", U8, 1)))
         self.off, self.match, self.flags = off, match, flags
         self.G = off.numel() - 1
         self.device = off.device
@@ -255,6 +255,7 @@ class WideGroups:
             commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
         if want_vote and vote_out is None:
             vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _check_outs(self.G, commit_out if want_commit else None, vote_out if want_vote else None)
         _lib.call("qb_dev_wide_committed_vote", self.G, self.max_slots, _ptr(self.off),
                   _ptr(self.match), _ptr(self.flags), _ptr(commit_out if want_commit else None),
                   _ptr(vote_out if want_vote else None), _stream(self.device))
@@ -276,10 +277,9 @@ class CsrGroups:
         self.votes = votes if votes is not None else torch.zeros(self.G, dtype=torch.int32,
                                                                  device=self.device)
         self.active = active
-        for t, w in ((off, "off"), (cfg, "cfg"), (match, "match"), (self.votes, "votes")):
-            _require_device(t, w)
-        if off.dtype != torch.int32 or cfg.dtype != torch.int32 or match.dtype != torch.int64:
-            raise TypeError("off/cfg must be int32 (uint32 bits), match int64 (uint64 bits)")
+        check_tensors(((off, "off", I32, self.G + 1), (cfg, "cfg", I32, self.G),
+                       (match, "match", I64, 1), (self.votes, "votes", I32, self.G),
+                       (active, "active", I16, self.G)))
 
     @classmethod
     def from_compiled(cls, cc: CompiledConfigs, match_u64: np.ndarray, votes_u32=None,
@@ -326,6 +326,7 @@ class CsrGroups:
             commit_out = torch.empty(self.G, dtype=torch.int64, device=self.device)
         if want_vote and vote_out is None:
             vote_out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
+        _check_outs(self.G, commit_out if want_commit else None, vote_out if want_vote else None)
         args = (self.G, self.max_slots, _ptr(self.off), _ptr(self.match), _ptr(self.cfg),
                 _ptr(self.votes), _ptr(commit_out if want_commit else None),
                 _ptr(vote_out if want_vote else None))
@@ -347,6 +348,7 @@ class CsrGroups:
         active = active if active is not None else self.active
         if active is None:
             raise ValueError("no RecentActive bits given")
+        check_tensors(((active, "active", I16, self.G), (self.cfg, "cfg", I32, self.G)))
         out = torch.empty(self.G, dtype=torch.uint8, device=self.device)
         _lib.call("qb_dev_csr_quorum_active", self.G, _ptr(self.cfg), _ptr(active), _ptr(out),
                   _stream(self.device))
@@ -376,6 +378,11 @@ class CsrGroups:
             decided_at = torch.empty(self.G, dtype=torch.int32, device=self.device)
         if stats is None:
             stats = torch.zeros(8, dtype=torch.int64, device=self.device)
+        batch.check()
+        check_tensors(((group_term, "group_term", I64, self.G),
+                       (stepdown_at, "stepdown_at", I32, self.G),
+                       (decided_at, "decided_at", I32, self.G),
+                       (stats, "stats", I64, len(_lib.QB_VSTAT_NAMES))))
         need = _lib.load().qb_votes_workspace_bytes(batch.M)
         ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         _lib.call("qb_dev_record_votes", _lib.QB_VOTE_MODE_PREVOTE if prevote else
@@ -409,6 +416,12 @@ class AppRespBatch:
     def M(self) -> int:
         return self.group.numel()
 
+    def check(self) -> None:
+        """Every column a contiguous device tensor of its dtype with M entries."""
+        M = self.M
+        check_tensors(((self.group, "batch.group", I32, 0), (self.flags, "batch.flags", U8, M),
+                       (self.index, "batch.index", I64, M), (self.term, "batch.term", I64, M)))
+
     @classmethod
     def from_numpy(cls, group, slot, index, term, reject=None, device="cuda"):
         dev = torch.device(device)
@@ -437,6 +450,7 @@ class FixedTracker:
 
     def apply_appresp(self, batch: AppRespBatch, reset_stats: bool = True):
         """stepLeader's MsgAppResp handling (quorum part) for a whole batch."""
+        batch.check()
         if reset_stats:
             self.stats.zero_()
         _lib.call("qb_dev_fixed_apply_appresp", self.n, self.G, batch.M, _ptr(batch.group),
@@ -446,6 +460,7 @@ class FixedTracker:
 
     def commit_advance(self, advanced_out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         """raft.maybeCommit for every group; returns the per-group advanced flags."""
+        check_tensors(((advanced_out, "advanced_out", FLAG, self.G),))
         _lib.call("qb_dev_fixed_commit_advance", self.n, self.G, _ptr(self.match),
                   _ptr(self.term_start), _ptr(self.committed), _ptr(advanced_out),
                   _stream(self.device))
@@ -462,6 +477,8 @@ class FixedTracker:
         so ``stepped_down()`` always describes this batch alone, as after
         ``apply_appresp``; ``rearm=False`` is the Go caller's protocol (it
         re-arms only the groups it stepped down; no per-group write per tick)."""
+        batch.check()
+        check_tensors(((advanced_out, "advanced_out", FLAG, self.G),))
         if reset_stats:
             self.stats.zero_()
         if rearm:
@@ -485,6 +502,8 @@ class FixedTracker:
         """First half of ``step`` (qb_dev_fixed_tracker_bucket): the batch sorted
         by group into ``ws``; touches no tracker state, so it may run on another
         stream while the previous batch is applied."""
+        batch.check()
+        check_tensors(((ws, "ws", U8, 1),))
         _lib.call("qb_dev_fixed_tracker_bucket", self.n, self.G, batch.M, _ptr(batch.group),
                   _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(ws), ws.numel(),
                   _stream(self.device) if stream is None else stream.cuda_stream)
@@ -493,6 +512,8 @@ class FixedTracker:
                        advanced_out: Optional[torch.Tensor] = None, stream=None):
         """Second half of ``step`` (qb_dev_fixed_tracker_apply) over a workspace
         that ``bucket`` filled for the same batch."""
+        batch.check()
+        check_tensors(((ws, "ws", U8, 1), (advanced_out, "advanced_out", FLAG, self.G)))
         _lib.call("qb_dev_fixed_tracker_apply", self.n, self.G, batch.M, _ptr(batch.group),
                   _ptr(batch.flags), _ptr(batch.index), _ptr(batch.term), _ptr(self.term),
                   _ptr(self.term_start), _ptr(self.match), _ptr(self.next), _ptr(self.active),
@@ -529,8 +550,7 @@ class CsrTracker:
 
     def __init__(self, off: torch.Tensor, cfg: torch.Tensor, max_slots: Optional[int] = None,
                  device="cuda", track_next: bool = False):
-        _require_device(off, "off")
-        _require_device(cfg, "cfg")
+        check_tensors(((off, "off", I32, cfg.numel() + 1), (cfg, "cfg", I32, 0)))
         self.off, self.cfg = off, cfg
         self.device = torch.device(device)
         self.G = cfg.numel()
@@ -568,6 +588,8 @@ class CsrTracker:
              reset_stats: bool = True, rearm: bool = True) -> Optional[torch.Tensor]:
         """One leader tick (qb_dev_csr_tracker_step); ``rearm`` as
         FixedTracker.step."""
+        batch.check()
+        check_tensors(((advanced_out, "advanced_out", FLAG, self.G),))
         if reset_stats:
             self.stats.zero_()
         if rearm:

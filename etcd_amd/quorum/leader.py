@@ -18,6 +18,7 @@ Array names and meanings (all numpy dtypes little-endian):
 from __future__ import annotations
 
 import ctypes as C
+import operator
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -25,6 +26,7 @@ import numpy as np
 import torch
 
 from .. import _lib
+from ._checks import I32, I64, U8, check_tensors
 
 MAX_RUNS = 8
 MAX_READQ = 16
@@ -115,6 +117,21 @@ class LeaderInbox:
     def M(self) -> int:
         return self._m
 
+    def check(self) -> None:
+        """Every column a contiguous device tensor of its dtype holding M
+        records (M = ``_m``, set by whoever filled the columns)."""
+        try:
+            M = operator.index(self._m)
+        except TypeError:
+            M = -1
+        if M < 0:
+            raise _lib.QuorumBatchError(f"inbox record count must be a non-negative int, "
+                                        f"got {self._m!r}")
+        check_tensors(((self.group, "inbox.group", I32, M), (self.flags, "inbox.flags", U8, M),
+                       (self.index, "inbox.index", I64, M), (self.term, "inbox.term", I64, M),
+                       (self.hint, "inbox.hint", I64, M),
+                       (self.log_term, "inbox.log_term", I64, M)))
+
     @classmethod
     def from_numpy(cls, group, slot, kind, index, term, reject=None, hint=None, log_term=None,
                    device="cuda"):
@@ -155,16 +172,24 @@ class LeaderGroups:
     def __init__(self, arrays: Dict[str, np.ndarray], inflight_cap: int, readq_cap: int = 0,
                  read_only: int = READ_ONLY_SAFE, device="cuda"):
         self.device = torch.device(device)
+        self.G = len(arrays["cfg"])
+        self.S = int(arrays["off"][-1]) if len(arrays["off"]) else 0
+        self.inflight_cap, self.readq_cap, self.read_only = inflight_cap, readq_cap, read_only
+        need = self._lengths()
+        for k in GROUP_ARRAYS:
+            if k not in arrays:
+                raise _lib.QuorumBatchError(f"leader state array {k!r} missing")
+            if np.asarray(arrays[k]).size < need[k]:
+                raise _lib.QuorumBatchError(f"leader state array {k!r} holds "
+                                            f"{np.asarray(arrays[k]).size} entries, < {need[k]}")
         if not self.device.type == "cuda":
             raise _lib.QuorumBatchError("LeaderGroups needs a HIP device; there is no CPU path")
-        self.G = len(arrays["cfg"])
-        self.S = int(arrays["off"][-1])
-        self.inflight_cap, self.readq_cap, self.read_only = inflight_cap, readq_cap, read_only
         self.t = {k: _to_dev(arrays[k], dt, self.device) for k, dt in GROUP_ARRAYS.items()}
         self._ws = None
 
-    def numpy(self) -> Dict[str, np.ndarray]:
-        n = {"off": self.G + 1, "cfg": self.G, "meta": self.G, "term": self.G,
+    def _lengths(self) -> Dict[str, int]:
+        """Entries per state array (include/quorum_batch.h qb_leader_groups)."""
+        return {"off": self.G + 1, "cfg": self.G, "meta": self.G, "term": self.G,
              "committed": self.G, "first_index": self.G, "last_index": self.G,
              "snap_index": self.G, "snap_term": self.G, "max_ents": self.G,
              "run_start": self.G * MAX_RUNS, "run_term": self.G * MAX_RUNS,
@@ -172,6 +197,9 @@ class LeaderGroups:
              "infl_pos": self.S, "infl_buf": self.S * self.inflight_cap,
              "rq_ctx": self.G * self.readq_cap, "rq_index": self.G * self.readq_cap,
              "rq_meta": self.G * self.readq_cap}
+
+    def numpy(self) -> Dict[str, np.ndarray]:
+        n = self._lengths()
         return {k: _to_np(self.t[k], dt, n[k]) for k, dt in GROUP_ARRAYS.items()}
 
     def _struct(self) -> LeaderGroupsC:
@@ -185,6 +213,8 @@ class LeaderGroups:
              stats: Optional[torch.Tensor] = None, fetch: bool = True):
         """One batch through qb_dev_leader_step.  Returns a LeaderStepResult
         (host copies) when fetch, else the device outputs."""
+        inbox.check()
+        check_tensors(((stats, "stats", I64, len(LSTAT_NAMES)),))
         lib = _lib.load()
         M = inbox.M
         dev = self.device
@@ -227,6 +257,8 @@ class LeaderGroups:
         LeaderStepResult with the outbox read back into group order on the
         host (msg_total = messages stored); else the device outbox dict and
         stats."""
+        inbox.check()
+        check_tensors(((stats, "stats", I64, len(LSTAT_NAMES)),))
         lib = _lib.load()
         M, G, dev = inbox.M, self.G, self.device
         need = lib.qb_leader_outbox_workspace_bytes(G, M)

@@ -8,6 +8,7 @@ import numpy as np
 import torch
 
 from .. import _lib
+from ._checks import check_tensors as _check_tensors
 from .leader import LeaderInbox
 
 WIRE_OK, WIRE_UNMARSHAL, WIRE_TYPE, WIRE_CTX = 0, 1, 2, 3
@@ -34,26 +35,6 @@ def group_rows(off: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     _lib.call("qb_dev_wire_group_rows", G, off.data_ptr(), ids.data_ptr(), rows.data_ptr(),
               torch.cuda.current_stream(off.device).cuda_stream)
     return rows
-
-
-def _check_tensors(specs):
-    """(tensor, name, dtypes, min elements) each: a contiguous device tensor of
-    one of dtypes and at least that many elements (None: optional, skipped);
-    all on one device.  The C ABI takes plain pointers, so a short or
-    mistyped tensor here would be read past its end on the device."""
-    dev = None
-    for t, what, dts, n_min in specs:
-        if t is None:
-            continue
-        if not isinstance(t, torch.Tensor) or not t.is_cuda:
-            raise _lib.QuorumBatchError(f"{what} must be a device tensor; there is no CPU path")
-        if t.dtype not in dts or not t.is_contiguous() or t.numel() < n_min:
-            raise _lib.QuorumBatchError(f"{what} must be a contiguous {dts[0]} device tensor of "
-                                        f">= {n_min} elements")
-        if dev is None:
-            dev = t.device
-        elif t.device != dev:
-            raise _lib.QuorumBatchError(f"{what} is on {t.device}, the batch on {dev}")
 
 
 def _check_batch(buf, nbytes, msg_off, msg_group):

@@ -137,6 +137,9 @@ def _device_columns(cols: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     M = cols["group"].numel()
     out = {}
     for name, col in cols.items():
+        if col.device != cols["group"].device:
+            raise ValueError(f"route_partition: column {name!r} is on {col.device}, group on "
+                             f"{cols['group'].device}")
         if col.dim() != 1 or col.numel() != M:
             raise ValueError(f"route_partition: column {name!r} must be 1-D of length {M}")
         if name == "group":
@@ -191,6 +194,8 @@ def compact_changed(changed: torch.Tensor, commit: torch.Tensor, g_base: int = 0
     host tensors the same compaction in torch."""
     if changed.numel() != commit.numel():
         raise ValueError("changed and commit differ in length")
+    if changed.device != commit.device:
+        raise ValueError(f"changed is on {changed.device}, commit on {commit.device}")
     if changed.dtype not in (torch.uint8, torch.bool):
         raise ValueError(f"changed must be uint8/bool, not {changed.dtype}")
     if commit.dtype not in _WIDE:

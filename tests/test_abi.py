@@ -281,3 +281,46 @@ def test_leader_outbox_binding_layout_matches_header(tmp_path):
                                           text=True).stdout.split()]
     assert got == [C.sizeof(LeaderOutboxC), LeaderOutboxC.read_states.offset,
                    LeaderOutboxC.read_count.offset, READ_STATE_DTYPE.itemsize]
+
+
+def test_leader_state_arrays_checked_before_any_device_work():
+    """LeaderGroups refuses a state table with a missing or short array (the
+    C ABI would read past it on the device) before it touches a device."""
+    import numpy as np
+    from etcd_amd.quorum import leader
+    G, n, K = 4, 3, 4
+    arrays = {k: np.zeros(1, dt) for k, dt in leader.GROUP_ARRAYS.items()}
+    arrays["off"] = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    arrays["cfg"] = np.zeros(G, np.uint32)
+    for k in ("meta", "term", "committed", "first_index", "last_index", "snap_index",
+              "snap_term", "max_ents"):
+        arrays[k] = np.zeros(G, leader.GROUP_ARRAYS[k])
+    for k in ("run_start", "run_term"):
+        arrays[k] = np.zeros(G * leader.MAX_RUNS, np.uint64)
+    for k in ("match", "next", "pending_snapshot", "pstate", "infl_pos"):
+        arrays[k] = np.zeros(n * G, leader.GROUP_ARRAYS[k])
+    arrays["infl_buf"] = np.zeros(n * G * K, np.uint64)
+    # complete: only the device is refused
+    with pytest.raises(_lib.QuorumBatchError, match="HIP device"):
+        leader.LeaderGroups(arrays, K, device="cpu")
+    short = dict(arrays, infl_buf=np.zeros(n * G * K - 1, np.uint64))
+    with pytest.raises(_lib.QuorumBatchError, match="infl_buf"):
+        leader.LeaderGroups(short, K, device="cpu")
+    with pytest.raises(_lib.QuorumBatchError, match="rq_ctx"):
+        leader.LeaderGroups(arrays, K, readq_cap=2, device="cpu")
+    missing = {k: v for k, v in arrays.items() if k != "match"}
+    with pytest.raises(_lib.QuorumBatchError, match="match"):
+        leader.LeaderGroups(missing, K, device="cpu")
+
+
+def test_tensor_checks_refuse_host_tensors_and_bad_counts():
+    import torch
+    from etcd_amd.quorum import _checks, leader
+    with pytest.raises(_lib.QuorumBatchError, match="device tensor"):
+        _checks.check_tensors(((torch.zeros(4, dtype=torch.int64), "x", _checks.I64, 4),))
+    _checks.check_tensors(((None, "omitted", _checks.I64, 4),))
+    z = torch.zeros(1)
+    ib = leader.LeaderInbox(z, z, z, z, z, z)
+    ib._m = -1
+    with pytest.raises(_lib.QuorumBatchError, match="non-negative"):
+        ib.check()
