@@ -1,6 +1,7 @@
 // qb_wire_tracker.hip — the composed per-tick path in one pipeline: raw
 // raftpb.Message bytes of a tick's responses -> the leader's ProgressTracker
-// (FIXED layout) stepped and the commit advanced, without the decoded record
+// (FIXED layout, or CSR: qb_dev_ingest_csr_tracker_step, K5 as the CSR step)
+// stepped and the commit advanced, without the decoded record
 // columns between the two (VERDICT r5 "next" item 2).
 //
 // Reference path (paths relative to the reference's root):
@@ -13,11 +14,13 @@
 //
 // Pipeline (one call of qb_dev_ingest_fixed_tracker_step):
 //   memset           stat shards, flag words, region fills, chunk flags
-//   K3w k_wire_scatter  per tile of 4096 messages (1024 threads, 4 per
-//                    thread): each wave stages its 64 messages' bytes into
-//                    its own LDS slice (LDS-DMA, no block barrier), decodes
-//                    them with the ingest's fast prefix, looks From up in the
-//                    group row, writes the status byte, and the tile's
+//   K3w k_wire_scatter  per tile of 2048 messages (512 threads, one message
+//                    per thread in each of 4 sub-rounds; two workgroups per
+//                    CU): each wave stages its 64 messages' bytes into its
+//                    own LDS slice (LDS-DMA, double-buffered across
+//                    sub-rounds, no block barrier), decodes them with the
+//                    ingest's fast prefix, looks From up in the group row,
+//                    writes the status bytes after the last sub-round, and the tile's
 //                    records go straight into the reserved regions as K3 of
 //                    the tracker step writes them (compact 8-byte records,
 //                    chunk-low bytes, side column) — the ingest's record
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(kWtThreads) void k_wire_scatter(
   u8* slice = reinterpret_cast<u8*>(&L) + w * kSlice;
   BlockTally<4> wtally;  // OK, UNMARSHAL, TYPE, CTX
   u32 nbad = 0, nnon = 0, nside = 0;
-  // per record (message t0 + r * 1024 + threadIdx.x): bin | chunk-low << 16
+  // per record (message t0 + r * kWtThreads + threadIdx.x): bin | chunk-low << 16
   // (kNoBin: none), its rank in the bin, the encoded record, a side term
   u32 bj[kPer], rj[kPer], tj[kPer];
   u64 vj[kPer];
