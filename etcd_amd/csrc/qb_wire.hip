@@ -85,7 +85,9 @@ __global__ __launch_bounds__(kBlock) void k_ingest(Args A) {
     // Pieces wholly inside the byte buffer go by LDS-DMA, all issued before
     // the barrier's one wait; only the buffer's last piece can be partial.
     // (A byte buffer that is not 16-byte aligned stages with plain loads.)
-    const u64 whole = (A.nbytes - a0) / 16;
+    // (offsets past the buffer — a caller error the decode reports as
+    // UNMARSHAL — stage nothing from it)
+    const u64 whole = a0 < A.nbytes ? (A.nbytes - a0) / 16 : 0;
     u32 nfull = u32(n16 < whole ? n16 : whole);
     if ((reinterpret_cast<uintptr_t>(A.bytes) & 15u) == 0) {
       constexpr int kIt = int((kStage + 16) / 16 / kBlock) + 1;

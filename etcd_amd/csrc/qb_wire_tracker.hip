@@ -110,7 +110,7 @@ __device__ __forceinline__ void stage_span(u8* slice, const WireArgs& W, u32 nre
   const u64 a0 = b0 & ~u64(15);
   const u64 a1 = (b1 + 15) & ~u64(15);
   const u32 n16 = u32((a1 - a0) / 16);
-  const u64 whole = (W.nbytes - a0) / 16;
+  const u64 whole = a0 < W.nbytes ? (W.nbytes - a0) / 16 : 0;  // (offsets past the buffer: none)
   const u32 nfull = u32(n16 < whole ? n16 : whole);
   if ((reinterpret_cast<uintptr_t>(W.bytes) & 15u) == 0) {
 #pragma unroll

@@ -289,9 +289,10 @@ def leader_step(arrays, inflight_cap, readq_cap, read_only, rec, threads=1, msg_
     return msgs[:min(total, msg_cap)], int(total), sd, gf, stats
 
 
-def ingest(buf, moff, mgroup, off, ids, threads=1):
+def ingest(buf, moff, mgroup, off, ids, threads=1, nbytes=None):
     """Wire ingest restated (oracle/wire_oracle.c): returns dict of record
-    columns + status."""
+    columns + status.  nbytes: the buffer's length (default the last offset;
+    given when the offsets are corrupt and may point past it)."""
     lib = load()
     M = len(mgroup)
     out = {"group": np.empty(M, np.uint32), "flags": np.empty(M, np.uint8),
@@ -299,7 +300,9 @@ def ingest(buf, moff, mgroup, off, ids, threads=1):
            "hint": np.empty(M, np.uint64), "log_term": np.empty(M, np.uint64),
            "status": np.empty(M, np.uint8)}
     b = buf if buf.size else np.zeros(1, np.uint8)
-    lib.orc_ingest(M, ptr(b), int(moff[-1]), ptr(moff), ptr(mgroup), len(off) - 1, ptr(off),
+    nb = int(moff[-1]) if nbytes is None else int(nbytes)
+    assert nb <= buf.size or nb == 0, "nbytes past the host buffer"
+    lib.orc_ingest(M, ptr(b), nb, ptr(moff), ptr(mgroup), len(off) - 1, ptr(off),
                    ptr(ids if ids.size else np.zeros(1, np.uint64)), ptr(out["group"]),
                    ptr(out["flags"]), ptr(out["index"]), ptr(out["term"]), ptr(out["hint"]),
                    ptr(out["log_term"]), ptr(out["status"]), threads)

@@ -27,7 +27,7 @@ def _u64(t):
 
 def _chain_oracle(n, G, buf, moff, grp, off, ids, st):
     """C decode, the fused contract on its records, the sequential tracker."""
-    want = oc.ingest(buf, moff, grp, off, ids, threads=8)
+    want = oc.ingest(buf, moff, grp, off, ids, threads=8, nbytes=buf.size)
     g = want["group"].copy()
     f = want["flags"].copy()
     notrec = (want["status"] != 0) | (((f >> 4) & 3) != 0)
@@ -364,3 +364,54 @@ def test_fused_unaligned_buffer_and_input_checks():
     for i, call in enumerate(bad):
         with pytest.raises(_lib.QuorumBatchError):
             call()
+
+
+def test_corrupt_offsets_ingest_and_fused():
+    """msg_off from a broken caller: an end before its start, a last offset
+    past the buffer and an aligned block of 257 offsets far past it (whole
+    waves and ingest workgroups whose staged span starts beyond the buffer:
+    nothing may be staged from there).  Both the ingest and the composed call
+    report what the restated Unmarshal does (UNMARSHAL for a slice outside
+    the buffer), and the tracker steps what is left."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(21)
+    G, n = 1 << 11, 5
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (11 + np.arange(n * G, dtype=np.uint64) * 7)
+    dev = torch.device("cuda")
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    rows = wire.group_rows(d_off, d_ids)
+    msgs, grps = [], []
+    for _ in range(4 * G):
+        g = r.randrange(G)
+        s = r.randrange(n)
+        msgs.append(W.marshal_message(4, int(ids[n * g]), int(ids[n * g + s]), 4, 0,
+                                      30 + r.randrange(500), (), 0, W.EMPTY_SNAPSHOT,
+                                      r.random() < 0.1, 0))
+        grps.append(g)
+    buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+    h = _u64(moff).copy()
+    M = len(msgs)
+    for i in (5, 900, 3001):  # message i - 1 spans two messages, message i ends before it starts
+        h[i], h[i + 1] = h[i + 1], h[i]
+    h[M] = nbytes + 1000  # the last message ends past the buffer
+    h[1024:1024 + 257] = nbytes + (1 << 20) + np.arange(257, dtype=np.uint64) * 40
+    moff = torch.from_numpy(h.view(np.int64)).to(dev)
+    ib, status, _ = wire.ingest(buf, nbytes, moff, grp, d_off, d_ids, rows=rows)
+    want = oc.ingest(buf.cpu().numpy()[:nbytes], h, grp.cpu().numpy().view(np.uint32), off, ids,
+                     threads=8, nbytes=nbytes)
+    got = status.cpu().numpy()
+    assert np.array_equal(got, want["status"])
+    assert (got[1024:1024 + 257] == wire.WIRE_UNMARSHAL).all() and got[M - 1] == wire.WIRE_UNMARSHAL
+    assert np.array_equal(ib.group.cpu().numpy().view(np.uint32)[:M], want["group"])
+    tr = batch.FixedTracker(n, G, dev)
+    tr.term.fill_(4)
+    tr.term_start.fill_(20)
+    st = _host_state(tr, G)
+    status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows)
+    want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], h,
+                                            grp.cpu().numpy().view(np.uint32), off, ids, st)
+    assert np.array_equal(status.cpu().numpy(), want_status)
+    _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
