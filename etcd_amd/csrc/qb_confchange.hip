@@ -392,10 +392,30 @@ constexpr u8 kCodeAppended = 0x10, kCodeFresh = 0x20, kCodeNone = 0xFF;
 // and leaves markers, as round 4 did for every group).
 constexpr u64 kBigCode = 0xFEull << 56;
 
+// A group whose current config has more slots than the working table (only
+// possible for an input this engine did not produce: past QB_MAX_SLOTS
+// members) is never replayed — its table would overrun the LDS block — and
+// keeps its config as it is: no operation copies it through, any other is
+// refused with the engine limit's error.
+__device__ __forceinline__ u32 oversize_slots(const Args& A, u64 g) {
+  const u32 ns = A.off[g + 1] - A.off[g];
+  return ns > u32(kTab) ? ns : 0u;
+}
+
 template <int TAB, bool BIG>
 __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
   __shared__ u64 tabs[TAB][kBlk];
   for_my_groups<BIG>(A, [&](u64 g) {
+    if constexpr (BIG) {
+      if (const u32 ns = oversize_slots(A, g)) {
+        const int rc = A.op[g] == QB_CC_NONE ? 0 : QB_CCERR_TOO_MANY_SLOTS;
+        A.new_cnt[g] = ns;
+        A.err[g] = u8(rc);
+        if (A.err_id) A.err_id[g] = 0;
+        A.codes[g] = kBigCode | ns;
+        return;
+      }
+    }
     Tab t = tab_of(tabs);
     Roles r;
     bool al;
@@ -433,6 +453,20 @@ __global__ __launch_bounds__(kBlk) void k_cc_count(Args A) {
 // the usual batch): the write pass replays the change again.
 template <int TAB>
 __device__ void write_group(const Args& A, u64 g, u64 (*tabs)[kBlk]) {
+  if (const u32 ns = oversize_slots(A, g)) {  // kept in slot order, every Progress carried
+    const u32 s0 = A.off[g];
+    const u64 d0 = u64(A.new_cnt[g]) + A.nbsum[g / scan::kScanPer];
+    A.new_cnt[g] = u32(d0);
+    if (d0 + ns > A.S_cap) return;
+    for (u32 j = 0; j < ns; ++j) {
+      A.n_ids[d0 + j] = A.ids[s0 + j];
+      A.n_pstate[d0 + j] = kCarried;
+      A.n_infl_pos[d0 + j] = s0 + j;
+    }
+    A.n_cfg[g] = A.cfg[g];
+    A.n_ext[g] = A.ext ? A.ext[g] & 0x1FFFFu : 0u;
+    return;
+  }
   Tab t = tab_of(tabs);
   Roles r;
   bool al;

@@ -772,7 +772,9 @@ enum {
   QB_CCERR_LEARNER_INCOMING = 12,   /* "%d is in Learners and Voters[0]"                */
   QB_CCERR_LEARNER_NOT_MARKED = 13, /* "%d is in Learners, but is not marked as learner" */
   QB_CCERR_AUTOLEAVE_NOT_JOINT = 14, /* "AutoLeave must be false when not joint"        */
-  QB_CCERR_TOO_MANY_SLOTS = 15,     /* engine limit: > QB_MAX_SLOTS members, or > 24 IDs alive at once within one change list */
+  QB_CCERR_TOO_MANY_SLOTS = 15,     /* engine limit: > QB_MAX_SLOTS members, or > 24 IDs alive at once within one change list
+                                       (a current config of > 24 slots is kept as it is, and
+                                       copied through under QB_CC_NONE) */
   QB_CCERR_BAD_OP = 16              /* op is not a QB_CC_* operation                     */
 };
 

@@ -368,26 +368,32 @@ def test_ring16_unaligned_buffers_take_the_word_loop():
     _check_rings(got, rings, K)
 
 
-def test_wide_wave_owner_lookup():
+@pytest.mark.parametrize("learners", [15, 25, 40])
+def test_wide_wave_owner_lookup(learners):
     """a wave of 64 groups whose slots exceed k_cc_move's owner
-    table (64 x QB_MAX_SLOTS): groups of 20 slots (5 voters, 15 learners) kept
-    as they are (no operation) and refused (a learner more breaks the engine's
+    table (64 x QB_MAX_SLOTS): groups of 5 voters and 15 learners kept as they
+    are (no operation) and refused (a learner more breaks the engine's
     16-member limit: the old slots stay) — every slot found by the binary
-    search and moved exactly, rings included."""
+    search and moved exactly, rings included.  With 25 and 40 learners the
+    groups exceed the replay's 24-entry working table too (and 40 the 32-bit
+    role masks): they are never replayed, copied through or refused the same
+    way."""
     K = 3
     G = 256
+    ns = 5 + learners
 
     def tracker(g):
         prs = {i: CC.Pr(match=0, next=10 + g, inflight_size=K) for i in range(1, 6)}
         prs.update({i: CC.Pr(match=0, next=20 + g, is_learner=True, inflight_size=K)
-                    for i in range(100, 115)})
-        return CC.Tracker(set(range(1, 6)), None, set(range(100, 115)), None, False, prs, K)
+                    for i in range(100, 100 + learners)})
+        return CC.Tracker(set(range(1, 6)), None, set(range(100, 100 + learners)), None, False,
+                          prs, K)
     import torch
     orc = [tracker(g) for g in range(G)]
     table, rings = _ring_marks(_table(orc, K=K), K)
     before = table.numpy()
     dev = table.t["off"].device
-    cap = 20 * G + 8   # (the default capacity assumes <= 16 slots per group)
+    cap = ns * G + 8   # (the default capacity assumes <= 16 slots per group)
     for op, ccs in ((0, []), (1, [(CC.ADD_LEARNER, 200)])):
         o = {"new_off": torch.zeros(G + 1, dtype=torch.int32, device=dev),
              "cfg": torch.empty(G, dtype=torch.int32, device=dev),
@@ -401,7 +407,7 @@ def test_wide_wave_owner_lookup():
             o[k] = torch.empty(cap, dtype=torch.int64, device=dev)
         got, err, _ = table.change([op] * G, [ccs] * G, [50] * G, out=o)
         a = got.numpy()
-        assert int(a["off"][-1]) == 20 * G
+        assert int(a["off"][-1]) == ns * G
         assert (err == (15 if op else 0)).all()
         for k in ("off", "ids", "cfg", "match", "next", "pstate"):
             assert np.array_equal(a[k], before[k]), (op, k)
