@@ -182,6 +182,16 @@ class LeaderGroups:
             if np.asarray(arrays[k]).size < need[k]:
                 raise _lib.QuorumBatchError(f"leader state array {k!r} holds "
                                             f"{np.asarray(arrays[k]).size} entries, < {need[k]}")
+        if not 1 <= inflight_cap <= 4096:
+            raise _lib.QuorumBatchError(f"inflight_cap must be 1..4096, got {inflight_cap}")
+        # the rings' invariant (start < cap, count <= cap): the step indexes a
+        # slot's ring by it without a check (include/quorum_batch.h)
+        ip = np.asarray(arrays["infl_pos"]).astype(np.uint32)[: self.S]
+        bad = ((ip & 0xFFFF) >= inflight_cap) | ((ip >> 16) > inflight_cap)
+        if bad.any():
+            j = int(np.argmax(bad))
+            raise _lib.QuorumBatchError(f"infl_pos[{j}] = {int(ip[j]):#x} breaks the ring invariant "
+                                        f"(start < {inflight_cap}, count <= {inflight_cap})")
         if not self.device.type == "cuda":
             raise _lib.QuorumBatchError("LeaderGroups needs a HIP device; there is no CPU path")
         self.t = {k: _to_dev(arrays[k], dt, self.device) for k, dt in GROUP_ARRAYS.items()}

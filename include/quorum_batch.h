@@ -537,7 +537,9 @@ typedef struct qb_leader_groups {
   uint64_t* next;
   uint64_t* pending_snapshot;
   uint8_t* pstate;       /* QB_PR_* */
-  uint32_t* infl_pos;    /* start | count << 16 */
+  uint32_t* infl_pos;    /* start | count << 16; start < inflight_cap, count <=
+                            inflight_cap (the ring's invariant, not checked here:
+                            etcd_amd/quorum/leader.py checks it on the host) */
   uint64_t* infl_buf;    /* [S * inflight_cap] ring */
   /* pending ReadIndex queue, oldest first: [G * readq_cap] (in/out) */
   uint64_t* rq_ctx;

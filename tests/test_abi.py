@@ -308,6 +308,16 @@ def test_leader_state_arrays_checked_before_any_device_work():
         leader.LeaderGroups(short, K, device="cpu")
     with pytest.raises(_lib.QuorumBatchError, match="rq_ctx"):
         leader.LeaderGroups(arrays, K, readq_cap=2, device="cpu")
+    ring = dict(arrays, infl_pos=np.full(n * G, K << 16, np.uint32))  # full rings: valid
+    with pytest.raises(_lib.QuorumBatchError, match="HIP device"):
+        leader.LeaderGroups(ring, K, device="cpu")
+    for bad in (K, (K + 1) << 16):  # start past the ring, count past it
+        ring["infl_pos"] = np.zeros(n * G, np.uint32)
+        ring["infl_pos"][7] = bad
+        with pytest.raises(_lib.QuorumBatchError, match=r"infl_pos\[7\]"):
+            leader.LeaderGroups(ring, K, device="cpu")
+    with pytest.raises(_lib.QuorumBatchError, match="inflight_cap"):
+        leader.LeaderGroups(arrays, 0, device="cpu")
     missing = {k: v for k, v in arrays.items() if k != "match"}
     with pytest.raises(_lib.QuorumBatchError, match="match"):
         leader.LeaderGroups(missing, K, device="cpu")
