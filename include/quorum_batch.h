@@ -643,7 +643,10 @@ int qb_dev_leader_step_outbox(const qb_leader_groups* lg, const qb_leader_inbox*
  * big-endian request id, which becomes rec_index); any other status leaves
  * rec_group = UINT32_MAX (dropped by the step as a bad group).
  * msg_type (nullable) receives the low byte of Message.Type;
- * stats (nullable, 4 device uint64, accumulated) counts each status. */
+ * stats (nullable, 4 device uint64, accumulated) counts each status.
+ * A message whose slice is not inside the buffer (msg_off[i+1] < msg_off[i]
+ * or msg_off[i+1] > nbytes: a caller error — Go would panic slicing it) gets
+ * QB_WIRE_UNMARSHAL; nothing outside [bytes, bytes + nbytes) is read. */
 #define QB_WIRE_OK 0
 #define QB_WIRE_UNMARSHAL 1 /* Message.Unmarshal returns an error           */
 #define QB_WIRE_TYPE 2      /* not a leader-inbox response type             */
