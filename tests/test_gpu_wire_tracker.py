@@ -418,3 +418,46 @@ def test_corrupt_offsets_ingest_and_fused():
                                             grp.cpu().numpy().view(np.uint32), off, ids, st)
     assert np.array_equal(status.cpu().numpy(), want_status)
     _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+
+
+@pytest.mark.parametrize("all_empty", [True, False])
+def test_empty_messages_ingest_and_fused(all_empty):
+    """Zero-length messages (an empty slice unmarshals to a default Message:
+    type MsgHup, not a response) — every message empty with no bytes at all,
+    or one in three empty between real responses — through the ingest and
+    the composed call, against the C oracle."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(31 + all_empty)
+    G, n = 1 << 10, 5
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (3 + np.arange(n * G, dtype=np.uint64) * 2)
+    dev = torch.device("cuda")
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    rows = wire.group_rows(d_off, d_ids)
+    msgs, grps = [], []
+    for i in range(3 * G + 5):
+        g = r.randrange(G)
+        if all_empty or i % 3 == 0:
+            msgs.append(b"")
+        else:
+            msgs.append(W.marshal_message(4, int(ids[n * g]), int(ids[n * g + r.randrange(n)]), 2,
+                                          0, 10 + r.randrange(100), (), 0, W.EMPTY_SNAPSHOT,
+                                          False, 0))
+        grps.append(g)
+    buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+    h_moff, h_grp = _u64(moff), grp.cpu().numpy().view(np.uint32)
+    want = oc.ingest(buf.cpu().numpy()[:nbytes], h_moff, h_grp, off, ids, threads=8, nbytes=nbytes)
+    _, status, _ = wire.ingest(buf, nbytes, moff, grp, d_off, d_ids, rows=rows)
+    assert np.array_equal(status.cpu().numpy(), want["status"])
+    assert (want["status"][[i for i, m in enumerate(msgs) if not m]] == wire.WIRE_TYPE).all()
+    tr = batch.FixedTracker(n, G, dev)
+    tr.term.fill_(2)
+    tr.term_start.fill_(5)
+    st = _host_state(tr, G)
+    status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows)
+    want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], h_moff, h_grp, off,
+                                            ids, st)
+    assert np.array_equal(status.cpu().numpy(), want_status)
+    _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
