@@ -138,6 +138,14 @@ def test_fuzz_terms_past_32_bits():
     _fuzz(51, G=3000, M=9000, inflight_cap=6, readq_cap=3, term_base=(1 << 32) - 25)
 
 
+@pytest.mark.parametrize("cap", [1, 2, 600])
+def test_fuzz_ring_capacities(cap):
+    """MaxInflightMsgs at its small end (a one-entry ring: full after every
+    send) and far past the others (600), both output forms."""
+    _fuzz(60 + cap, G=200, M=900, inflight_cap=cap, readq_cap=2)
+    _fuzz(70 + cap, G=200, M=900, inflight_cap=cap, readq_cap=2, outbox=True)
+
+
 def test_fuzz_larger():
     _fuzz(21, G=5000, M=12000, inflight_cap=8, readq_cap=4)
 
