@@ -461,3 +461,40 @@ def test_empty_messages_ingest_and_fused(all_empty):
                                             ids, st)
     assert np.array_equal(status.cpu().numpy(), want_status)
     _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+
+
+@pytest.mark.parametrize("G", [1, 64])
+def test_fused_few_groups_many_records(G):
+    """A tick of 2^16 responses over one group or 64: one super-bucket takes
+    every record (its regions run past their reserved cap into the pool when
+    they fill) and K4 folds a thousand or more records per group — the
+    composed call against the C chain."""
+    import torch
+    from etcd_amd.quorum import batch, wire
+    r = random.Random(41 + G)
+    n = 5
+    off = np.arange(0, n * G + 1, n, dtype=np.uint32)
+    ids = (9 + np.arange(n * G, dtype=np.uint64) * 4)
+    dev = torch.device("cuda")
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+    rows = wire.group_rows(d_off, d_ids)
+    msgs, grps = [], []
+    for _ in range(1 << 16):
+        g = r.randrange(G)
+        msgs.append(W.marshal_message(4, int(ids[n * g]), int(ids[n * g + r.randrange(n)]),
+                                      6 if r.random() < 0.98 else 5, 0, 100 + r.randrange(5000), (),
+                                      0, W.EMPTY_SNAPSHOT, r.random() < 0.05, 0))
+        grps.append(g)
+    buf, nbytes, moff, grp = wire.pack_messages(msgs, grps, device=dev)
+    tr = batch.FixedTracker(n, G, dev)
+    tr.term.fill_(6)
+    tr.term_start.fill_(50)
+    st = _host_state(tr, G)
+    wst = torch.zeros(4, dtype=torch.int64, device=dev)
+    status = wire.ingest_tracker_step(tr, buf, nbytes, moff, grp, rows=rows, wire_stats=wst)
+    want_status, want_stats = _chain_oracle(n, G, buf.cpu().numpy()[:nbytes], _u64(moff),
+                                            grp.cpu().numpy().view(np.uint32), off, ids, st)
+    assert np.array_equal(status.cpu().numpy(), want_status)
+    _check(tr, G, st, tr.stats.cpu().numpy(), want_stats)
+    assert int(wst[0].item()) == len(msgs)
