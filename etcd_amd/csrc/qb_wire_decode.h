@@ -511,8 +511,16 @@ __device__ __forceinline__ Decoded decode_one(const RowArgs& A, u64 nbytes, cons
 #pragma unroll
     for (u32 k = kIdBatch; k-- > 0;)
       if (k < n && k < held && row.id[k] == f.from) slot = k;
-    for (u32 j = row.s0 + held; j < row.s1 && slot == QB_REC_NO_PROGRESS; ++j)
-      if (A.ids[j] == f.from) slot = j - row.s0;
+    // members past the row: four IDs per round trip (a ragged config's
+    // 8th-11th slots in one; loads clamped to the group's last slot)
+    for (u32 j = row.s0 + held; j < row.s1 && slot == QB_REC_NO_PROGRESS; j += 4) {
+      u64 v[4];
+#pragma unroll
+      for (u32 q = 0; q < 4; ++q) v[q] = A.ids[j + q < row.s1 ? j + q : row.s1 - 1];
+#pragma unroll
+      for (u32 q = 4; q-- > 0;)
+        if (j + q < row.s1 && v[q] == f.from) slot = j + q - row.s0;
+    }
   }
   d.flags = u8(slot | (u32(kind) << 4) | (f.reject ? QB_REC_REJECT : 0u));
   d.index = index;
